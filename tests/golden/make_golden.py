@@ -1,0 +1,430 @@
+"""Generate the golden fixtures under tests/golden/ by RUNNING THE REFERENCE.
+
+Test infrastructure (survey container only -- /root/reference does not exist on the
+GPU box).  Imports the reference's own model.py / nn.py / utils.py / optim.py /
+trainer/__init__.py from /root/reference (read-only, PYTHONDONTWRITEBYTECODE) in a
+scratch cwd (model.py:209-214 writes '<spk>.txt' there; we pre-create them so the
+reference neither prints nor writes), feeds it weights/inputs from recipe.py and
+writes inputs + outputs as .npz fixtures.  Nothing of the reference's source is
+copied; only its outputs are stored.
+
+Known reference defects worked around by composition, not by editing it:
+  * Predictor only runs at B=1 (model.py:209 `reshape(1)` of spk): batch goldens
+    run one reference Predictor per row sharing one SampleRNN (rows independent).
+  * torch>=2 `zero_grad()` sets grads to None and gradient_clipping
+    (optim.py:11-13) then crashes on h0: zero_grad(set_to_none=False) restores
+    the torch-0.4 semantics the reference was written for.
+
+Usage:  python tests/golden/make_golden.py [--skip-exhaustive]
+"""
+import argparse
+import glob
+import os
+import sys
+import tempfile
+import time
+import warnings
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import recipe  # noqa: E402
+
+REF = '/root/reference'
+
+
+def _import_reference():
+    sys.dont_write_bytecode = True
+    os.environ['PYTHONDONTWRITEBYTECODE'] = '1'
+    scratch = tempfile.mkdtemp(prefix='srnn_golden_')
+    os.chdir(scratch)
+    for i in range(16):
+        open('%d.txt' % i, 'w').close()
+    sys.path.insert(0, REF)
+    warnings.filterwarnings('ignore')
+    import torch
+    import model as ref_model
+    import nn as ref_nn
+    import utils as ref_utils
+    import optim as ref_optim
+    import trainer as ref_trainer
+    return torch, ref_model, ref_nn, ref_utils, ref_optim, ref_trainer
+
+
+torch, ref_model, ref_nn, ref_utils, ref_optim, ref_trainer = _import_reference()
+torch.set_num_threads(8)
+
+
+def save(name, **arrays):
+    path = os.path.join(HERE, name + '.npz')
+    np.savez_compressed(path, **arrays)
+    print('wrote', path, '%.1f KB' % (os.path.getsize(path) / 1024.0))
+
+
+# --------------------------------------------------------------------------- µ-law
+def ordered_f32(lo_bits, hi_bits, sign):
+    """float32 values for the given bit range (inclusive), increasing x order."""
+    bits = np.arange(lo_bits, hi_bits + 1, dtype=np.uint64).astype(np.uint32)
+    if sign < 0:
+        bits = (bits[::-1] | np.uint32(0x80000000))  # -1.0 ... -0.0 is increasing
+    return bits.view(np.float32)
+
+
+def ulaw_goldens(exhaustive=True):
+    Q = 256
+    lut = ref_utils.udequantize(torch.arange(Q), Q).numpy().astype(np.float32)
+
+    # --- float32 step function over [-1, 1], exhaustive --------------------------
+    steps_x, steps_v = [], []
+    prev = None
+    n_checked = 0
+    if exhaustive:
+        one = 0x3F800000
+        for sign in (-1, 1):
+            lo = 0
+            CH = 1 << 25
+            ranges = []
+            while lo <= one:
+                hi = min(one, lo + CH - 1)
+                ranges.append((lo, hi))
+                lo = hi + 1
+            if sign < 0:
+                ranges = ranges[::-1]
+            for lo, hi in ranges:
+                x = ordered_f32(lo, hi, sign)
+                q = ref_utils.uquantize(torch.from_numpy(x), Q).numpy()
+                n_checked += x.size
+                if prev is not None and q[0] != prev:
+                    chg = [0]
+                else:
+                    chg = []
+                d = np.nonzero(np.diff(q))[0] + 1
+                idx = np.concatenate([np.array(chg, dtype=np.int64), d])
+                for i in idx:
+                    steps_x.append(x[i])
+                    steps_v.append(q[i])
+                if prev is None:
+                    first_v = q[0]
+                prev = q[-1]
+        steps_x = np.array(steps_x, dtype=np.float32)
+        steps_v = np.array(steps_v, dtype=np.int64)
+        # monotone, +1 steps?
+        assert np.all(np.diff(steps_v) == 1), 'float32 quantizer not a +1 staircase'
+        assert steps_v[0] == first_v + 1
+        print('f32 exhaustive: %d values, base %d, %d steps' % (n_checked, first_v, len(steps_x)))
+        f32_base = int(first_v)
+    else:
+        f32_base = -1
+
+    # --- float64 thresholds by bisection on the ordered bit pattern --------------
+    def q64(v):
+        return int(ref_utils.uquantize(torch.tensor([v], dtype=torch.float64), Q)[0])
+
+    def key64(v):
+        b = np.array([v], dtype=np.float64).view(np.int64)[0]
+        return int(b) if b >= 0 else -int(b & 0x7FFFFFFFFFFFFFFF)
+
+    def val64(k):
+        if k >= 0:
+            return float(np.array([k], dtype=np.int64).view(np.float64)[0])
+        return float(np.array([(-k) | (1 << 63)], dtype=np.uint64).view(np.float64)[0])
+
+    lo_k, hi_k = key64(-1.0), key64(1.0)
+    base64 = q64(-1.0)
+    top64 = q64(1.0)
+    thr64 = []
+    for target in range(base64 + 1, top64 + 1):
+        a, b = lo_k, hi_k  # q(a) < target <= q(b)
+        while b - a > 1:
+            m = (a + b) // 2
+            if q64(val64(m)) >= target:
+                b = m
+            else:
+                a = m
+        thr64.append(val64(b))
+    thr64 = np.array(thr64, dtype=np.float64)
+    print('f64 thresholds: base %d top %d n %d' % (base64, top64, len(thr64)))
+
+    # --- KATs (vectorised reference path) ----------------------------------------
+    rng = np.random.Generator(np.random.PCG64(1234))
+    x32 = np.concatenate([
+        rng.uniform(-1, 1, 60000), rng.laplace(0, 0.05, 20000).clip(-1, 1),
+        np.array([-1.0, -0.5, -0.0, 0.0, 0.5, 1.0, 1e-30, -1e-30, 1e-8, -1e-8]),
+        (steps_x if exhaustive else np.zeros(0)),
+        (np.nextafter(steps_x, np.float32(-2)) if exhaustive else np.zeros(0)),
+    ]).astype(np.float32)
+    q32 = ref_utils.uquantize(torch.from_numpy(x32), Q).numpy()
+    x64 = np.concatenate([
+        rng.uniform(-1, 1, 60000), rng.laplace(0, 0.05, 20000).clip(-1, 1),
+        np.array([-1.0, -0.5, -0.0, 0.0, 0.5, 1.0, 1e-300, -1e-300]),
+        thr64, np.nextafter(thr64, -2.0), np.nextafter(thr64, 2.0),
+    ]).astype(np.float64)
+    q64v = ref_utils.uquantize(torch.from_numpy(x64), Q).numpy()
+    # linear quantizer KAT (utils.py:9-19), rows of 64 samples
+    xl = rng.uniform(-1, 1, (64, 257)).astype(np.float32)
+    # the reference's linear_quantize only broadcasts for 1-D input (utils.py:11-12)
+    ql = np.stack([ref_utils.linear_quantize(torch.from_numpy(r), Q).numpy() for r in xl])
+    ldq = ref_utils.linear_dequantize(torch.arange(Q), Q).numpy()
+
+    save('ulaw', lut=lut, f32_steps_x=steps_x, f32_steps_v=steps_v,
+         f32_base=np.array(f32_base), f64_thresholds=thr64, f64_base=np.array(base64),
+         kat_x32=x32, kat_q32=q32.astype(np.int16), kat_x64=x64, kat_q64=q64v.astype(np.int16),
+         lin_x=xl, lin_q=ql.astype(np.int16), lin_lut=ldq, q_zero=np.array(ref_utils.q_zero(Q)))
+
+
+# --------------------------------------------------------------------------- model
+def build_ref(cfg, weights):
+    m = ref_model.SampleRNN(cfg['frame_sizes'], cfg['n_rnn'], cfg['dim'], cfg['learn_h0'],
+                            cfg['q_levels'], True, cfg['weight_norm'], cfg['cond_dim'],
+                            cfg['spk_dim'])
+    pred = ref_model.Predictor(m)
+    sd = {k: torch.from_numpy(v.copy()) for k, v in weights.items()}
+    missing = pred.load_state_dict(sd, strict=True)
+    return m, pred
+
+
+def make_chunks(cfg, B, T, n_chunks, seed):
+    """Stateful TBPTT layout (dataset.py:155-163, 242-289) on synthetic streams."""
+    L = recipe.lookback(cfg)
+    total = n_chunks * T + L
+    audio = np.stack([recipe.synth_audio(total, seed + b) for b in range(B)])
+    idx = ref_utils.uquantize(torch.from_numpy(audio), cfg['q_levels']).numpy()  # float64 path
+    C = cfg['cond_dim']
+    cond = recipe.synth_cond((B, n_chunks * T // L, C), seed + 100)
+    spk = (np.arange(B) % cfg['spk_dim']).reshape(B, 1).astype(np.int64)
+    chunks = []
+    for n in range(n_chunks):
+        inp = np.ascontiguousarray(idx[:, n * T: n * T + L + T - 1])
+        tgt = np.ascontiguousarray(idx[:, n * T + L: n * T + L + T])
+        cnd = np.ascontiguousarray(cond[:, n * T // L: (n + 1) * T // L])
+        chunks.append((inp, n == 0, tgt, cnd, spk))
+    return audio, chunks
+
+
+def forward_goldens(name, B, T, n_chunks, seed, keep_rows=None):
+    cfg = recipe.CONFIGS[name]
+    w = recipe.make_weights(cfg, seed)
+    m, _ = build_ref(cfg, w)
+    preds = [ref_model.Predictor(m) for _ in range(B)]
+    audio, chunks = make_chunks(cfg, B, T, n_chunks, seed + 7)
+    out = dict(B=np.array(B), T=np.array(T), n_chunks=np.array(n_chunks),
+               weight_seed=np.array(seed))
+    with torch.no_grad():
+        for n, (inp, reset, tgt, cnd, spk) in enumerate(chunks):
+            logps = []
+            for b in range(B):
+                lp = preds[b](torch.from_numpy(inp[b:b + 1]), reset,
+                              torch.from_numpy(cnd[b:b + 1]), torch.from_numpy(spk[b:b + 1]),
+                              None, 0)
+                logps.append(lp.numpy())
+            logp = np.concatenate(logps, 0)
+            loss = float(ref_nn.sequence_nll_loss_bits(torch.from_numpy(logp),
+                                                       torch.from_numpy(tgt)))
+            out['input_%d' % n] = inp
+            out['target_%d' % n] = tgt
+            out['cond_%d' % n] = cnd
+            out['spk_%d' % n] = spk
+            out['reset_%d' % n] = np.array(reset)
+            out['loss_%d' % n] = np.array(loss)
+            if keep_rows is None:
+                out['logp_%d' % n] = logp
+            else:
+                out['logp_rows_%d' % n] = logp[:, keep_rows]
+                out['logp_sum_%d' % n] = logp.astype(np.float64).sum(axis=(1, 2))
+            for t, rnn in enumerate(m.frame_level_rnns):
+                hs = np.concatenate([preds[b].hidden_states[rnn].numpy() for b in range(B)], 1)
+                out['hidden_%d_tier%d' % (n, t)] = hs
+    if keep_rows is not None:
+        out['keep_rows'] = np.array(keep_rows)
+    save('fwd_' + name, **out)
+
+
+def generation_goldens(name, n_seqs, num_cond, seed, gen_seed):
+    cfg = recipe.CONFIGS[name]
+    w = recipe.make_weights(cfg, seed)
+    m, _ = build_ref(cfg, w)
+    cond = recipe.synth_cond((num_cond, cfg['cond_dim']), seed + 3)
+    spk = 3 % cfg['spk_dim']
+    gen = ref_model.Generator(m, False)
+    # record every per-step MLP output (log-probs) the generator samples from
+    rec = []
+    orig = m.sample_level_mlp.forward
+
+    def hooked(prev, upper):
+        o = orig(prev, upper)
+        rec.append(o.detach().clone())
+        return o
+    m.sample_level_mlp.forward = hooked
+    torch.manual_seed(gen_seed)
+    state = torch.get_rng_state()
+    devnull = open(os.devnull, 'w')
+    so = sys.stdout
+    sys.stdout = devnull
+    try:
+        with torch.no_grad():
+            samples = gen(n_seqs, 0, cond, spk)
+    finally:
+        sys.stdout = so
+    m.sample_level_mlp.forward = orig
+    L = recipe.lookback(cfg)
+    T = num_cond * L
+    logp = torch.cat(rec, 1).numpy()  # (n_seqs, T, Q)
+    samples = samples.numpy()
+    # replay the sampler: q_t ~ Exp(1) drawn in the reference's order
+    torch.set_rng_state(state)
+    q = torch.empty(T, n_seqs, cfg['q_levels']).exponential_(1).numpy()
+    p = np.exp(logp).astype(np.float32)
+    idx = np.argmax(p.transpose(1, 0, 2) / q, axis=-1).T  # (n_seqs, T)
+    ratio = np.sort(p.transpose(1, 0, 2) / q, axis=-1)
+    margin = float(np.min((ratio[..., -1] - ratio[..., -2]) / ratio[..., -1]))
+    lut = ref_utils.udequantize(torch.arange(cfg['q_levels']), cfg['q_levels']).numpy()
+    assert np.array_equal(lut[idx], samples), 'noise replay does not reproduce the reference'
+    print('gen %s: T=%d n_seqs=%d min relative margin %.3g' % (name, T, n_seqs, margin))
+    save('gen_' + name, cond=cond, spk=np.array(spk), n_seqs=np.array(n_seqs),
+         weight_seed=np.array(seed), noise=q, idx=idx.astype(np.int64), samples=samples,
+         logp=logp, margin=np.array(margin))
+
+
+class _RowwisePredictor(torch.nn.Module):
+    """B independent reference Predictors over ONE shared SampleRNN (model.py:209 is B=1)."""
+
+    def __init__(self, m, B):
+        super().__init__()
+        self.model = m
+        self.rows = [ref_model.Predictor(m) for _ in range(B)]
+
+    def forward(self, inp, reset, cond, spk, writer, it):
+        return torch.cat([p(inp[b:b + 1], reset, cond[b:b + 1], spk[b:b + 1], writer, it)
+                          for b, p in enumerate(self.rows)], 0)
+
+
+class _Adam(torch.optim.Adam):
+    """torch-0.4 zero_grad semantics + capture of the clipped grads per step."""
+
+    def __init__(self, *a, **k):
+        super().__init__(*a, **k)
+        self.captured = []
+
+    def zero_grad(self, set_to_none=False):
+        super().zero_grad(set_to_none=False)
+
+    def step(self, closure=None):
+        loss = closure()
+        self.captured.append([p.grad.detach().clone() for g in self.param_groups
+                              for p in g['params']])
+        super().step()
+        return loss
+
+
+def tbptt_goldens(name, B, T, n_steps, seed, lr=1e-3):
+    cfg = recipe.CONFIGS[name]
+    w = recipe.make_weights(cfg, seed)
+    m, _ = build_ref(cfg, w)
+    rp = _RowwisePredictor(m, B)
+    names = [k for k, _ in rp.named_parameters()]
+    params = [p for _, p in rp.named_parameters()]
+    opt = ref_optim.gradient_clipping(_Adam(params, lr=lr))
+    audio, chunks = make_chunks(cfg, B, T, n_steps, seed + 11)
+    losses = []
+
+    def criterion(out, tgt):
+        loss = ref_nn.sequence_nll_loss_bits(out, tgt)
+        losses.append(float(loss))
+        return loss
+    # dataset items as the DataLoader would collate them
+    data = [(torch.from_numpy(inp), torch.tensor([int(reset)] * B), torch.from_numpy(tgt),
+             torch.from_numpy(cnd), torch.from_numpy(spk)) for inp, reset, tgt, cnd, spk in chunks]
+    tr = ref_trainer.Trainer(rp, criterion, opt, data, False, None)
+    tr.run(1)
+    out = dict(B=np.array(B), T=np.array(T), n_steps=np.array(n_steps), lr=np.array(lr),
+               weight_seed=np.array(seed), losses=np.array(losses), names=np.array(names))
+    for n, (inp, reset, tgt, cnd, spk) in enumerate(chunks):
+        out['input_%d' % n] = inp
+        out['target_%d' % n] = tgt
+        out['cond_%d' % n] = cnd
+        out['spk_%d' % n] = spk
+        out['reset_%d' % n] = np.array(reset)
+    for s, grads in enumerate(opt.captured[:2]):  # step 1 = non-reset (h0 zero grad)
+        for k, g in zip(names, grads):
+            out['grad_%d/%s' % (s, k)] = g.numpy()
+    for k, p in zip(names, params):
+        out['param_final/%s' % k] = p.detach().numpy()
+    for t, rnn in enumerate(m.frame_level_rnns):
+        out['hidden_final_tier%d' % t] = np.concatenate(
+            [r.hidden_states[rnn].numpy() for r in rp.rows], 1)
+    print('tbptt %s losses' % name, losses)
+    save('tbptt_' + name, **out)
+
+
+def init_goldens():
+    """a13: parameter init recipe (RNG consumption order) -> checksums."""
+    out = {}
+    for name in ('t2', 't3', 't3r2wn'):
+        cfg = recipe.CONFIGS[name]
+        torch.manual_seed(77977)
+        m = ref_model.SampleRNN(cfg['frame_sizes'], cfg['n_rnn'], cfg['dim'], cfg['learn_h0'],
+                                cfg['q_levels'], True, cfg['weight_norm'], cfg['cond_dim'],
+                                cfg['spk_dim'])
+        sd = ref_model.Predictor(m).state_dict()
+        for k, v in sd.items():
+            a = v.detach().numpy().astype(np.float64).ravel()
+            out['%s/%s' % (name, k)] = np.array([a.sum(), np.abs(a).sum(), (a * a).sum(),
+                                                  a[0], a[-1], a[len(a) // 2]])
+    save('init', **out)
+
+
+def samples_wav_kat():
+    """samples/*.wav (generated by the reference's checkpoint) lie on the LUT grid."""
+    from scipy.io import wavfile
+    vals, lens, kinds = [], [], []
+    for f in sorted(glob.glob(os.path.join(REF, 'samples', '*.wav'))):
+        sr, a = wavfile.read(f)
+        lens.append(len(a))
+        kinds.append(str(a.dtype))
+        if a.dtype == np.float32:
+            vals.append(np.unique(a))
+    u = np.unique(np.concatenate(vals))
+    save('samples_wav', unique_values=u.astype(np.float32), lengths=np.array(lens),
+         dtypes=np.array(kinds))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--skip-exhaustive', action='store_true')
+    ap.add_argument('--only', default='')
+    a = ap.parse_args()
+    only = set(a.only.split(',')) if a.only else None
+    t0 = time.time()
+
+    def want(x):
+        return only is None or x in only
+    if want('ulaw'):
+        ulaw_goldens(exhaustive=not a.skip_exhaustive)
+    if want('init'):
+        init_goldens()
+    if want('wav'):
+        samples_wav_kat()
+    if want('fwd'):
+        forward_goldens('t2', B=2, T=64, n_chunks=3, seed=11)
+        forward_goldens('t3', B=2, T=128, n_chunks=3, seed=12)
+        forward_goldens('t3r2wn', B=2, T=128, n_chunks=2, seed=13)
+        forward_goldens('t4la', B=2, T=256, n_chunks=2, seed=14)
+        forward_goldens('t3_20_4', B=2, T=160, n_chunks=2, seed=15)
+        forward_goldens('big', B=1, T=1024, n_chunks=1, seed=16,
+                        keep_rows=list(range(0, 1024, 16)))
+    if want('gen'):
+        generation_goldens('t2', n_seqs=3, num_cond=8, seed=21, gen_seed=5)
+        generation_goldens('t3', n_seqs=3, num_cond=3, seed=22, gen_seed=6)
+        generation_goldens('t4la', n_seqs=2, num_cond=2, seed=23, gen_seed=7)
+        generation_goldens('t3_20_4', n_seqs=2, num_cond=3, seed=24, gen_seed=8)
+        generation_goldens('t3r2wn', n_seqs=2, num_cond=2, seed=25, gen_seed=9)
+    if want('tbptt'):
+        tbptt_goldens('t3', B=2, T=128, n_steps=3, seed=31)
+        tbptt_goldens('t3r2wn', B=2, T=64, n_steps=3, seed=32)
+        tbptt_goldens('t2', B=3, T=64, n_steps=3, seed=33)
+    print('done in %.1fs' % (time.time() - t0))
+
+
+if __name__ == '__main__':
+    main()

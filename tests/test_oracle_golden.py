@@ -1,0 +1,113 @@
+"""Pin the CPU oracle (oracle/) to the reference's own outputs (tests/golden/)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import ROOT, golden
+import recipe
+import samplernn_oracle as O
+
+
+@pytest.fixture(scope='module')
+def culaw():
+    d = os.path.join(ROOT, 'oracle')
+    subprocess.check_call(['make', '-s', '-C', d])
+    return ctypes.CDLL(os.path.join(d, 'build', 'libulaw_oracle.so'))
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def test_c_oracle_ulaw_kat(culaw):
+    g = golden('ulaw')
+    for k, fn in (('32', culaw.oracle_uquantize_f32_n), ('64', culaw.oracle_uquantize_f64_n)):
+        x = np.ascontiguousarray(g['kat_x' + k])
+        out = np.zeros(x.size, np.int64)
+        fn(_p(x), _p(out), ctypes.c_int64(x.size), 256)
+        assert np.array_equal(out, g['kat_q' + k].astype(np.int64))
+    kk = np.arange(256, dtype=np.int64)
+    lut = np.zeros(256, np.float32)
+    culaw.oracle_udequantize_n(_p(kk), _p(lut), ctypes.c_int64(256), 256)
+    assert np.array_equal(lut, g['lut'])
+
+
+def test_torch_oracle_ulaw_kat():
+    g = golden('ulaw')
+    assert np.array_equal(O.uquantize(torch.from_numpy(g['kat_x32']), 256).numpy(), g['kat_q32'])
+    assert np.array_equal(O.uquantize(torch.from_numpy(g['kat_x64']), 256).numpy(), g['kat_q64'])
+    assert np.array_equal(O.udequantize(torch.arange(256), 256).numpy(), g['lut'])
+    lq = np.stack([O.linear_quantize(torch.from_numpy(r), 256).numpy() for r in g['lin_x']])
+    assert np.array_equal(lq, g['lin_q'])
+    assert np.array_equal(O.linear_dequantize(torch.arange(256), 256).numpy(), g['lin_lut'])
+    assert O.q_zero(256) == int(g['q_zero'])
+
+
+def test_samples_wav_on_lut_grid():
+    """samples/*.wav from the reference's checkpoint: every float32 value is a LUT entry."""
+    g = golden('samples_wav')
+    lut = golden('ulaw')['lut']
+    assert np.all(np.isin(g['unique_values'], lut))
+    f32 = [l for l, d in zip(g['lengths'], g['dtypes']) if d == 'float32']
+    assert len(f32) == 17 and all(l % 80 == 0 for l in f32)
+
+
+@pytest.mark.parametrize('name', ['t2', 't3', 't3r2wn', 't4la', 't3_20_4', 'big'])
+def test_oracle_forward(name):
+    g = golden('fwd_' + name)
+    cfg = recipe.CONFIGS[name]
+    m = O.from_state_dict(cfg, recipe.make_weights(cfg, int(g['weight_seed'])))
+    with torch.no_grad():
+        for n in range(int(g['n_chunks'])):
+            lp = m.predict(torch.from_numpy(g['input_%d' % n]), bool(g['reset_%d' % n]),
+                           torch.from_numpy(g['cond_%d' % n]), torch.from_numpy(g['spk_%d' % n]))
+            if 'keep_rows' in g:
+                np.testing.assert_allclose(lp[:, g['keep_rows']].numpy(), g['logp_rows_%d' % n],
+                                           atol=2e-5, rtol=0)
+            else:
+                np.testing.assert_allclose(lp.numpy(), g['logp_%d' % n], atol=2e-5, rtol=0)
+            for t in range(len(cfg['frame_sizes'])):
+                np.testing.assert_allclose(m.hidden[t].numpy(), g['hidden_%d_tier%d' % (n, t)],
+                                           atol=2e-6, rtol=0)
+
+
+@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn'])
+def test_oracle_generation(name):
+    g = golden('gen_' + name)
+    cfg = recipe.CONFIGS[name]
+    m = O.from_state_dict(cfg, recipe.make_weights(cfg, int(g['weight_seed'])))
+    seq, lp = m.generate(int(g['n_seqs']), g['cond'], int(g['spk']), torch.from_numpy(g['noise']),
+                         return_logp=True)
+    L = m.lookback
+    assert np.array_equal(seq[:, L:].numpy(), g['idx'])
+    np.testing.assert_allclose(lp.numpy(), g['logp'], atol=2e-5, rtol=0)
+    samples = O.udequantize(seq[:, L:], 256).numpy()
+    assert np.array_equal(samples, g['samples'])
+
+
+@pytest.mark.parametrize('name', ['t3', 't3r2wn', 't2'])
+def test_oracle_tbptt(name):
+    g = golden('tbptt_' + name)
+    cfg = recipe.CONFIGS[name]
+    m = O.from_state_dict(cfg, recipe.make_weights(cfg, int(g['weight_seed'])))
+    names = [str(s) for s in g['names']]
+    opt = O.OracleAdam([m.p[k] for k in names], lr=float(g['lr']))
+    for s in range(int(g['n_steps'])):
+        batch = (torch.from_numpy(g['input_%d' % s]), bool(g['reset_%d' % s]),
+                 torch.from_numpy(g['target_%d' % s]), torch.from_numpy(g['cond_%d' % s]),
+                 torch.from_numpy(g['spk_%d' % s]))
+        loss, grads = O.tbptt_step(m, opt, names, batch)
+        assert abs(loss - g['losses'][s]) < 1e-4
+        if ('grad_%d/%s' % (s, names[0])) in g:
+            for k, gr in zip(names, grads):
+                np.testing.assert_allclose(gr.numpy(), g['grad_%d/%s' % (s, k)], atol=2e-5,
+                                           rtol=1e-4, err_msg=k)
+    for k in names:
+        np.testing.assert_allclose(m.p[k].detach().numpy(), g['param_final/' + k], atol=1e-4,
+                                   rtol=0, err_msg=k)
+    for t in range(len(cfg['frame_sizes'])):
+        np.testing.assert_allclose(m.hidden[t].numpy(), g['hidden_final_tier%d' % t], atol=1e-5)
