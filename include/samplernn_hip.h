@@ -1,0 +1,168 @@
+/* samplernn_hip.h -- C ABI of the MI355X-native SampleRNN hot path (libsamplernn_hip.so).
+ *
+ * Plain pointers and sizes only: every buffer argument is a device pointer allocated
+ * and owned by the caller; `stream` is the caller's hipStream_t (NULL = default).
+ * Every entry point returns 0 on success, 1 on a bad argument and 2 on a HIP error;
+ * srnn_last_error() returns the text (per host thread).  Dtype codes: 0 = fp32,
+ * 1 = bf16.  GEMM operands follow BLAS conventions on row-major storage.
+ *
+ * The reference (mahdeslami11/jalil-saboorizadeh-Multi-speaker-Neural-Vocoder) is pure
+ * Python with no FFI; each entry point below names the reference function/operator it
+ * replaces.  The drop-in binding is the Python package beside this header
+ * (model.py / nn.py / utils.py / optim.py / trainer), see INTEGRATION.md.
+ */
+#ifndef SAMPLERNN_HIP_H
+#define SAMPLERNN_HIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRNN_MAX_TIERS 6
+#define SRNN_MAX_RNN 4
+
+const char* srnn_last_error(void);
+int srnn_abi_version(void);
+
+/* ---- mu-law / linear quantisation ------------------------------------------------
+ * utils.uquantize (utils.py:58-59 = midrise(ulaw(x)), utils.py:33-36,48-51): bit-exact to
+ * the reference for every float32 / float64 input in [-1, 1] (q_levels = 256).        */
+int srnn_uquantize_f32(const float* x, int64_t* out, int64_t n, int q_levels, void* stream);
+int srnn_uquantize_f64(const double* x, int64_t* out, int64_t n, int q_levels, void* stream);
+/* out = scale * udequantize(k) (utils.py:62-63, mode 0) or linear_dequantize
+ * (utils.py:18-19, mode 1); scale = 2 gives the model's `2 * dequantize` (model.py:385,471) */
+int srnn_udequantize(const int64_t* k, float* out, int64_t n, int q_levels, float scale,
+                     int mode, void* stream);
+
+/* ---- dense projections -------------------------------------------------------------
+ * C = act(alpha * op(A) . op(B) + beta * Cin + bias)  (bias_mode 1: per column, 2: per row)
+ * Replaces the Conv1d(k=1) / nn.Linear / GRU-input / ConvTranspose1d matmuls of
+ * model.py:85-116,148-178,287-301 and nn.py:12-43 (forward, dgrad and wgrad).
+ * tile = -1 picks the tile shape from the problem size.  mask (optional, input dtype,
+ * row stride ldmask) zeroes outputs where mask <= 0 (the ReLU backward of model.py:320-321). */
+int srnn_gemm(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
+              float alpha, const void* A, int64_t lda, int64_t strideA, const void* B,
+              int64_t ldb, int64_t strideB, float beta, const float* Cin, int64_t ldcin,
+              int64_t strideCin, void* C, int64_t ldc, int64_t strideC, const float* bias,
+              int bias_mode, int relu, int batch, int tile, const void* mask, int64_t ldmask,
+              void* stream);
+
+/* ---- GRU (torch.nn.GRU, model.py:148-165,244) -----------------------------------------
+ * One time step for B rows: h_t from h_{t-1} and either x (gi computed in-kernel with
+ * W_ih) or a precomputed gi = x W_ih^T + b_ih.  Optionally saves r|z|n|gh_n (4D/row).  */
+int srnn_gru_cell(int dtype, int B, int D, int Din, const void* x, int64_t ldx, const void* wih,
+                  const float* bih, const float* gi, int64_t ldgi, const void* h, int64_t ldh,
+                  const float* hf, int64_t ldhf, const void* whh, const float* bhh, float* hout,
+                  int64_t ldho, void* hout_lp, int64_t ldhl, float* gates, int64_t ldgt,
+                  void* stream);
+/* Backward of one step: dh_t = dy_t + dh_direct_{t+1} + dgh_{t+1} . W_hh, then the gate
+ * backward.  Writes dgh_t (fp32 + optional T copy), dgi_t (fp32), dh_direct_t = z*dh_t. */
+int srnn_gru_cell_bwd(int dtype, int B, int D, const float* dy, int64_t lddy,
+                      const void* dgh_next, int64_t lddgn, const float* ddir_next,
+                      const void* whh, const float* gates, int64_t ldgt, const float* hprev,
+                      int64_t ldhp, float* dgh, int64_t lddgh, void* dgh_lp, int64_t lddghl,
+                      float* dgi, int64_t lddgi, float* ddir, void* stream);
+
+/* ---- SampleLevelMLP (model.py:308-325) ----------------------------------------------
+ * a1[b*Tlen+t] = relu(sum_k tab[k][x[b*ldx + xoff + t + k]] + upper[b*Tlen+t])          */
+int srnn_mlp_l1(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff, int B,
+                int Tlen, const float* upper, int64_t ldu, void* out, int64_t ldo, int D,
+                int FS0, int Q, void* stream);
+/* dtab[x_{t+k}][k][:] += da_t  (Q, FS0, D) fp32 accumulate; backward of the folded     *
+ * embedding+conv                                                                        */
+int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x, int64_t ldx,
+                  int xoff, int B, int Tlen, float* dtab, int D, int FS0, int Q, void* stream);
+/* log_softmax (model.py:324-325) + NLL rows (nn.py:66-70) + dlogits (softmax-onehot)*g  */
+/* dz = dlogp - exp(logp) * rowsum(dlogp)   (log_softmax backward, rows of Q)          */
+int srnn_logsoftmax_bwd(const float* dlogp, int64_t lddl, const float* logp, int64_t ldl,
+                        int64_t rows, int Q, void* dz, int dz_dtype, int64_t ldd, void* stream);
+/* NLL over log-probs (nn.py:66-70): loss_row[r] = -logp[r, target]; and its gradient
+ * dlogp[r, :] = 0 except dlogp[r, target] = -gscale                                      */
+int srnn_nll_fwd(const float* logp, int64_t ldl, const int64_t* target, int64_t ldt, int Tlen,
+                 int64_t rows, float* loss_row, void* stream);
+int srnn_nll_bwd(const int64_t* target, int64_t ldt, int Tlen, int64_t rows, int Q,
+                 float* dlogp, int64_t ldd, float gscale, void* stream);
+int srnn_logsoftmax_nll(const float* z, int64_t ldz, const int64_t* target, int64_t ldt,
+                        int Tlen, int64_t rows, int Q, float* loss_row, float* logp,
+                        int64_t ldl, void* dz, int dz_dtype, int64_t ldd, float gscale,
+                        void* stream);
+
+/* Host-side (no GPU) bit-exact quantisers with the same tables, for the CPU data path. */
+int srnn_uquantize_f64_host(const double* x, int64_t* out, int64_t n, int q_levels);
+int srnn_uquantize_f32_host(const float* x, int64_t* out, int64_t n, int q_levels);
+int srnn_udequantize_host(const int64_t* k, float* out, int64_t n, int q_levels);
+
+/* ---- weight norm (torch weight_norm dim=0, model.py:119-131,177-178,303-306) -------- */
+int srnn_weight_norm_fwd(const float* g, const float* v, float* w, float* norm, int O,
+                         int64_t R, void* stream);
+int srnn_weight_norm_bwd(const float* g, const float* v, const float* dw, float* dg, float* dv,
+                         int O, int64_t R, int accumulate, void* stream);
+
+/* ---- layout / elementwise helpers ------------------------------------------------- */
+int srnn_permute3(const float* src, void* dst, int dst_dtype, int d0, int d1, int d2, int p0,
+                  int p1, int p2, int accumulate, void* stream);
+int srnn_copy2d(int src_dtype, int dst_dtype, int rows, int cols, const void* src, int64_t lds,
+                void* dst, int64_t ldd, void* stream);
+int srnn_gather_rows(const float* table, int64_t ldt, const int64_t* idx, int64_t n, int cols,
+                     void* out, int out_dtype, int64_t ldo, void* stream);
+int srnn_scatter_add_rows(float* table, int64_t ldt, const int64_t* idx, int64_t n, int cols,
+                          const float* src, int64_t lds, void* stream);
+int srnn_axpby(float* out, const float* a, const float* b, float alpha, float beta, int64_t n,
+               void* stream);
+int srnn_add_bcast_rows(float* x, const float* v, int B, int F, int D, int64_t ldv, void* stream);
+int srnn_colsum(int dtype, const void* src, int64_t lds, int64_t rows, int cols, float* out,
+                float alpha, int accumulate, float* work, int64_t work_elems, void* stream);
+
+/* ---- optimizer: gradient_clipping(-1, 1) + Adam (optim.py:4-21, train.py:238) --------
+ * Elementwise in-place clamp of g to [clip_lo, clip_hi] then torch.optim.Adam update.
+ * p_bf16 (optional) receives the updated parameters rounded to bf16.                    */
+int srnn_adam_clip(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n,
+                   float clip_lo, float clip_hi, double lr, double beta1, double beta2,
+                   double eps, int64_t step, void* stream);
+
+/* ---- autoregressive generation (Generator.__call__, model.py:445-520) --------------- */
+typedef struct SrnnTier {
+    int frame_size;            /* upsampling ratio of this tier                           */
+    int n_frame_samples;       /* nfs = cumprod(frame_sizes)                              */
+    int in_dim;                /* columns of w_in: nfs (+ cond_dim for the top tier)      */
+    const void* w_in;          /* (D, in_dim) [input_expand | cond_expand]               */
+    const float* b_in;         /* (D) input_expand bias (lower tiers; top uses row_bias)  */
+    const void* w_ih[SRNN_MAX_RNN];
+    const float* b_ih[SRNN_MAX_RNN];
+    const void* w_hh[SRNN_MAX_RNN];
+    const float* b_hh[SRNN_MAX_RNN];
+    const void* w_up;          /* (fs*D, D): row j*D+o = conv_t.weight[:, o, j]            */
+    const float* b_up;         /* (fs*D):   [j*D+o] = upsampling.bias[o, j]               */
+    const float* h0;           /* (n_rnn, D) learned / buffer initial state               */
+} SrnnTier;
+
+typedef struct SrnnModel {
+    int n_tiers, n_rnn, dim, q_levels, cond_dim, dtype;
+    SrnnTier tier[SRNN_MAX_TIERS]; /* index 0 = bottom tier (frame_sizes[0])             */
+    const void* tab;           /* (FS0, Q, D) folded embedding . input conv               */
+    const void* w_hid;         /* (D, D)  */
+    const float* b_hid;
+    const void* w_out;         /* (Q, D)  */
+    const float* b_out;
+} SrnnModel;
+
+/* Workspace bytes needed by srnn_generate for n_seqs rows. */
+int srnn_gen_workspace_size(const SrnnModel* m, int n_seqs, size_t* bytes);
+/* Generates n_cond * lookback samples for n_seqs rows.
+ *   cond     (n_seqs, n_cond, cond_dim) fp32, per-row conditioning frames
+ *   row_bias (n_seqs, D) fp32 = spk_expand(spk_embedding(spk)) + b_spk + b_cond + b_in (top)
+ *   noise    (n_cond*L, n_seqs, Q) fp32 Exp(1) draws consumed as argmax(p/q), or NULL to
+ *            draw q in-kernel from Philox4x32-10(seed)
+ *   seq      (n_seqs, L + n_cond*L) int64, columns [0, L) pre-filled (q_zero); output
+ *   logp     optional (n_cond*L, n_seqs, Q) fp32 per-step log-probs (debug / parity)
+ *   flags    bit 0: replay the generation block as a hipGraph                           */
+int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const float* cond,
+                  const float* row_bias, const float* noise, uint64_t seed, int64_t* seq,
+                  float* logp, void* workspace, size_t workspace_bytes, int flags, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

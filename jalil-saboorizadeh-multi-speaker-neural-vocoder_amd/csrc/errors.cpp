@@ -1,0 +1,11 @@
+#include <stdarg.h>
+#include <stdio.h>
+static thread_local char g_err[1024] = "";
+void srnn_set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+extern "C" const char* srnn_last_error() { return g_err; }
+extern "C" int srnn_abi_version() { return 1; }

@@ -1,0 +1,157 @@
+// General MFMA GEMM with fused epilogue:  C = act(alpha * op(A) op(B) + beta * Cin + bias)
+// Used for every dense projection of the SampleRNN hot path (tier input_expand /
+// cond_expand / spk_expand conv-k1, GRU input projection, LearnedUpsampling1d, the
+// MLP hidden/output conv-k1 layers) and their backward dgrad/wgrad products.
+#include "gemm_core.hpp"
+#include "samplernn_hip_internal.hpp"
+
+struct GemmArgs {
+    const void* A;
+    const void* B;
+    void* C;
+    const float* Cin;
+    const float* bias;
+    int64_t lda, ldb, ldc, ldcin;
+    int64_t sA, sB, sC, sCin;
+    int M, N, K;
+    float alpha, beta;
+    int bias_mode;  // 0 none, 1 per column, 2 per row
+    int relu;
+    int vecA, vecB;
+    const void* mask;  // optional relu-backward mask (input dtype): out = 0 where mask <= 0
+    int64_t ldmask;
+};
+
+template <typename T, typename TO, int BM, int BN, int KS, int WM, int WN, int WK, bool KCA,
+          bool KCB>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+    typedef GemmCfg<T, BM, BN, KS, WM, WN, WK> C;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int bz = blockIdx.z;
+    const T* A = reinterpret_cast<const T*>(g.A) + (int64_t)bz * g.sA;
+    const T* B = reinterpret_cast<const T*>(g.B) + (int64_t)bz * g.sB;
+    TO* Cp = reinterpret_cast<TO*>(g.C) + (int64_t)bz * g.sC;
+    const float* Cin = g.Cin ? g.Cin + (int64_t)bz * g.sCin : nullptr;
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    floatx4 acc[C::FM][C::FN];
+#pragma unroll
+    for (int i = 0; i < C::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    gemm_core<T, BM, BN, KS, WM, WN, WK, KCA, KCB>(
+        A, g.lda, RowIdentity{m0, g.M}, m0, g.M, g.vecA != 0, B, g.ldb, RowIdentity{n0, g.N}, n0,
+        g.N, g.vecB != 0, g.K, smem, acc);
+    wk_reduce<T, BM, BN, KS, WM, WN, WK>(smem, acc);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
+    if (wk != 0) return;
+#pragma unroll
+    for (int fm = 0; fm < C::FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < C::FN; ++fn) {
+            const int col = n0 + wn * C::FN * 16 + fn * 16 + (lane & 15);
+            if (col >= g.N) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = m0 + wm * C::FM * 16 + fm * 16 + (lane >> 4) * 4 + i;
+                if (row >= g.M) continue;
+                float v = g.alpha * acc[fm][fn][i];
+                if (g.beta != 0.f) v += g.beta * Cin[(int64_t)row * g.ldcin + col];
+                if (g.bias_mode == 1) v += g.bias[col];
+                else if (g.bias_mode == 2) v += g.bias[row];
+                if (g.relu) v = fmaxf(v, 0.f);
+                if (g.mask && !(to_f(((const T*)g.mask)[(int64_t)row * g.ldmask + col]) > 0.f))
+                    v = 0.f;
+                Cp[(int64_t)row * g.ldc + col] = from_f<TO>(v);
+            }
+        }
+}
+
+template <typename T, typename TO, int BM, int BN, int KS, int WM, int WN, int WK, bool KCA,
+          bool KCB>
+static int launch_t(const GemmArgs& g, int batch, hipStream_t s) {
+    typedef GemmCfg<T, BM, BN, KS, WM, WN, WK> C;
+    dim3 grid(cdiv(g.N, BN), cdiv(g.M, BM), batch);
+    auto k = gemm_kernel<T, TO, BM, BN, KS, WM, WN, WK, KCA, KCB>;
+    static bool attr_set = false;
+    if (!attr_set && C::LDS > 65536) {
+        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS));
+    }
+    attr_set = true;
+    hipLaunchKernelGGL(k, grid, dim3(256), C::LDS, s, g);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+template <typename T, typename TO, bool KCA, bool KCB>
+static int launch_layout(const GemmArgs& g, int batch, int tile, hipStream_t s) {
+    switch (tile) {
+    case 0:  return launch_t<T, TO, 128, 128, 2, 2, 2, 1, KCA, KCB>(g, batch, s);
+    case 1:  return launch_t<T, TO, 64, 64, 4, 2, 2, 1, KCA, KCB>(g, batch, s);
+    default: return launch_t<T, TO, 32, 32, 4, 1, 1, 4, KCA, KCB>(g, batch, s);
+    }
+}
+
+template <typename T, typename TO>
+static int launch_types(const GemmArgs& g, int transA, int transB, int batch, int tile,
+                        hipStream_t s) {
+    const bool kca = !transA, kcb = transB;
+    if (kca && kcb) return launch_layout<T, TO, true, true>(g, batch, tile, s);
+    if (kca && !kcb) return launch_layout<T, TO, true, false>(g, batch, tile, s);
+    if (!kca && kcb) return launch_layout<T, TO, false, true>(g, batch, tile, s);
+    return launch_layout<T, TO, false, false>(g, batch, tile, s);
+}
+
+static int pick_tile(int M, int N, int batch) {
+    const int64_t t128 = (int64_t)cdiv(M, 128) * cdiv(N, 128) * batch;
+    if (t128 >= 256) return 0;
+    const int64_t t64 = (int64_t)cdiv(M, 64) * cdiv(N, 64) * batch;
+    if (t64 >= 192) return 1;
+    return 2;
+}
+
+int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
+                   float alpha, const void* A, int64_t lda, int64_t strideA, const void* B,
+                   int64_t ldb, int64_t strideB, float beta, const float* Cin, int64_t ldcin,
+                   int64_t strideCin, void* C, int64_t ldc, int64_t strideC, const float* bias,
+                   int bias_mode, int relu, int batch, int tile, hipStream_t s,
+                   const void* mask, int64_t ldmask) {
+    SRNN_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: bad sizes");
+    SRNN_REQUIRE(dtype == SRNN_F32 || dtype == SRNN_BF16, "gemm: bad dtype %d", dtype);
+    SRNN_REQUIRE(out_dtype == SRNN_F32 || out_dtype == SRNN_BF16, "gemm: bad out dtype");
+    SRNN_REQUIRE(!(beta != 0.f && Cin == nullptr), "gemm: beta != 0 needs Cin");
+    if (M == 0 || N == 0) return 0;
+    const int es = dtype == SRNN_F32 ? 4 : 2;
+    const int E = 16 / es;
+    GemmArgs g;
+    g.A = A; g.B = B; g.C = C; g.Cin = Cin; g.bias = bias;
+    g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldcin = ldcin;
+    g.sA = strideA; g.sB = strideB; g.sC = strideC; g.sCin = strideCin;
+    g.M = M; g.N = N; g.K = K; g.alpha = alpha; g.beta = beta;
+    g.bias_mode = bias ? bias_mode : 0; g.relu = relu;
+    g.mask = mask; g.ldmask = ldmask;
+    auto aligned = [&](const void* p, int64_t ld, int64_t st) {
+        return ((uintptr_t)p % 16 == 0) && (ld % E == 0) && (batch == 1 || st % E == 0);
+    };
+    g.vecA = aligned(A, lda, strideA);
+    g.vecB = aligned(B, ldb, strideB);
+    if (tile < 0) tile = pick_tile(M, N, batch);
+    if (dtype == SRNN_F32) {
+        if (out_dtype == SRNN_F32) return launch_types<float, float>(g, transA, transB, batch, tile, s);
+        return launch_types<float, bf16>(g, transA, transB, batch, tile, s);
+    }
+    if (out_dtype == SRNN_F32) return launch_types<bf16, float>(g, transA, transB, batch, tile, s);
+    return launch_types<bf16, bf16>(g, transA, transB, batch, tile, s);
+}
+
+extern "C" int srnn_gemm(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
+                         float alpha, const void* A, int64_t lda, int64_t strideA, const void* B,
+                         int64_t ldb, int64_t strideB, float beta, const float* Cin, int64_t ldcin,
+                         int64_t strideCin, void* C, int64_t ldc, int64_t strideC,
+                         const float* bias, int bias_mode, int relu, int batch, int tile,
+                         const void* mask, int64_t ldmask, void* stream) {
+    return srnn_gemm_impl(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, strideA, B,
+                          ldb, strideB, beta, Cin, ldcin, strideCin, C, ldc, strideC, bias,
+                          bias_mode, relu, batch, tile, (hipStream_t)stream, mask, ldmask);
+}

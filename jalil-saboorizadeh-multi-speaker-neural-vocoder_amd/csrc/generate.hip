@@ -1,0 +1,331 @@
+// Autoregressive generation (Generator.__call__, model.py:445-520) on the device.
+//
+// The reference runs a Python loop per sample: ~10 small kernels + a host<->device
+// round trip + a print per tier tick.  Here the whole loop stays on the GPU: the
+// sample indices live in a device int64 buffer (never copied back until the end),
+// every kernel that depends on the current sample position reads a device-side
+// block base `*base` plus a compile-time-constant offset, so one block of 2 top-tier
+// periods (2 * lookback samples, every tier ticking an even number of times so the
+// GRU state ping-pong returns to buffer 0) is captured once as a hipGraph and
+// replayed n_cond / 2 times.  Per sample: L1 gather -> hidden GEMM (relu) -> output
+// GEMM -> softmax/sampler; per tier tick: input build -> input GEMM -> GRU cell(s) ->
+// upsampling GEMM.
+#include "samplernn_hip_internal.hpp"
+#include "ulaw_tables.h"
+#include "../../include/samplernn_hip.h"
+
+int srnn_mlp_l1_impl(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff,
+                     const int* base, int B, int Tlen, const float* upper, int64_t ldu, void* out,
+                     int64_t ldo, int D, int FS0, int Q, hipStream_t s);
+int srnn_sample_impl(const float* z, int64_t ldz, int B, const float* noise, uint64_t seed,
+                     const int* base, int off, int L, int64_t* seq, int64_t ldseq,
+                     float* logp_out, hipStream_t s);
+int srnn_gru_cell_impl(int dtype, int B, int D, int Din, const void* x, int64_t ldx,
+                       const void* wih, const float* bih, const float* gi, int64_t ldgi,
+                       const void* h, int64_t ldh, const float* hf, int64_t ldhf, const void* whh,
+                       const float* bhh, float* hout, int64_t ldho, void* hout_lp, int64_t ldhl,
+                       float* gates, int64_t ldgt, hipStream_t s);
+
+// A_in[b, s] = 2*deq(seq[b, i - nfs + s]) (s < nfs);  A_in[b, nfs + c] = cond[b, j, c]
+template <typename T>
+__global__ void build_input_kernel(const int64_t* __restrict__ seq, int64_t ldseq,
+                                   const int* __restrict__ base, int off, int nfs,
+                                   const float* __restrict__ lut2, const float* __restrict__ cond,
+                                   int n_cond, int C, int L, int B, T* __restrict__ A,
+                                   int in_dim) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= B * in_dim) return;
+    const int b = e / in_dim, s = e % in_dim;
+    const int i = *base + off;
+    float v;
+    if (s < nfs) {
+        v = lut2[seq[(int64_t)b * ldseq + i - nfs + s]];
+    } else {
+        const int j = i / L - 1;   // model.py:483
+        v = cond[((int64_t)b * n_cond + j) * C + (s - nfs)];
+    }
+    A[(int64_t)b * in_dim + s] = from_f<T>(v);
+}
+
+template <typename T>
+__global__ void init_state_kernel(const float* __restrict__ h0, float* __restrict__ h,
+                                  T* __restrict__ hlp, int B, int D) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= B * D) return;
+    const float v = h0[e % D];
+    h[e] = v;
+    if (hlp) hlp[e] = from_f<T>(v);
+}
+
+__global__ void advance_kernel(int* base, int by) { *base += by; }
+
+namespace {
+
+constexpr size_t ALIGN = 256;
+inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
+
+struct Bufs {
+    void* A_in[SRNN_MAX_TIERS];
+    void* x[SRNN_MAX_TIERS];
+    float* h[SRNN_MAX_TIERS][SRNN_MAX_RNN][2];
+    void* hlp[SRNN_MAX_TIERS][SRNN_MAX_RNN][2];
+    float* up[SRNN_MAX_TIERS];
+    void* a1;
+    void* a2;
+    float* logits;
+    float* lut2;
+    int* base;
+};
+
+// carve (or size, if ws == nullptr) the workspace
+size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b) {
+    const int D = m->dim, Q = m->q_levels;
+    const size_t es = m->dtype == SRNN_F32 ? 4 : 2;
+    const bool lp = m->dtype != SRNN_F32;
+    size_t off = 0;
+    auto take = [&](size_t bytes) -> char* {
+        char* p = ws ? ws + off : nullptr;
+        off += al(bytes);
+        return p;
+    };
+    for (int k = 0; k < m->n_tiers; ++k) {
+        const SrnnTier& t = m->tier[k];
+        b->A_in[k] = take((size_t)B * t.in_dim * es);
+        b->x[k] = take((size_t)B * D * es);
+        for (int l = 0; l < m->n_rnn; ++l)
+            for (int p = 0; p < 2; ++p) {
+                b->h[k][l][p] = (float*)take((size_t)B * D * 4);
+                b->hlp[k][l][p] = lp ? (void*)take((size_t)B * D * es) : (void*)b->h[k][l][p];
+            }
+        b->up[k] = (float*)take((size_t)B * t.frame_size * D * 4);
+    }
+    b->a1 = take((size_t)B * D * es);
+    b->a2 = take((size_t)B * D * es);
+    b->logits = (float*)take((size_t)B * Q * 4);
+    b->lut2 = (float*)take((size_t)Q * 4);
+    b->base = (int*)take(64);
+    return off;
+}
+
+struct Ctx {
+    const SrnnModel* m;
+    Bufs b;
+    int B, n_cond, L;
+    const float* cond;
+    const float* row_bias;
+    const float* noise;
+    uint64_t seed;
+    int64_t* seq;
+    int64_t ldseq;
+    float* logp;
+    hipStream_t s;
+};
+
+#define RET(x) do { int _r = (x); if (_r) return _r; } while (0)
+
+// one tier tick at block-relative offset `off`; `par` = tick parity of this tier
+int tier_tick(Ctx& c, int k, int off, int par) {
+    const SrnnModel* m = c.m;
+    const SrnnTier& t = m->tier[k];
+    const int D = m->dim, B = c.B, dt = m->dtype;
+    const bool top = (k == m->n_tiers - 1);
+    const bool lp = dt != SRNN_F32;
+    // 1. input rows
+    {
+        const int n = B * t.in_dim;
+        if (dt == SRNN_F32)
+            hipLaunchKernelGGL((build_input_kernel<float>), dim3(cdiv(n, 256)), dim3(256), 0, c.s,
+                               c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.cond,
+                               c.n_cond, m->cond_dim, c.L, B, (float*)c.b.A_in[k], t.in_dim);
+        else
+            hipLaunchKernelGGL((build_input_kernel<bf16>), dim3(cdiv(n, 256)), dim3(256), 0, c.s,
+                               c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.cond,
+                               c.n_cond, m->cond_dim, c.L, B, (bf16*)c.b.A_in[k], t.in_dim);
+        SRNN_LAUNCH_CHECK();
+    }
+    // 2. x = A_in . W_in^T + (top: row_bias ; lower: b_in + upper-tier conditioning row)
+    if (top) {
+        RET(linear_fwd(dt, dt, B, D, t.in_dim, c.b.A_in[k], t.in_dim, t.w_in, t.in_dim, nullptr,
+                       c.b.x[k], D, 0, c.s, 1.f, c.row_bias, D));
+    } else {
+        const SrnnTier& u = m->tier[k + 1];
+        // frame_index = (i // nfs_k) % FS_{k+1}  (model.py:491-492); base is a multiple of L
+        const int fi = (off / t.n_frame_samples) % u.frame_size;
+        RET(linear_fwd(dt, dt, B, D, t.in_dim, c.b.A_in[k], t.in_dim, t.w_in, t.in_dim, t.b_in,
+                       c.b.x[k], D, 0, c.s, 1.f, c.b.up[k + 1] + (size_t)fi * D,
+                       (int64_t)u.frame_size * D));
+    }
+    // 3. GRU layers
+    const int cur = par, nxt = par ^ 1;
+    for (int l = 0; l < m->n_rnn; ++l) {
+        const void* xin = l == 0 ? c.b.x[k] : c.b.hlp[k][l - 1][nxt];
+        RET(srnn_gru_cell_impl(dt, B, D, D, xin, D, t.w_ih[l], t.b_ih[l], nullptr, 0,
+                               c.b.hlp[k][l][cur], D, c.b.h[k][l][cur], D, t.w_hh[l], t.b_hh[l],
+                               c.b.h[k][l][nxt], D, lp ? c.b.hlp[k][l][nxt] : nullptr, D, nullptr,
+                               0, c.s));
+    }
+    // 4. LearnedUpsampling1d: up = h . W_up^T + b_up   (B, fs*D) fp32
+    RET(linear_fwd(dt, SRNN_F32, B, t.frame_size * D, D, c.b.hlp[k][m->n_rnn - 1][nxt], D, t.w_up,
+                   D, t.b_up, c.b.up[k], (int64_t)t.frame_size * D, 0, c.s));
+    return 0;
+}
+
+int mlp_step(Ctx& c, int off) {
+    const SrnnModel* m = c.m;
+    const int D = m->dim, Q = m->q_levels, B = c.B, dt = m->dtype;
+    const int FS0 = m->tier[0].frame_size;
+    RET(srnn_mlp_l1_impl(dt, m->tab, c.seq, c.ldseq, off - FS0, c.b.base, B, 1,
+                         c.b.up[0] + (size_t)(off % FS0) * D, (int64_t)FS0 * D, c.b.a1, D, D, FS0,
+                         Q, c.s));
+    RET(linear_fwd(dt, dt, B, D, D, c.b.a1, D, m->w_hid, D, m->b_hid, c.b.a2, D, 1, c.s));
+    RET(linear_fwd(dt, SRNN_F32, B, Q, D, c.b.a2, D, m->w_out, D, m->b_out, c.b.logits, Q, 0,
+                   c.s));
+    RET(srnn_sample_impl(c.b.logits, Q, B, c.noise, c.seed, c.b.base, off, c.L, c.seq, c.ldseq,
+                         c.logp, c.s));
+    return 0;
+}
+
+// `periods` consecutive top-tier periods starting at sample *base; tick parity restarts
+// at 0 (callers only chain blocks with an even tick count per tier)
+int run_block(Ctx& c, int periods) {
+    const SrnnModel* m = c.m;
+    int ticks[SRNN_MAX_TIERS] = {0};
+    for (int off = 0; off < periods * c.L; ++off) {
+        for (int k = m->n_tiers - 1; k >= 0; --k) {
+            if (off % m->tier[k].n_frame_samples != 0) continue;
+            RET(tier_tick(c, k, off, ticks[k] & 1));
+            ticks[k]++;
+        }
+        RET(mlp_step(c, off));
+    }
+    hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(1), 0, c.s, c.b.base, periods * c.L);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int srnn_gen_workspace_size(const SrnnModel* m, int n_seqs, size_t* bytes) {
+    SRNN_REQUIRE(m && bytes && n_seqs > 0, "gen_workspace_size: bad args");
+    Bufs b;
+    *bytes = carve(m, n_seqs, nullptr, &b);
+    return 0;
+}
+
+extern "C" int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const float* cond,
+                             const float* row_bias, const float* noise, uint64_t seed,
+                             int64_t* seq, float* logp, void* workspace, size_t workspace_bytes,
+                             int flags, void* stream) {
+    SRNN_REQUIRE(m && n_seqs > 0 && n_cond > 0 && seq && workspace, "generate: bad args");
+    SRNN_REQUIRE(m->n_tiers >= 1 && m->n_tiers <= SRNN_MAX_TIERS, "generate: n_tiers");
+    SRNN_REQUIRE(m->n_rnn >= 1 && m->n_rnn <= SRNN_MAX_RNN, "generate: n_rnn");
+    SRNN_REQUIRE(m->q_levels == 256, "generate: q_levels must be 256");
+    SRNN_REQUIRE(m->dim % 16 == 0, "generate: dim must be a multiple of 16");
+    Ctx c;
+    c.m = m;
+    size_t need = carve(m, n_seqs, (char*)workspace, &c.b);
+    SRNN_REQUIRE(workspace_bytes >= need, "generate: workspace %zu < %zu", workspace_bytes, need);
+    c.B = n_seqs;
+    c.n_cond = n_cond;
+    c.L = m->tier[m->n_tiers - 1].n_frame_samples;
+    c.cond = cond;
+    c.row_bias = row_bias;
+    c.noise = noise;
+    c.seed = seed;
+    c.seq = seq;
+    c.ldseq = (int64_t)c.L * (n_cond + 1);
+    c.logp = logp;
+    hipStream_t user = (hipStream_t)stream;
+    const int D = m->dim, B = n_seqs;
+    // private stream so a hipGraph can be captured regardless of the caller's stream
+    hipStream_t s;
+    SRNN_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    hipEvent_t ev;
+    SRNN_CHECK_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    SRNN_CHECK_HIP(hipEventRecord(ev, user));
+    SRNN_CHECK_HIP(hipStreamWaitEvent(s, ev, 0));
+    c.s = s;
+    int rc = 0;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    do {
+        // 2 * udequantize LUT (bit-exact reference table for mu-law q = 256)
+        {
+            float lut2[256];
+            for (int q = 0; q < 256; ++q) {
+                float v;
+                memcpy(&v, &SRNN_ULAW_LUT_BITS[q], 4);
+                lut2[q] = 2.0f * v;
+            }
+            rc = hipMemcpyAsync(c.b.lut2, lut2, sizeof(lut2), hipMemcpyHostToDevice, s) ? 2 : 0;
+            if (rc) { srnn_set_error("generate: lut upload"); break; }
+            rc = hipMemsetAsync(c.b.base, 0, 64, s) ? 2 : 0;
+            if (rc) break;
+            int L = c.L;
+            rc = hipMemcpyAsync(c.b.base, &L, sizeof(int), hipMemcpyHostToDevice, s) ? 2 : 0;
+            if (rc) break;
+            rc = hipStreamSynchronize(s) ? 2 : 0;   // host staging arrays go out of scope
+            if (rc) break;
+        }
+        // initial hidden states: h0 expanded over rows (model.py:224-228)
+        for (int k = 0; k < m->n_tiers && !rc; ++k)
+            for (int l = 0; l < m->n_rnn; ++l) {
+                const float* h0 = m->tier[k].h0 + (size_t)l * D;
+                if (m->dtype == SRNN_F32)
+                    hipLaunchKernelGGL((init_state_kernel<float>), dim3(cdiv(B * D, 256)),
+                                       dim3(256), 0, s, h0, c.b.h[k][l][0], (float*)nullptr, B, D);
+                else
+                    hipLaunchKernelGGL((init_state_kernel<bf16>), dim3(cdiv(B * D, 256)),
+                                       dim3(256), 0, s, h0, c.b.h[k][l][0],
+                                       (bf16*)c.b.hlp[k][l][0], B, D);
+            }
+        if (rc) break;
+        const bool use_graph = (flags & 1) != 0;
+        int done = 0;
+        const int nblocks = n_cond / 2;
+        if (nblocks > 0) {
+            // first block eagerly (also warms up per-kernel attributes)
+            rc = run_block(c, 2);
+            if (rc) break;
+            done = 1;
+            if (use_graph && nblocks > 1) {
+                if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+                    srnn_set_error("generate: begin capture failed");
+                    rc = 2;
+                    break;
+                }
+                rc = run_block(c, 2);
+                hipError_t ce = hipStreamEndCapture(s, &graph);
+                if (rc) break;
+                if (ce != hipSuccess || hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) !=
+                                            hipSuccess) {
+                    srnn_set_error("generate: graph capture/instantiate failed");
+                    rc = 2;
+                    break;
+                }
+                for (; done < nblocks; ++done) {
+                    if (hipGraphLaunch(exec, s) != hipSuccess) {
+                        srnn_set_error("generate: graph launch failed");
+                        rc = 2;
+                        break;
+                    }
+                }
+                if (rc) break;
+            } else {
+                for (; done < nblocks && !rc; ++done) rc = run_block(c, 2);
+                if (rc) break;
+            }
+        }
+        if (n_cond % 2) rc = run_block(c, 1);
+    } while (0);
+    // the private stream is drained before its resources go (generation is one long call)
+    if (hipStreamSynchronize(s) != hipSuccess && !rc) {
+        srnn_set_error("generate: %s", hipGetErrorString(hipGetLastError()));
+        rc = 2;
+    }
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    (void)hipEventDestroy(ev);
+    (void)hipStreamDestroy(s);
+    return rc;
+}

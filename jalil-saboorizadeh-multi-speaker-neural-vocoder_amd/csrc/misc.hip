@@ -1,0 +1,500 @@
+// Memory-bound support kernels of the hot path: mu-law quantize/dequantize (utils.py),
+// weight-norm forward/backward (torch weight_norm, model.py:119-131,177-178,303-306),
+// layout permutes for the folded weights, row gathers (nn.Embedding), column sums
+// (bias grads), and the fused clip + Adam update (optim.py:4-21, train.py:238).
+#include "samplernn_hip_internal.hpp"
+#include "ulaw_tables.h"
+
+__constant__ uint32_t c_ulaw_f32_steps[256];
+__constant__ uint64_t c_ulaw_f64_thresh[256];
+__constant__ uint32_t c_ulaw_lut[256];
+
+static int g_tables_ready = 0;
+static int ensure_tables() {
+    if (g_tables_ready) return 0;
+    SRNN_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_ulaw_f32_steps), SRNN_ULAW_F32_STEPS_BITS,
+                                     sizeof(SRNN_ULAW_F32_STEPS_BITS)));
+    SRNN_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_ulaw_f64_thresh), SRNN_ULAW_F64_THRESH_BITS,
+                                     sizeof(SRNN_ULAW_F64_THRESH_BITS)));
+    SRNN_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(c_ulaw_lut), SRNN_ULAW_LUT_BITS,
+                                     sizeof(SRNN_ULAW_LUT_BITS)));
+    g_tables_ready = 1;
+    return 0;
+}
+int srnn_init_tables() { return ensure_tables(); }
+
+// ------------------------------------------------------------------ mu-law quantize
+// Bit-exact to utils.uquantize on [-1, 1] by counting reference-derived bin edges
+// (branch-free 8-step binary search); outside [-1, 1] (not audio) the formula in
+// double is used.
+__device__ __forceinline__ int64_t uq_formula(double x, int q) {
+    double s = (x > 0) - (x < 0);
+    double y = s * log(255.0 * fabs(x) + 1.0) / 5.5451774444795623;
+    y = 0.5 * (y + 1.0) * ((double)q - 1e-6);
+    return (int64_t)y;
+}
+
+__global__ void uquantize_f32_kernel(const float* __restrict__ x, int64_t* __restrict__ out,
+                                     int64_t n, int q) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float v = x[i];
+    if (q == 256 && v >= -1.0f && v <= 1.0f) {
+        int lo = 0;  // count of steps <= v
+#pragma unroll
+        for (int s = 128; s > 0; s >>= 1)
+            if (__uint_as_float(c_ulaw_f32_steps[lo + s - 1]) <= v) lo += s;
+        // the loop counts over steps[0..254]; steps[255] (value 256 at x = 1) last
+        if (lo == 255 && __uint_as_float(c_ulaw_f32_steps[255]) <= v) lo = 256;
+        out[i] = lo;
+    } else {
+        // float32 formula path (utils.py:33-36, 48-51) for out-of-domain values
+        float sgn = (float)((v > 0) - (v < 0));
+        float y = sgn * logf(255.0f * fabsf(v) + 1.0f) / 5.5451774444795623f;
+        y = 0.5f * (y + 1.0f);
+        y *= (float)((double)q - 1e-6);
+        out[i] = (int64_t)y;
+    }
+}
+
+__global__ void uquantize_f64_kernel(const double* __restrict__ x, int64_t* __restrict__ out,
+                                     int64_t n, int q) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double v = x[i];
+    if (q == 256 && v >= -1.0 && v <= 1.0) {
+        int lo = 0;
+#pragma unroll
+        for (int s = 128; s > 0; s >>= 1)
+            if (__longlong_as_double((long long)c_ulaw_f64_thresh[lo + s - 1]) <= v) lo += s;
+        out[i] = lo;
+    } else {
+        out[i] = uq_formula(v, q);
+    }
+}
+
+// mode 0: mu-law (utils.py:62-63, LUT for q = 256), mode 1: linear (utils.py:18-19)
+__global__ void udequantize_kernel(const int64_t* __restrict__ k, float* __restrict__ out,
+                                   int64_t n, int q, float scale, int mode) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int64_t kk = k[i];
+    float v;
+    if (mode == 1) {
+        v = (float)kk / (float)(q / 2) - 1.0f;
+    } else if (q == 256 && kk >= 0 && kk < 256) {
+        v = __uint_as_float(c_ulaw_lut[kk]);
+    } else {
+        float c = (float)kk * 2.0f / (float)q - 1.0f;
+        float e = expf(fabsf(c) * 5.5451774444795623f) - 1.0f;
+        v = (float)((c > 0) - (c < 0)) * e / 255.0f;
+    }
+    out[i] = scale * v;
+}
+
+extern "C" int srnn_uquantize_f32(const float* x, int64_t* out, int64_t n, int q, void* stream) {
+    if (int e = ensure_tables()) return e;
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(uquantize_f32_kernel, dim3(cdiv(n, 256)), dim3(256), 0,
+                       (hipStream_t)stream, x, out, n, q);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+extern "C" int srnn_uquantize_f64(const double* x, int64_t* out, int64_t n, int q, void* stream) {
+    if (int e = ensure_tables()) return e;
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(uquantize_f64_kernel, dim3(cdiv(n, 256)), dim3(256), 0,
+                       (hipStream_t)stream, x, out, n, q);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+extern "C" int srnn_udequantize(const int64_t* k, float* out, int64_t n, int q, float scale,
+                                int mode, void* stream) {
+    if (int e = ensure_tables()) return e;
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(udequantize_kernel, dim3(cdiv(n, 256)), dim3(256), 0,
+                       (hipStream_t)stream, k, out, n, q, scale, mode);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// host (CPU) forms with the same tables: the DataLoader-side quantiser (dataset.py:253-254)
+static int64_t uq_host_f64(double v, int q) {
+    if (q == 256 && v >= -1.0 && v <= 1.0) {
+        int lo = 0;
+        for (int s = 128; s > 0; s >>= 1) {
+            double t;
+            memcpy(&t, &SRNN_ULAW_F64_THRESH_BITS[lo + s - 1], 8);
+            if (t <= v) lo += s;
+        }
+        return lo;
+    }
+    double s = (v > 0) - (v < 0);
+    double y = s * log(255.0 * fabs(v) + 1.0) / 5.5451774444795623;
+    y = 0.5 * (y + 1.0) * ((double)q - 1e-6);
+    return (int64_t)y;
+}
+static int64_t uq_host_f32(float v, int q) {
+    if (q == 256 && v >= -1.0f && v <= 1.0f) {
+        int lo = 0;
+        for (int s = 128; s > 0; s >>= 1) {
+            float t;
+            memcpy(&t, &SRNN_ULAW_F32_STEPS_BITS[lo + s - 1], 4);
+            if (t <= v) lo += s;
+        }
+        float t255;
+        memcpy(&t255, &SRNN_ULAW_F32_STEPS_BITS[255], 4);
+        if (lo == 255 && t255 <= v) lo = 256;
+        return lo;
+    }
+    float sg = (float)((v > 0) - (v < 0));
+    float y = sg * logf(255.0f * fabsf(v) + 1.0f) / 5.5451774444795623f;
+    y = 0.5f * (y + 1.0f);
+    y *= (float)((double)q - 1e-6);
+    return (int64_t)y;
+}
+extern "C" int srnn_uquantize_f64_host(const double* x, int64_t* out, int64_t n, int q) {
+    for (int64_t i = 0; i < n; ++i) out[i] = uq_host_f64(x[i], q);
+    return 0;
+}
+extern "C" int srnn_uquantize_f32_host(const float* x, int64_t* out, int64_t n, int q) {
+    for (int64_t i = 0; i < n; ++i) out[i] = uq_host_f32(x[i], q);
+    return 0;
+}
+extern "C" int srnn_udequantize_host(const int64_t* k, float* out, int64_t n, int q) {
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t kk = k[i];
+        if (q == 256 && kk >= 0 && kk < 256) {
+            memcpy(&out[i], &SRNN_ULAW_LUT_BITS[kk], 4);
+        } else {
+            float c = (float)kk * 2.0f / (float)q - 1.0f;
+            float e = expf(fabsf(c) * 5.5451774444795623f) - 1.0f;
+            out[i] = (float)((c > 0) - (c < 0)) * e / 255.0f;
+        }
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------ weight norm
+// w[o, r] = g[o] * v[o, r] / ||v[o, :]||   (norm over all dims but 0; one block per o)
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) sh[w] = v;
+    __syncthreads();
+    float t = 0.f;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += sh[i];
+    return t;
+}
+
+__global__ void wn_fwd_kernel(const float* __restrict__ g, const float* __restrict__ v,
+                              float* __restrict__ w, float* __restrict__ norm, int64_t R) {
+    __shared__ float sh[16];
+    const int64_t o = blockIdx.x;
+    const float* vr = v + o * R;
+    float s = 0.f;
+    for (int64_t r = threadIdx.x; r < R; r += blockDim.x) s += vr[r] * vr[r];
+    s = block_sum(s, sh);
+    const float nrm = sqrtf(s);
+    const float scale = g[o] / nrm;
+    if (norm && threadIdx.x == 0) norm[o] = nrm;
+    for (int64_t r = threadIdx.x; r < R; r += blockDim.x) w[o * R + r] = vr[r] * scale;
+}
+
+// dg[o] = sum_r dw v / n ;  dv = (g/n) (dw - (dg/n) v)
+__global__ void wn_bwd_kernel(const float* __restrict__ g, const float* __restrict__ v,
+                              const float* __restrict__ dw, float* __restrict__ dg,
+                              float* __restrict__ dv, int64_t R, int accumulate) {
+    __shared__ float sh[16];
+    const int64_t o = blockIdx.x;
+    const float* vr = v + o * R;
+    const float* dr = dw + o * R;
+    float s = 0.f, d = 0.f;
+    for (int64_t r = threadIdx.x; r < R; r += blockDim.x) {
+        s += vr[r] * vr[r];
+        d += dr[r] * vr[r];
+    }
+    s = block_sum(s, sh);
+    d = block_sum(d, sh);
+    const float n = sqrtf(s);
+    const float dgo = d / n;
+    const float gn = g[o] / n;
+    if (threadIdx.x == 0) dg[o] = accumulate ? dg[o] + dgo : dgo;
+    for (int64_t r = threadIdx.x; r < R; r += blockDim.x) {
+        float val = gn * (dr[r] - dgo / n * vr[r]);
+        dv[o * R + r] = accumulate ? dv[o * R + r] + val : val;
+    }
+}
+
+extern "C" int srnn_weight_norm_fwd(const float* g, const float* v, float* w, float* norm, int O,
+                                    int64_t R, void* stream) {
+    if (O <= 0) return 0;
+    hipLaunchKernelGGL(wn_fwd_kernel, dim3(O), dim3(256), 0, (hipStream_t)stream, g, v, w, norm, R);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+extern "C" int srnn_weight_norm_bwd(const float* g, const float* v, const float* dw, float* dg,
+                                    float* dv, int O, int64_t R, int accumulate, void* stream) {
+    if (O <= 0) return 0;
+    hipLaunchKernelGGL(wn_bwd_kernel, dim3(O), dim3(256), 0, (hipStream_t)stream, g, v, dw, dg, dv,
+                       R, accumulate);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// ------------------------------------------------------------------ layout permutes
+// dst[p-order index] = src[(i0, i1, i2)], src dims (d0, d1, d2) row-major; `perm` gives
+// which src axis becomes dst axis 0/1/2.  Converts fp32 -> fp32 / bf16.
+template <typename TO, bool ACC>
+__global__ void permute3_kernel(const float* __restrict__ src, TO* __restrict__ dst, int d0,
+                                int d1, int d2, int p0, int p1, int p2) {
+    const int64_t n = (int64_t)d0 * d1 * d2;
+    int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= n) return;
+    const int dims[3] = {d0, d1, d2};
+    const int od1 = dims[p1], od2 = dims[p2];
+    const int a2 = idx % od2;
+    const int a1 = (idx / od2) % od1;
+    const int a0 = idx / ((int64_t)od2 * od1);
+    int s[3];
+    s[p0] = a0; s[p1] = a1; s[p2] = a2;
+    const float val = src[((int64_t)s[0] * d1 + s[1]) * d2 + s[2]];
+    if (ACC) dst[idx] = from_f<TO>(to_f(dst[idx]) + val);
+    else dst[idx] = from_f<TO>(val);
+}
+
+extern "C" int srnn_permute3(const float* src, void* dst, int dst_dtype, int d0, int d1, int d2,
+                             int p0, int p1, int p2, int accumulate, void* stream) {
+    const int64_t n = (int64_t)d0 * d1 * d2;
+    if (n <= 0) return 0;
+    SRNN_REQUIRE(p0 + p1 + p2 == 3 && p0 != p1 && p1 != p2 && p0 != p2, "permute3: bad perm");
+    dim3 grid(cdiv(n, 256));
+    hipStream_t s = (hipStream_t)stream;
+    if (dst_dtype == SRNN_F32) {
+        if (accumulate)
+            hipLaunchKernelGGL((permute3_kernel<float, true>), grid, dim3(256), 0, s, src,
+                               (float*)dst, d0, d1, d2, p0, p1, p2);
+        else
+            hipLaunchKernelGGL((permute3_kernel<float, false>), grid, dim3(256), 0, s, src,
+                               (float*)dst, d0, d1, d2, p0, p1, p2);
+    } else {
+        SRNN_REQUIRE(!accumulate, "permute3: accumulate needs fp32 dst");
+        hipLaunchKernelGGL((permute3_kernel<bf16, false>), grid, dim3(256), 0, s, src, (bf16*)dst,
+                           d0, d1, d2, p0, p1, p2);
+    }
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// 2-D strided copy with dtype conversion (fp32 -> fp32/bf16, bf16 -> fp32)
+template <typename TI, typename TO>
+__global__ void copy2d_kernel(const TI* __restrict__ src, int64_t lds, TO* __restrict__ dst,
+                              int64_t ldd, int rows, int cols) {
+    int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (int64_t)rows * cols) return;
+    int r = idx / cols, c = idx % cols;
+    dst[(int64_t)r * ldd + c] = from_f<TO>(to_f(src[(int64_t)r * lds + c]));
+}
+
+extern "C" int srnn_copy2d(int src_dtype, int dst_dtype, int rows, int cols, const void* src,
+                           int64_t lds, void* dst, int64_t ldd, void* stream) {
+    const int64_t n = (int64_t)rows * cols;
+    if (n <= 0) return 0;
+    dim3 grid(cdiv(n, 256));
+    hipStream_t s = (hipStream_t)stream;
+    if (src_dtype == SRNN_F32 && dst_dtype == SRNN_F32)
+        hipLaunchKernelGGL((copy2d_kernel<float, float>), grid, dim3(256), 0, s, (const float*)src,
+                           lds, (float*)dst, ldd, rows, cols);
+    else if (src_dtype == SRNN_F32 && dst_dtype == SRNN_BF16)
+        hipLaunchKernelGGL((copy2d_kernel<float, bf16>), grid, dim3(256), 0, s, (const float*)src,
+                           lds, (bf16*)dst, ldd, rows, cols);
+    else if (src_dtype == SRNN_BF16 && dst_dtype == SRNN_F32)
+        hipLaunchKernelGGL((copy2d_kernel<bf16, float>), grid, dim3(256), 0, s, (const bf16*)src,
+                           lds, (float*)dst, ldd, rows, cols);
+    else
+        hipLaunchKernelGGL((copy2d_kernel<bf16, bf16>), grid, dim3(256), 0, s, (const bf16*)src,
+                           lds, (bf16*)dst, ldd, rows, cols);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// ------------------------------------------------------------------ gathers / adds
+// out[r, :] = table[idx[r], :]   (nn.Embedding forward, model.py:103-106, 274-277)
+template <typename T>
+__global__ void gather_rows_kernel(const float* __restrict__ table, int64_t ldt,
+                                   const int64_t* __restrict__ idx, int64_t n, int cols,
+                                   T* __restrict__ out, int64_t ldo) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * cols) return;
+    int64_t r = e / cols;
+    int c = e % cols;
+    out[r * ldo + c] = from_f<T>(table[idx[r] * ldt + c]);
+}
+
+extern "C" int srnn_gather_rows(const float* table, int64_t ldt, const int64_t* idx, int64_t n,
+                                int cols, void* out, int out_dtype, int64_t ldo, void* stream) {
+    if (n * cols <= 0) return 0;
+    dim3 grid(cdiv(n * cols, 256));
+    if (out_dtype == SRNN_F32)
+        hipLaunchKernelGGL((gather_rows_kernel<float>), grid, dim3(256), 0, (hipStream_t)stream,
+                           table, ldt, idx, n, cols, (float*)out, ldo);
+    else
+        hipLaunchKernelGGL((gather_rows_kernel<bf16>), grid, dim3(256), 0, (hipStream_t)stream,
+                           table, ldt, idx, n, cols, (bf16*)out, ldo);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// table[idx[r], :] += src[r, :]  (embedding backward; fp32 atomics, few rows)
+__global__ void scatter_add_rows_kernel(float* __restrict__ table, int64_t ldt,
+                                        const int64_t* __restrict__ idx, int64_t n, int cols,
+                                        const float* __restrict__ src, int64_t lds) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n * cols) return;
+    int64_t r = e / cols;
+    int c = e % cols;
+    atomicAdd(&table[idx[r] * ldt + c], src[r * lds + c]);
+}
+
+extern "C" int srnn_scatter_add_rows(float* table, int64_t ldt, const int64_t* idx, int64_t n,
+                                     int cols, const float* src, int64_t lds, void* stream) {
+    if (n * cols <= 0) return 0;
+    hipLaunchKernelGGL(scatter_add_rows_kernel, dim3(cdiv(n * cols, 256)), dim3(256), 0,
+                       (hipStream_t)stream, table, ldt, idx, n, cols, src, lds);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// out = alpha * a + beta * b  (fp32, elementwise; out may alias a or b)
+__global__ void axpby_kernel(float* out, const float* a, const float* b, float alpha, float beta,
+                             int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = alpha * a[i] + (b ? beta * b[i] : 0.f);
+}
+
+extern "C" int srnn_axpby(float* out, const float* a, const float* b, float alpha, float beta,
+                          int64_t n, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(axpby_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, out, a,
+                       b, alpha, beta, n);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// x[b, f, :] += v[b, :]  for x (B, F, D) with row stride ldx per (b, f)
+__global__ void add_bcast_rows_kernel(float* __restrict__ x, const float* __restrict__ v, int B,
+                                      int F, int D, int64_t ldv) {
+    int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)B * F * D) return;
+    int d = e % D;
+    int64_t bf = e / D;
+    int b = bf / F;
+    x[e] += v[(int64_t)b * ldv + d];
+}
+
+extern "C" int srnn_add_bcast_rows(float* x, const float* v, int B, int F, int D, int64_t ldv,
+                                   void* stream) {
+    if ((int64_t)B * F * D <= 0) return 0;
+    hipLaunchKernelGGL(add_bcast_rows_kernel, dim3(cdiv((int64_t)B * F * D, 256)), dim3(256), 0,
+                       (hipStream_t)stream, x, v, B, F, D, ldv);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// ------------------------------------------------------------------ column sums
+// partial[rb, c] = sum_{r in row block rb} src[r, c]  then out[c] (+)= sum_rb partial
+template <typename T>
+__global__ void colsum_partial_kernel(const T* __restrict__ src, int64_t lds, int64_t rows,
+                                      int cols, int rows_per_block, float* __restrict__ partial) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= cols) return;
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+    const int64_t r1 = min(rows, r0 + rows_per_block);
+    float s = 0.f;
+    for (int64_t r = r0; r < r1; ++r) s += to_f(src[r * lds + c]);
+    partial[(int64_t)blockIdx.y * cols + c] = s;
+}
+
+__global__ void colsum_final_kernel(const float* __restrict__ partial, int nrb, int cols,
+                                    float* __restrict__ out, float alpha, int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= cols) return;
+    float s = 0.f;
+    for (int i = 0; i < nrb; ++i) s += partial[(int64_t)i * cols + c];
+    out[c] = accumulate ? out[c] + alpha * s : alpha * s;
+}
+
+int srnn_colsum_impl(int dtype, const void* src, int64_t lds, int64_t rows, int cols, float* out,
+                     float alpha, int accumulate, float* work, int64_t work_elems, hipStream_t s) {
+    if (cols <= 0) return 0;
+    int rpb = 256;
+    int nrb = (int)((rows + rpb - 1) / rpb);
+    while ((int64_t)nrb * cols > work_elems && rpb < (1 << 30)) {
+        rpb *= 2;
+        nrb = (int)((rows + rpb - 1) / rpb);
+    }
+    SRNN_REQUIRE((int64_t)nrb * cols <= work_elems, "colsum: workspace too small");
+    if (nrb == 0) nrb = 1;
+    dim3 g1(cdiv(cols, 256), nrb);
+    if (dtype == SRNN_F32)
+        hipLaunchKernelGGL((colsum_partial_kernel<float>), g1, dim3(256), 0, s, (const float*)src,
+                           lds, rows, cols, rpb, work);
+    else
+        hipLaunchKernelGGL((colsum_partial_kernel<bf16>), g1, dim3(256), 0, s, (const bf16*)src,
+                           lds, rows, cols, rpb, work);
+    SRNN_LAUNCH_CHECK();
+    hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(cols, 256)), dim3(256), 0, s, work, nrb, cols,
+                       out, alpha, accumulate);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int srnn_colsum(int dtype, const void* src, int64_t lds, int64_t rows, int cols,
+                           float* out, float alpha, int accumulate, float* work,
+                           int64_t work_elems, void* stream) {
+    return srnn_colsum_impl(dtype, src, lds, rows, cols, out, alpha, accumulate, work, work_elems,
+                            (hipStream_t)stream);
+}
+
+// ------------------------------------------------------------------ clip + Adam
+// optim.py:11-13 clamps every grad to [lo, hi]; then torch.optim.Adam (single-tensor
+// form, torch 2.x order): m.lerp_(g, 1-b1); v = v*b2 + (1-b2)*g*g;
+// p -= step_size * m / (sqrt(v)/sqrt(bc2) + eps).  Optionally refreshes a bf16 copy.
+__global__ void adam_clip_kernel(float* __restrict__ p, float* __restrict__ g,
+                                 float* __restrict__ m, float* __restrict__ v,
+                                 bf16* __restrict__ p_lp, int64_t n, float lo, float hi, float w1,
+                                 float b2, float omb2, float step_size, float bc2s, float eps) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float gi = fminf(fmaxf(g[i], lo), hi);
+    g[i] = gi;   // hardtanh_ is in place in the reference (optim.py:13)
+    float mi = m[i];
+    mi = mi + w1 * (gi - mi);
+    float vi = v[i] * b2;
+    vi = vi + omb2 * gi * gi;
+    float denom = sqrtf(vi) / bc2s + eps;
+    float pi = p[i] + (-step_size) * mi / denom;
+    m[i] = mi;
+    v[i] = vi;
+    p[i] = pi;
+    if (p_lp) p_lp[i] = __float2bfloat16(pi);
+}
+
+extern "C" int srnn_adam_clip(float* p, float* g, float* m, float* v, void* p_bf16,
+                              int64_t n, float clip_lo, float clip_hi, double lr, double beta1,
+                              double beta2, double eps, int64_t step, void* stream) {
+    if (n <= 0) return 0;
+    SRNN_REQUIRE(step >= 1, "adam: step must be >= 1");
+    const double bc1 = 1.0 - pow(beta1, (double)step);
+    const double bc2 = 1.0 - pow(beta2, (double)step);
+    const float step_size = (float)(lr / bc1);
+    const float bc2s = (float)sqrt(bc2);
+    hipLaunchKernelGGL(adam_clip_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, p,
+                       g, m, v, (bf16*)p_bf16, n, clip_lo, clip_hi, (float)(1.0 - beta1),
+                       (float)beta2, (float)(1.0 - beta2), step_size, bc2s, (float)eps);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}

@@ -1,0 +1,369 @@
+// SampleLevelMLP kernels (model.py:266-325) and the loss / sampler around it.
+//
+// The embedding (Q x Q) followed by the FS0-tap Conv1d (D x Q x FS0, no bias) is a
+// linear map of one-hot inputs, so it is folded into a per-tap table
+//     Tab[k][q][:] = W[:, :, k] . E[q, :]          (FS0 x Q x D, built by one batched GEMM)
+// and the first MLP layer becomes a 16-row gather-sum:  a1 = relu(sum_k Tab[k][x_{t+k}] + u_t).
+// That removes the Q*FS0*D = 4.2 M MAC/sample dense conv (59 % of the reference's MLP
+// FLOPs) from both the training and the generation path.
+//
+// The log-softmax + NLL (nn.py:66-70) is one wave per row (Q = 256 -> 4 values / lane,
+// wave shuffles for max / sum) and writes the loss row and dlogits in the same pass.
+// The generation sampler draws  argmax(exp(logp) / q), q ~ Exp(1)  -- exactly how
+// torch>=2 implements `multinomial(1)` on CPU (model.py:514-517) -- with q either
+// supplied (bit-replay of the reference's RNG) or from a counter-based Philox4x32-10.
+#include "samplernn_hip_internal.hpp"
+
+// ------------------------------------------------------------------ L1 gather
+// rows r = b * Tlen + t;  idx_k = x[b * ldx + xoff(+base) + t + k]
+template <typename T, int VPT>
+__global__ __launch_bounds__(256) void mlp_l1_kernel(const T* __restrict__ tab,
+                                                     const int64_t* __restrict__ x, int64_t ldx,
+                                                     int xoff, const int* __restrict__ base,
+                                                     int Tlen, const float* __restrict__ upper,
+                                                     int64_t ldu, T* __restrict__ out, int64_t ldo,
+                                                     int D, int FS0, int Q) {
+    const int64_t r = blockIdx.y;
+    const int b = r / Tlen, t = r % Tlen;
+    const int off = xoff + (base ? *base : 0);
+    const int64_t* xr = x + (int64_t)b * ldx + off + t;
+    const int o0 = (blockIdx.x * 256 + threadIdx.x) * VPT;
+    if (o0 >= D) return;
+    float acc[VPT];
+    const float* ur = upper + r * ldu + o0;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) acc[j] = ur[j];
+    for (int k = 0; k < FS0; ++k) {
+        const int64_t q = xr[k];
+        const T* tr = tab + ((int64_t)k * Q + q) * D + o0;
+#pragma unroll
+        for (int j = 0; j < VPT; ++j) acc[j] += to_f(tr[j]);
+    }
+    T* orow = out + r * ldo + o0;
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) orow[j] = from_f<T>(fmaxf(acc[j], 0.f));
+}
+
+int srnn_mlp_l1_impl(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff,
+                     const int* base, int B, int Tlen, const float* upper, int64_t ldu, void* out,
+                     int64_t ldo, int D, int FS0, int Q, hipStream_t s) {
+    SRNN_REQUIRE(D % 4 == 0, "mlp_l1: D must be a multiple of 4");
+    dim3 grid(cdiv(D, 256 * 4), (int64_t)B * Tlen);
+    if (dtype == SRNN_F32)
+        hipLaunchKernelGGL((mlp_l1_kernel<float, 4>), grid, dim3(256), 0, s, (const float*)tab, x,
+                           ldx, xoff, base, Tlen, upper, ldu, (float*)out, ldo, D, FS0, Q);
+    else
+        hipLaunchKernelGGL((mlp_l1_kernel<bf16, 4>), grid, dim3(256), 0, s, (const bf16*)tab, x,
+                           ldx, xoff, base, Tlen, upper, ldu, (bf16*)out, ldo, D, FS0, Q);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int srnn_mlp_l1(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff,
+                           int B, int Tlen, const float* upper, int64_t ldu, void* out,
+                           int64_t ldo, int D, int FS0, int Q, void* stream) {
+    return srnn_mlp_l1_impl(dtype, tab, x, ldx, xoff, nullptr, B, Tlen, upper, ldu, out, ldo, D,
+                            FS0, Q, (hipStream_t)stream);
+}
+
+// ------------------------------------------------------------------ wave helpers
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// ------------------------------------------------------------------ log-softmax + NLL
+// One wave per row (Q = 256: lane holds q = lane + 64 j).  Writes
+//   loss_row[r] = lse - z[target]     (if loss_row)
+//   logp[r, q]  = (z - max) - log(sum exp(z - max))   (if logp; torch CPU op order)
+//   dz[r, q]    = (softmax - onehot) * gscale        (if dz; T dtype)
+template <typename TG>
+__global__ __launch_bounds__(256) void logsoftmax_nll_kernel(
+    const float* __restrict__ z, int64_t ldz, const int64_t* __restrict__ target, int64_t ldt,
+    int Tlen, int64_t rows, float* __restrict__ loss_row, float* __restrict__ logp, int64_t ldl,
+    TG* __restrict__ dz, int64_t ldd, float gscale) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= rows) return;
+    const float* zr = z + r * ldz;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = zr[lane + 64 * j];
+    float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+    m = wave_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += expf(v[j] - m);
+    s = wave_sum(s);
+    const float ls = logf(s);
+    int64_t tgt = -1;
+    if (target) {
+        const int b = r / Tlen, t = r % Tlen;
+        tgt = target[(int64_t)b * ldt + t];
+    }
+    if (logp) {
+        float* lr = logp + r * ldl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) lr[lane + 64 * j] = (v[j] - m) - ls;
+    }
+    if (loss_row && lane == (int)(tgt & 63)) {
+        const int j = (int)(tgt >> 6);
+        float vt = v[0];
+#pragma unroll
+        for (int jj = 1; jj < 4; ++jj) if (jj == j) vt = v[jj];
+        loss_row[r] = -((vt - m) - ls);
+    }
+    if (dz) {
+        TG* dr = dz + r * ldd;
+        const float inv = 1.0f / s;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int q = lane + 64 * j;
+            float p = expf(v[j] - m) * inv;
+            if (q == tgt) p -= 1.0f;
+            dr[q] = from_f<TG>(p * gscale);
+        }
+    }
+}
+
+extern "C" int srnn_logsoftmax_nll(const float* z, int64_t ldz, const int64_t* target, int64_t ldt,
+                                   int Tlen, int64_t rows, int Q, float* loss_row, float* logp,
+                                   int64_t ldl, void* dz, int dz_dtype, int64_t ldd, float gscale,
+                                   void* stream) {
+    SRNN_REQUIRE(Q == 256, "logsoftmax_nll: q_levels must be 256");
+    SRNN_REQUIRE(!(loss_row || dz) || target, "logsoftmax_nll: loss/grad needs target");
+    if (rows <= 0) return 0;
+    dim3 grid(cdiv(rows, 4));
+    hipStream_t s = (hipStream_t)stream;
+    if (dz_dtype == SRNN_BF16)
+        hipLaunchKernelGGL((logsoftmax_nll_kernel<bf16>), grid, dim3(256), 0, s, z, ldz, target,
+                           ldt, Tlen, rows, loss_row, logp, ldl, (bf16*)dz, ldd, gscale);
+    else
+        hipLaunchKernelGGL((logsoftmax_nll_kernel<float>), grid, dim3(256), 0, s, z, ldz, target,
+                           ldt, Tlen, rows, loss_row, logp, ldl, (float*)dz, ldd, gscale);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// dz = dlogp - exp(logp) * sum(dlogp)   (one wave per row)
+template <typename TG>
+__global__ __launch_bounds__(256) void logsoftmax_bwd_kernel(const float* __restrict__ dl,
+                                                             int64_t lddl,
+                                                             const float* __restrict__ lp,
+                                                             int64_t ldl, int64_t rows,
+                                                             TG* __restrict__ dz, int64_t ldd) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= rows) return;
+    float g[4], p[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        g[j] = dl[r * lddl + lane + 64 * j];
+        p[j] = lp[r * ldl + lane + 64 * j];
+    }
+    float s = wave_sum(g[0] + g[1] + g[2] + g[3]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dz[r * ldd + lane + 64 * j] = from_f<TG>(g[j] - expf(p[j]) * s);
+}
+
+extern "C" int srnn_logsoftmax_bwd(const float* dlogp, int64_t lddl, const float* logp,
+                                   int64_t ldl, int64_t rows, int Q, void* dz, int dz_dtype,
+                                   int64_t ldd, void* stream) {
+    SRNN_REQUIRE(Q == 256, "logsoftmax_bwd: q_levels must be 256");
+    if (rows <= 0) return 0;
+    dim3 grid(cdiv(rows, 4));
+    if (dz_dtype == SRNN_BF16)
+        hipLaunchKernelGGL((logsoftmax_bwd_kernel<bf16>), grid, dim3(256), 0, (hipStream_t)stream,
+                           dlogp, lddl, logp, ldl, rows, (bf16*)dz, ldd);
+    else
+        hipLaunchKernelGGL((logsoftmax_bwd_kernel<float>), grid, dim3(256), 0,
+                           (hipStream_t)stream, dlogp, lddl, logp, ldl, rows, (float*)dz, ldd);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+__global__ void nll_fwd_kernel(const float* __restrict__ lp, int64_t ldl,
+                               const int64_t* __restrict__ target, int64_t ldt, int Tlen,
+                               int64_t rows, float* __restrict__ loss_row) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rows) return;
+    const int64_t b = r / Tlen, t = r % Tlen;
+    loss_row[r] = -lp[r * ldl + target[b * ldt + t]];
+}
+
+__global__ void nll_bwd_kernel(const int64_t* __restrict__ target, int64_t ldt, int Tlen,
+                               int64_t rows, int Q, float* __restrict__ dl, int64_t ldd,
+                               float gscale) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= rows * Q) return;
+    const int64_t r = e / Q;
+    const int q = e % Q;
+    const int64_t b = r / Tlen, t = r % Tlen;
+    dl[r * ldd + q] = (q == target[b * ldt + t]) ? -gscale : 0.f;
+}
+
+extern "C" int srnn_nll_fwd(const float* logp, int64_t ldl, const int64_t* target, int64_t ldt,
+                            int Tlen, int64_t rows, float* loss_row, void* stream) {
+    if (rows <= 0) return 0;
+    hipLaunchKernelGGL(nll_fwd_kernel, dim3(cdiv(rows, 256)), dim3(256), 0, (hipStream_t)stream,
+                       logp, ldl, target, ldt, Tlen, rows, loss_row);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int srnn_nll_bwd(const int64_t* target, int64_t ldt, int Tlen, int64_t rows, int Q,
+                            float* dlogp, int64_t ldd, float gscale, void* stream) {
+    if (rows <= 0) return 0;
+    hipLaunchKernelGGL(nll_bwd_kernel, dim3(cdiv(rows * Q, 256)), dim3(256), 0,
+                       (hipStream_t)stream, target, ldt, Tlen, rows, Q, dlogp, ldd, gscale);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// ------------------------------------------------------------------ sampler
+// Philox4x32-10 (Salmon et al. 2011): counter = (q/4, row, step, 0), key = seed.
+__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t lo0 = c.x * 0xD2511F53u, hi0 = __umulhi(c.x, 0xD2511F53u);
+        const uint32_t lo1 = c.z * 0xCD9E8D57u, hi1 = __umulhi(c.z, 0xCD9E8D57u);
+        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
+        k.x += 0x9E3779B9u;
+        k.y += 0xBB67AE85u;
+    }
+    return c;
+}
+
+// Exp(1) from a 32-bit draw: u in (0, 1], q = -log(u)
+__device__ __forceinline__ float exp1_from_u32(uint32_t x) {
+    const float u = ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
+    return -logf(u);
+}
+
+// One wave per row; lane holds q = 4 * lane + j (16-B loads of logits and noise).
+__global__ __launch_bounds__(256) void sample_kernel(
+    const float* __restrict__ z, int64_t ldz, int B, const float* __restrict__ noise,
+    uint64_t seed, const int* __restrict__ base, int off, int L, int64_t* __restrict__ seq,
+    int64_t ldseq, float* __restrict__ logp_out) {
+    const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (b >= B) return;
+    const int i = *base + off;        // absolute sample index being generated
+    const int step = i - L;
+    const floatx4 v = *reinterpret_cast<const floatx4*>(z + (int64_t)b * ldz + 4 * lane);
+    float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+    m = wave_max(m);
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += expf(v[j] - m);
+    s = wave_sum(s);
+    const float ls = logf(s);
+    floatx4 q;
+    if (noise) {
+        q = *reinterpret_cast<const floatx4*>(noise + ((int64_t)step * B + b) * 256 + 4 * lane);
+    } else {
+        const uint4 rnd = philox4x32(make_uint4((uint32_t)lane, (uint32_t)b, (uint32_t)step, 0u),
+                                     make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
+        q = floatx4{exp1_from_u32(rnd.x), exp1_from_u32(rnd.y), exp1_from_u32(rnd.z),
+                    exp1_from_u32(rnd.w)};
+    }
+    float best = -1.0f;
+    int bi = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const float lp = (v[j] - m) - ls;
+        if (logp_out) logp_out[((int64_t)step * B + b) * 256 + 4 * lane + j] = lp;
+        const float r = expf(lp) / q[j];
+        if (r > best) { best = r; bi = 4 * lane + j; }
+    }
+    // wave argmax, first index on ties (torch argmax)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bi, o);
+        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if (lane == 0) seq[(int64_t)b * ldseq + i] = bi;
+}
+
+int srnn_sample_impl(const float* z, int64_t ldz, int B, const float* noise, uint64_t seed,
+                     const int* base, int off, int L, int64_t* seq, int64_t ldseq,
+                     float* logp_out, hipStream_t s) {
+    hipLaunchKernelGGL(sample_kernel, dim3(cdiv(B, 4)), dim3(256), 0, s, z, ldz, B, noise, seed,
+                       base, off, L, seq, ldseq, logp_out);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// ------------------------------------------------------------------ dTab scatter
+// dTab[x_{b, t+k}][k][:] += da[b, t, :]  over all rows: per (row block, 64-column slice)
+// the workgroup accumulates into an LDS copy of dTab[:, :, slice] (FS0*Q*64 fp32 would be
+// 1 MiB for FS0=16, so the slice is 8 columns: 16*256*8*4 = 128 KiB) with LDS atomics,
+// then flushes it with global atomics.
+template <typename T>
+__global__ __launch_bounds__(256) void dtab_kernel(const T* __restrict__ da, int64_t ldda,
+                                                   const int64_t* __restrict__ x, int64_t ldx,
+                                                   int xoff, int Tlen, int64_t rows,
+                                                   int rows_per_block, float* __restrict__ dtab,
+                                                   int D, int FS0, int Q) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* acc = reinterpret_cast<float*>(smem);   // [FS0][Q][8]
+    const int c0 = blockIdx.x * 8;
+    const int n = FS0 * Q * 8;
+    for (int i = threadIdx.x; i < n; i += 256) acc[i] = 0.f;
+    __syncthreads();
+    const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+    const int64_t r1 = min(rows, r0 + rows_per_block);
+    // each thread: one (row, column) pair per iteration; 32 rows x 8 cols per pass
+    const int cc = threadIdx.x & 7;
+    for (int64_t r = r0 + (threadIdx.x >> 3); r < r1; r += 32) {
+        const int b = r / Tlen, t = r % Tlen;
+        const int64_t* xr = x + (int64_t)b * ldx + xoff + t;
+        const float g = (c0 + cc < D) ? to_f(da[r * ldda + c0 + cc]) : 0.f;
+        if (g != 0.f) {
+            for (int k = 0; k < FS0; ++k) atomicAdd(&acc[(k * Q + (int)xr[k]) * 8 + cc], g);
+        }
+    }
+    __syncthreads();
+    // flush q-major: dtab[(q * FS0 + k) * D + c]  (the layout the dE GEMM consumes)
+    for (int i = threadIdx.x; i < n; i += 256) {
+        const float v = acc[i];
+        const int c = c0 + (i & 7);
+        const int kq = i >> 3, k = kq / Q, q = kq % Q;
+        if (v != 0.f && c < D) atomicAdd(&dtab[((int64_t)q * FS0 + k) * D + c], v);
+    }
+}
+
+extern "C" int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x,
+                             int64_t ldx, int xoff, int B, int Tlen, float* dtab, int D, int FS0,
+                             int Q, void* stream) {
+    const int64_t rows = (int64_t)B * Tlen;
+    if (rows <= 0) return 0;
+    const int lds = FS0 * Q * 8 * 4;
+    SRNN_REQUIRE(lds <= 160 * 1024, "dtab: FS0*Q too large for LDS");
+    const int rpb = 2048;
+    dim3 grid(cdiv(D, 8), cdiv(rows, rpb));
+    hipStream_t s = (hipStream_t)stream;
+    static bool attr = false;
+    if (!attr) {
+        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_kernel<float>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_kernel<bf16>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    if (dtype == SRNN_F32)
+        hipLaunchKernelGGL((dtab_kernel<float>), grid, dim3(256), lds, s, (const float*)da, ldda, x,
+                           ldx, xoff, Tlen, rows, rpb, dtab, D, FS0, Q);
+    else
+        hipLaunchKernelGGL((dtab_kernel<bf16>), grid, dim3(256), lds, s, (const bf16*)da, ldda, x,
+                           ldx, xoff, Tlen, rows, rpb, dtab, D, FS0, Q);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}

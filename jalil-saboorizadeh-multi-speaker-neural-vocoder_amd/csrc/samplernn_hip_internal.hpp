@@ -1,0 +1,19 @@
+// Internal (C++) entry points shared between translation units of the library.
+#pragma once
+#include "common.hpp"
+
+int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
+                   float alpha, const void* A, int64_t lda, int64_t strideA, const void* B,
+                   int64_t ldb, int64_t strideB, float beta, const float* Cin, int64_t ldcin,
+                   int64_t strideCin, void* C, int64_t ldc, int64_t strideC, const float* bias,
+                   int bias_mode, int relu, int batch, int tile, hipStream_t s,
+                   const void* mask = nullptr, int64_t ldmask = 0);
+
+// y[M,N] = act(x[M,K] . W[N,K]^T + bias)   (nn.Linear / Conv1d(k=1) forward)
+static inline int linear_fwd(int dt, int odt, int M, int N, int K, const void* x, int64_t ldx,
+                             const void* W, int64_t ldw, const float* bias, void* y, int64_t ldy,
+                             int relu, hipStream_t s, float beta = 0.f, const float* yin = nullptr,
+                             int64_t ldyin = 0) {
+    return srnn_gemm_impl(dt, odt, 0, 1, M, N, K, 1.f, x, ldx, 0, W, ldw, 0, beta, yin, ldyin, 0,
+                          y, ldy, 0, bias, 1, relu, 1, -1, s);
+}

@@ -1,0 +1,689 @@
+"""Drop-in for the reference's model.py (model.py:1-520), MI355X-native.
+
+Same classes, constructor signatures, attributes, state_dict keys and init recipe
+(RNG consumption order) as the reference -- SampleRNN, FrameLevelRNN, SampleLevelMLP,
+Runner, Predictor, Generator -- so train.py / generate.py bind unchanged.  Every
+forward/backward runs on the hand-written HIP kernels of libsamplernn_hip.so:
+
+  * FrameLevelRNN  -> _TierFn: input/cond/speaker projections (MFMA GEMMs with fused
+    bias + upper-tier add), GRU input projection for all frames in one GEMM, one fused
+    MFMA+gate kernel per time step, LearnedUpsampling1d as one GEMM; backward mirrors it.
+  * SampleLevelMLP -> _MlpFn: embedding . conv folded into a per-tap table, L1 as a
+    gather-sum, hidden/output GEMMs with fused bias/ReLU, log-softmax kernel.
+  * Generator      -> srnn_generate: the whole autoregressive loop on the device,
+    captured as a hipGraph (no per-sample host round trip).
+
+Numerics: fp32 by default (parity mode, logits within 1e-4 of the reference);
+`SampleRNN.compute_dtype = torch.bfloat16` (or env SRNN_COMPUTE_DTYPE=bf16) runs the
+matmuls on bf16 MFMA with fp32 accumulation, fp32 master weights and fp32 recurrences.
+"""
+import ctypes
+import os
+
+import numpy as np
+import torch
+from torch.nn import init
+
+import nn
+import utils
+import samplernn_hip as H
+
+verbose = False
+
+
+def _default_dtype():
+    v = os.environ.get('SRNN_COMPUTE_DTYPE', 'fp32').lower()
+    return torch.bfloat16 if v in ('bf16', 'bfloat16') else torch.float32
+
+
+class _GRUParams(torch.nn.Module):
+    """Parameter container with torch.nn.GRU's names and reset_parameters RNG order
+    (weight_ih_l{l}, weight_hh_l{l}, bias_ih_l{l}, bias_hh_l{l}); the recurrence itself
+    runs in the HIP gru_cell kernel."""
+
+    def __init__(self, input_size, hidden_size, num_layers):
+        super().__init__()
+        self.input_size, self.hidden_size, self.num_layers = input_size, hidden_size, num_layers
+        for l in range(num_layers):
+            isz = input_size if l == 0 else hidden_size
+            self.register_parameter('weight_ih_l%d' % l,
+                                    torch.nn.Parameter(torch.empty(3 * hidden_size, isz)))
+            self.register_parameter('weight_hh_l%d' % l,
+                                    torch.nn.Parameter(torch.empty(3 * hidden_size, hidden_size)))
+            self.register_parameter('bias_ih_l%d' % l,
+                                    torch.nn.Parameter(torch.empty(3 * hidden_size)))
+            self.register_parameter('bias_hh_l%d' % l,
+                                    torch.nn.Parameter(torch.empty(3 * hidden_size)))
+        stdv = 1.0 / np.sqrt(hidden_size)
+        for p in self.parameters():
+            init.uniform_(p, -stdv, stdv)
+
+
+class SampleRNN(torch.nn.Module):
+    """model.py:18-62."""
+
+    def __init__(self, frame_sizes, n_rnn, dim, learn_h0, q_levels, ulaw, weight_norm, cond_dim,
+                 spk_dim, qrnn=False):
+        super().__init__()
+        self.dim = dim
+        self.q_levels = q_levels
+        self.ulaw = ulaw
+        self.cond_dim = cond_dim
+        self.spk_dim = spk_dim
+        self.frame_sizes = [int(f) for f in frame_sizes]
+        self.n_rnn = n_rnn
+        self.compute_dtype = _default_dtype()
+        self.dequantize = utils.udequantize if ulaw else utils.linear_dequantize
+        ns_frame_samples = list(map(int, np.cumprod(frame_sizes)))
+        is_cond = [False] * len(frame_sizes)
+        is_cond[-1] = True
+        self.frame_level_rnns = torch.nn.ModuleList([
+            FrameLevelRNN(frame_size, n_frame_samples, n_rnn, dim, learn_h0, c, cond_dim,
+                          spk_dim, weight_norm, qrnn)
+            for (frame_size, n_frame_samples, c) in zip(frame_sizes, ns_frame_samples, is_cond)
+        ])
+        self.sample_level_mlp = SampleLevelMLP(frame_sizes[0], dim, q_levels, weight_norm)
+        for m in self.modules():
+            if m is not self:
+                m.__dict__['_root'] = self
+
+    @property
+    def lookback(self):
+        return self.frame_level_rnns[-1].n_frame_samples
+
+
+class FrameLevelRNN(torch.nn.Module):
+    """model.py:65-263 (parameters, init recipe, forward contract)."""
+
+    def __init__(self, frame_size, n_frame_samples, n_rnn, dim, learn_h0, is_cond, cond_dim,
+                 spk_dim, w_norm, qrnn):
+        super().__init__()
+        self.frame_size = frame_size
+        self.n_frame_samples = n_frame_samples
+        self.dim = dim
+        self.cond_dim = cond_dim
+        self.spk_dim = spk_dim
+        self.weight_norm = w_norm
+        self.qrnn = qrnn
+        self.n_rnn = n_rnn
+        self.is_cond = is_cond
+        h0 = torch.zeros(n_rnn, dim)
+        if learn_h0:
+            self.h0 = torch.nn.Parameter(h0)
+        else:
+            self.register_buffer('h0', h0)
+        self.input_expand = torch.nn.Conv1d(n_frame_samples, dim, kernel_size=1)
+        if is_cond:
+            self.cond_expand = torch.nn.Conv1d(cond_dim, dim, kernel_size=1)
+            init.kaiming_uniform_(self.cond_expand.weight)
+            init.constant_(self.cond_expand.bias, 0)
+            self.spk_embedding = torch.nn.Embedding(spk_dim, spk_dim)
+            self.spk_expand = torch.nn.Conv1d(spk_dim, dim, kernel_size=1)
+            init.kaiming_uniform_(self.spk_expand.weight)
+            init.constant_(self.spk_expand.bias, 0)
+            if w_norm:
+                nn.apply_weight_norm(self.cond_expand)
+                nn.apply_weight_norm(self.spk_expand)
+        else:
+            self.cond_expand = None
+            self.spk_expand = None
+            self.spk_embedding = None
+        init.kaiming_uniform_(self.input_expand.weight)
+        init.constant_(self.input_expand.bias, 0)
+        if w_norm:
+            nn.apply_weight_norm(self.input_expand)
+        # qrnn=True in the reference also builds a torch GRU (model.py:133-139)
+        self.rnn = _GRUParams(dim, dim, n_rnn)
+        for i in range(n_rnn):
+            nn.concat_init(getattr(self.rnn, 'weight_ih_l%d' % i),
+                           [nn.lecun_uniform, nn.lecun_uniform, nn.lecun_uniform])
+            init.constant_(getattr(self.rnn, 'bias_ih_l%d' % i), 0)
+            nn.concat_init(getattr(self.rnn, 'weight_hh_l%d' % i),
+                           [nn.lecun_uniform, nn.lecun_uniform, init.orthogonal_])
+            init.constant_(getattr(self.rnn, 'bias_hh_l%d' % i), 0)
+        self.upsampling = nn.LearnedUpsampling1d(dim, dim, frame_size)
+        init.uniform_(self.upsampling.conv_t.weight, -np.sqrt(6 / dim), np.sqrt(6 / dim))
+        init.constant_(self.upsampling.bias, 0)
+        # always weight-normed: model.py:177 tests the imported function, not the flag
+        nn.apply_weight_norm(self.upsampling.conv_t)
+
+    # parameter tensors in the order _TierFn consumes them
+    def _param_list(self):
+        ps = []
+        ps += nn.weight_params(self.input_expand) + [self.input_expand.bias]
+        if self.is_cond:
+            ps += nn.weight_params(self.cond_expand) + [self.cond_expand.bias]
+            ps += [self.spk_embedding.weight]
+            ps += nn.weight_params(self.spk_expand) + [self.spk_expand.bias]
+        for l in range(self.n_rnn):
+            ps += [getattr(self.rnn, 'weight_ih_l%d' % l), getattr(self.rnn, 'weight_hh_l%d' % l),
+                   getattr(self.rnn, 'bias_ih_l%d' % l), getattr(self.rnn, 'bias_hh_l%d' % l)]
+        ps += nn.weight_params(self.upsampling.conv_t) + [self.upsampling.bias]
+        return ps
+
+    def forward(self, prev_samples, upper_tier_conditioning, hidden, cond, spk, writer,
+                iterations):
+        """model.py:180-263: (B,F,nfs) samples -> ((B, F*frame_size, D) conditioning, hidden)."""
+        H.need_cuda(prev_samples)
+        dev = prev_samples.device
+        if cond is not None:
+            cond = cond.to(dev)
+        if spk is not None:
+            spk = spk.to(dev).long()
+        h0 = self.h0
+        ps = self._param_list()
+        out, h = _TierFn.apply(self, prev_samples.float().contiguous(),
+                               None if upper_tier_conditioning is None
+                               else upper_tier_conditioning.contiguous(),
+                               cond, spk, None if hidden is None else hidden.contiguous(),
+                               h0, *ps)
+        return out, h
+
+
+def _dt(mod):
+    root = mod.__dict__.get('_root')
+    return root.compute_dtype if root is not None else torch.float32
+
+
+class _TierFn(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, mod, prev, upper, cond, spk, hidden, h0, *ps):
+        T = _dt(mod)
+        B, Fr, nfs = prev.shape
+        D = mod.dim
+        L = mod.n_rnn
+        dev = prev.device
+        it = iter(ps)
+
+        def take_w(m):
+            return [next(it) for _ in nn.weight_params(m)]
+
+        ie_p = take_w(mod.input_expand)
+        ie_b = next(it)
+        W_ie = H.cast(nn.weight_of(mod.input_expand).reshape(D, nfs), T)
+        prevT = H.cast(prev.reshape(B * Fr, nfs), T)
+        x0 = H.linear(prevT, W_ie, bias=ie_b,
+                      cin=None if upper is None else upper.reshape(B * Fr, D),
+                      beta=0.0 if upper is None else 1.0)
+        condT = spk_embT = W_c = W_s = None
+        if mod.is_cond:
+            take_w(mod.cond_expand)
+            c_b = next(it)
+            E_s = next(it)
+            take_w(mod.spk_expand)
+            s_b = next(it)
+            C = cond.shape[-1]
+            W_c = H.cast(nn.weight_of(mod.cond_expand).reshape(D, C), T)
+            condT = H.cast(cond.reshape(B * Fr, C).float().contiguous(), T)
+            H.linear(condT, W_c, bias=c_b, cin=x0, beta=1.0, out=x0)
+            S = E_s.shape[1]
+            spk_flat = spk.reshape(B).contiguous()
+            spk_emb = torch.empty((B, S), device=dev, dtype=torch.float32)
+            H.lib().call('srnn_gather_rows', H.ptr(E_s), S, H.ptr(spk_flat), B, S, H.ptr(spk_emb),
+                         H.F32, S, H.stream())
+            spk_embT = H.cast(spk_emb, T)
+            W_s = H.cast(nn.weight_of(mod.spk_expand).reshape(D, S), T)
+            spk_proj = H.linear(spk_embT, W_s, bias=s_b)
+            H.lib().call('srnn_add_bcast_rows', H.ptr(x0), H.ptr(spk_proj), B, Fr, D, D,
+                         H.stream())
+        else:
+            spk_flat = None
+        reset = hidden is None
+        if reset:   # model.py:224-228
+            h_in = h0.detach().reshape(L, 1, D).expand(L, B, D).contiguous()
+        else:
+            h_in = hidden.float().contiguous()
+        lp = T != torch.float32
+        Wih, Whh, bih, bhh = [], [], [], []
+        xs, outs, outsT, gates = [], [], [], []
+        X = x0
+        for l in range(L):
+            wih, whh, b_ih, b_hh = next(it), next(it), next(it), next(it)
+            Wih.append(H.cast(wih, T))
+            Whh.append(H.cast(whh, T))
+            bih.append(b_ih)
+            bhh.append(b_hh)
+            XT = H.cast(X, T)
+            gi = H.linear(XT, Wih[l], bias=b_ih)                      # (B*F, 3D)
+            out = torch.empty((B, Fr, D), device=dev, dtype=torch.float32)
+            outT = torch.empty((B, Fr, D), device=dev, dtype=T) if lp else out
+            gt = torch.empty((B, Fr, 4 * D), device=dev, dtype=torch.float32)
+            hpf = h_in[l]
+            hpT = H.cast(hpf, T)
+            for t in range(Fr):
+                if t == 0:
+                    hp_t, hp_f, ldh = hpT, hpf, D
+                else:
+                    hp_t, hp_f, ldh = outT[:, t - 1], out[:, t - 1], Fr * D
+                H.lib().call('srnn_gru_cell', H.dcode(T), B, D, D, None, 0, None, None,
+                             H.ptr(gi[t:]), Fr * 3 * D, H.ptr(hp_t), ldh, H.ptr(hp_f), ldh,
+                             H.ptr(Whh[l]), H.ptr(b_hh), H.ptr(out[:, t]), Fr * D,
+                             H.ptr(outT[:, t]) if lp else None, Fr * D, H.ptr(gt[:, t]),
+                             Fr * 4 * D, H.stream())
+            xs.append(XT)
+            outs.append(out)
+            outsT.append(outT)
+            gates.append(gt)
+            X = out.reshape(B * Fr, D)
+        up_p = take_w(mod.upsampling.conv_t)
+        up_b = next(it)
+        k = mod.frame_size
+        W_up = H.permute3(nn.weight_of(mod.upsampling.conv_t), (2, 1, 0), dtype=T)  # (k, D, D)
+        b_up = H.permute3(up_b.reshape(1, D, k), (0, 2, 1)).reshape(k * D)
+        Y = H.linear(outsT[-1].reshape(B * Fr, D), W_up.reshape(k * D, D), bias=b_up)
+        h_new = torch.stack([o[:, -1] for o in outs], 0)
+        ctx.mod = mod
+        ctx.reset = reset
+        ctx.has_upper = upper is not None
+        ctx.dims = (B, Fr, nfs, D, L, k)
+        ctx.T = T
+        ctx.save_for_backward(prevT, condT, spk_embT, spk_flat, h_in, W_ie, W_c, W_s, W_up,
+                              *Wih, *Whh, *xs, *outs, *outsT, *gates)
+        ctx.mark_non_differentiable(h_new)
+        return Y.reshape(B, Fr * k, D), h_new
+
+    @staticmethod
+    def backward(ctx, dY, dh_new):
+        mod = ctx.mod
+        B, Fr, nfs, D, L, k = ctx.dims
+        T = ctx.T
+        lp = T != torch.float32
+        sv = ctx.saved_tensors
+        prevT, condT, spk_embT, spk_flat, h_in, W_ie, W_c, W_s, W_up = sv[:9]
+        r = sv[9:]
+        Wih, Whh = r[:L], r[L:2 * L]
+        xs, outs, outsT, gates = r[2 * L:3 * L], r[3 * L:4 * L], r[4 * L:5 * L], r[5 * L:6 * L]
+        dev = dY.device
+        st = H.stream
+        M = B * Fr
+        # --- upsampling (nn.py:33-43)
+        dY2 = dY.reshape(M, k * D).float().contiguous()
+        dYT = H.cast(dY2, T)
+        dWup = H.gemm(dYT, outsT[-1].reshape(M, D), transA=True)          # (k*D, D)
+        db_up = H.colsum(dY2, M, k * D)
+        dX = H.gemm(dYT, W_up.reshape(k * D, D))                          # (M, D)
+        dW_conv = H.permute3(dWup.reshape(k, D, D), (2, 1, 0))            # (D_in, D_out, k)
+        g_up = nn.weight_grad_to_params(mod.upsampling.conv_t, dW_conv)
+        g_up_b = H.permute3(db_up.reshape(1, k, D), (0, 2, 1)).reshape(D, k)
+        # --- GRU layers, top layer first
+        g_rnn = [None] * L
+        dh_in = [None] * L
+        for l in reversed(range(L)):
+            dOut = dX.reshape(B, Fr, D)
+            dGH = torch.empty((B, Fr, 3 * D), device=dev, dtype=torch.float32)
+            dGHT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T) if lp else dGH
+            dGI = torch.empty((B, Fr, 3 * D), device=dev, dtype=torch.float32)
+            ddir = [torch.empty((B, D), device=dev, dtype=torch.float32) for _ in range(2)]
+            for t in reversed(range(Fr)):
+                nxt = t + 1 < Fr
+                if t > 0:
+                    hp, ldhp = outs[l][:, t - 1], Fr * D
+                else:
+                    hp, ldhp = h_in[l], D
+                H.lib().call('srnn_gru_cell_bwd', H.dcode(T), B, D, H.ptr(dOut[:, t]), Fr * D,
+                             H.ptr(dGHT[:, t + 1]) if nxt else None, Fr * 3 * D,
+                             H.ptr(ddir[(t + 1) % 2]) if nxt else None, H.ptr(Whh[l]),
+                             H.ptr(gates[l][:, t]), Fr * 4 * D, H.ptr(hp), ldhp,
+                             H.ptr(dGH[:, t]), Fr * 3 * D,
+                             H.ptr(dGHT[:, t]) if lp else None, Fr * 3 * D,
+                             H.ptr(dGI[:, t]), Fr * 3 * D, H.ptr(ddir[t % 2]), st())
+            dh_in[l] = H.gemm(dGHT[:, 0], Whh[l], M=B, N=D, K=3 * D, lda=Fr * 3 * D, ldb=D,
+                              cin=ddir[0], beta=1.0)
+            # previous hidden states of every step: [h_in, out[:, :F-1]]
+            hprevT = torch.empty((B, Fr, D), device=dev, dtype=T)
+            H.lib().call('srnn_copy2d', H.F32, H.dcode(T), B, D, H.ptr(h_in[l]), D,
+                         H.ptr(hprevT), Fr * D, st())
+            if Fr > 1:
+                H.lib().call('srnn_copy2d', H.dcode(T), H.dcode(T), B, (Fr - 1) * D,
+                             H.ptr(outsT[l]), Fr * D, H.ptr(hprevT[:, 1:]), Fr * D, st())
+            dGH2, dGI2 = dGH.reshape(M, 3 * D), dGI.reshape(M, 3 * D)
+            dW_hh = H.gemm(dGHT.reshape(M, 3 * D), hprevT.reshape(M, D), transA=True)
+            db_hh = H.colsum(dGH2, M, 3 * D)
+            dGIT = H.cast(dGI2, T)
+            dW_ih = H.gemm(dGIT, xs[l], transA=True)
+            db_ih = H.colsum(dGI2, M, 3 * D)
+            dX = H.gemm(dGIT, Wih[l])                                     # (M, D)
+            g_rnn[l] = [dW_ih, dW_hh, db_ih, db_hh]
+        # --- input projections
+        dx0 = dX
+        dx0T = H.cast(dx0, T)
+        dW_ie = H.gemm(dx0T, prevT, transA=True)                         # (D, nfs)
+        g_ie = nn.weight_grad_to_params(mod.input_expand, dW_ie.reshape(D, nfs, 1))
+        g_ie_b = H.colsum(dx0, M, D)
+        d_upper = dx0.reshape(B, Fr, D) if ctx.has_upper else None
+        grads = g_ie + [g_ie_b]
+        if mod.is_cond:
+            C = condT.shape[1]
+            S = spk_embT.shape[1]
+            dW_c = H.gemm(dx0T, condT, transA=True)                      # (D, C)
+            grads += nn.weight_grad_to_params(mod.cond_expand, dW_c.reshape(D, C, 1))
+            grads += [g_ie_b.clone()]                                    # cond bias grad
+            ones = torch.ones((1, Fr), device=dev, dtype=torch.float32)
+            dspk = torch.empty((B, D), device=dev, dtype=torch.float32)
+            H.gemm(ones, dx0, M=1, N=D, K=Fr, lda=Fr, ldb=D, ldc=D, out=dspk, batch=B, sA=0,
+                   sB=Fr * D, sC=D)
+            dspkT = H.cast(dspk, T)
+            dW_s = H.gemm(dspkT, spk_embT, transA=True)                  # (D, S)
+            db_s = H.colsum(dspk, B, D)
+            demb = H.gemm(dspkT, W_s)                                    # (B, S)
+            dE = torch.zeros((S, S), device=dev, dtype=torch.float32)
+            H.lib().call('srnn_scatter_add_rows', H.ptr(dE), S, H.ptr(spk_flat), B, S,
+                         H.ptr(demb), S, st())
+            grads += [dE]
+            grads += nn.weight_grad_to_params(mod.spk_expand, dW_s.reshape(D, S, 1))
+            grads += [db_s]
+        for l in range(L):
+            grads += g_rnn[l]
+        grads += g_up + [g_up_b]
+        dh0 = None
+        if ctx.reset and ctx.needs_input_grad[6]:
+            dh0 = torch.stack([H.colsum(dh_in[l], B, D) for l in range(L)], 0)
+        return (None, None, d_upper, None, None, None, dh0) + tuple(grads)
+
+
+class SampleLevelMLP(torch.nn.Module):
+    """model.py:266-325."""
+
+    def __init__(self, frame_size, dim, q_levels, wnorm):
+        super().__init__()
+        self.q_levels = q_levels
+        self.weight_norm = wnorm
+        self.frame_size = frame_size
+        self.dim = dim
+        self.embedding = torch.nn.Embedding(q_levels, q_levels)
+        self.input = torch.nn.Conv1d(q_levels, dim, kernel_size=frame_size, bias=False)
+        init.kaiming_uniform_(self.input.weight)
+        self.hidden = torch.nn.Conv1d(dim, dim, kernel_size=1)
+        init.kaiming_uniform_(self.hidden.weight)
+        init.constant_(self.hidden.bias, 0)
+        self.output = torch.nn.Conv1d(dim, q_levels, kernel_size=1)
+        nn.lecun_uniform(self.output.weight)
+        init.constant_(self.output.bias, 0)
+        if wnorm:
+            nn.apply_weight_norm(self.input)
+            nn.apply_weight_norm(self.hidden)
+            nn.apply_weight_norm(self.output)
+
+    def _param_list(self):
+        return ([self.embedding.weight] + nn.weight_params(self.input) +
+                nn.weight_params(self.hidden) + [self.hidden.bias] +
+                nn.weight_params(self.output) + [self.output.bias])
+
+    def tab(self, T):
+        """Tab[k][q][:] = W_in[:, :, k] . E[q, :]  (FS0, Q, D): the folded embedding+conv."""
+        return _build_tab(self, T)[0]
+
+    def forward(self, prev_samples, upper_tier_conditioning):
+        """model.py:308-325: indices (B, T+FS0-1), conditioning (B, T, D) -> log-probs (B,T,Q)."""
+        H.need_cuda(upper_tier_conditioning)
+        x = prev_samples.to(upper_tier_conditioning.device).long().contiguous()
+        return _MlpFn.apply(self, x, upper_tier_conditioning.float().contiguous(),
+                            *self._param_list())
+
+
+def _build_tab(mlp, T):
+    Q, D, FS0 = mlp.q_levels, mlp.dim, mlp.frame_size
+    W_in = nn.weight_of(mlp.input)                                       # (D, Q, FS0)
+    Wp = H.permute3(W_in, (2, 0, 1), dtype=T)                            # (FS0, D, Q)
+    ET = H.cast(mlp.embedding.weight, T)
+    tab = torch.empty((FS0, Q, D), device=ET.device, dtype=T)
+    H.gemm(ET, Wp, transB=True, out=tab, M=Q, N=D, K=Q, lda=Q, ldb=Q, ldc=D, batch=FS0, sA=0,
+           sB=D * Q, sC=Q * D)
+    return tab, Wp, ET
+
+
+class _MlpFn(torch.autograd.Function):
+
+    @staticmethod
+    def forward(ctx, mlp, x, upper, *ps):
+        T = _dt(mlp)
+        B, Tl, D = upper.shape
+        Q, FS0 = mlp.q_levels, mlp.frame_size
+        dev = upper.device
+        tab, Wp, ET = _build_tab(mlp, T)
+        a1 = torch.empty((B * Tl, D), device=dev, dtype=T)
+        H.lib().call('srnn_mlp_l1', H.dcode(T), H.ptr(tab), H.ptr(x), x.shape[1], 0, B, Tl,
+                     H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
+        W_hid = H.cast(nn.weight_of(mlp.hidden).reshape(D, D), T)
+        W_out = H.cast(nn.weight_of(mlp.output).reshape(Q, D), T)
+        a2 = H.linear(a1, W_hid, bias=mlp.hidden.bias, relu=True, out_dtype=T)
+        z = H.linear(a2, W_out, bias=mlp.output.bias)                    # (B*T, Q) fp32
+        logp = torch.empty((B * Tl, Q), device=dev, dtype=torch.float32)
+        H.lib().call('srnn_logsoftmax_nll', H.ptr(z), Q, None, 0, Tl, B * Tl, Q, None,
+                     H.ptr(logp), Q, None, H.F32, 0, 0.0, H.stream())
+        ctx.mlp = mlp
+        ctx.T = T
+        ctx.dims = (B, Tl, D, Q, FS0)
+        ctx.save_for_backward(x, a1, a2, logp, Wp, ET, W_hid, W_out)
+        return logp.reshape(B, Tl, Q)
+
+    @staticmethod
+    def backward(ctx, dlogp):
+        mlp = ctx.mlp
+        T = ctx.T
+        B, Tl, D, Q, FS0 = ctx.dims
+        x, a1, a2, logp, Wp, ET, W_hid, W_out = ctx.saved_tensors
+        dev = logp.device
+        st = H.stream
+        M = B * Tl
+        dl = dlogp.reshape(M, Q).float().contiguous()
+        dz = torch.empty((M, Q), device=dev, dtype=T)
+        H.lib().call('srnn_logsoftmax_bwd', H.ptr(dl), Q, H.ptr(logp), Q, M, Q, H.ptr(dz),
+                     H.dcode(T), Q, st())
+        dW_out = H.gemm(dz, a2, transA=True)                             # (Q, D)
+        db_out = H.colsum(dz, M, Q)
+        da2 = H.gemm(dz, W_out, mask=a2, out_dtype=T)                    # (M, D)
+        dW_hid = H.gemm(da2, a1, transA=True)                            # (D, D)
+        db_hid = H.colsum(da2, M, D)
+        da1 = H.gemm(da2, W_hid, mask=a1)                                # (M, D) fp32
+        # folded embedding . conv backward: dTab[q][k][:] += da1[t] for x_{t+k} = q
+        dtab = torch.zeros((Q, FS0, D), device=dev, dtype=torch.float32)
+        H.lib().call('srnn_mlp_dtab', H.F32, H.ptr(da1), D, H.ptr(x), x.shape[1], 0, B, Tl,
+                     H.ptr(dtab), D, FS0, Q, st())
+        dtabT = H.cast(dtab.reshape(Q, FS0 * D), T)
+        dE = H.gemm(dtabT, Wp.reshape(FS0 * D, Q))                       # (Q, Q)
+        dWp = torch.empty((FS0, D, Q), device=dev, dtype=torch.float32)
+        H.gemm(dtabT, ET, transA=True, out=dWp, M=D, N=Q, K=Q, lda=FS0 * D, ldb=Q, ldc=Q,
+               batch=FS0, sA=D, sB=0, sC=D * Q)
+        dW_in = H.permute3(dWp, (1, 2, 0))                               # (D, Q, FS0)
+        grads = [dE]
+        grads += nn.weight_grad_to_params(mlp.input, dW_in)
+        grads += nn.weight_grad_to_params(mlp.hidden, dW_hid.reshape(D, D, 1)) + [db_hid]
+        grads += nn.weight_grad_to_params(mlp.output, dW_out.reshape(Q, D, 1)) + [db_out]
+        return (None, None, da1.reshape(B, Tl, D)) + tuple(grads)
+
+
+class Runner:
+    """model.py:328-349."""
+
+    def __init__(self, model):
+        super().__init__()
+        self.model = model
+        self.reset_hidden_states()
+
+    def reset_hidden_states(self):
+        self.hidden_states = {rnn: None for rnn in self.model.frame_level_rnns}
+
+    def run_rnn(self, rnn, prev_samples, upper_tier_conditioning, cond, spk, writer=None,
+                iterations=None):
+        (output, new_hidden) = rnn(prev_samples, upper_tier_conditioning,
+                                   self.hidden_states[rnn], cond, spk, writer, iterations)
+        self.hidden_states[rnn] = new_hidden.detach()    # TBPTT truncation (model.py:348)
+        return output
+
+
+class Predictor(Runner, torch.nn.Module):
+    """model.py:352-436: teacher-forced forward with TBPTT hidden-state carry."""
+
+    def __init__(self, model):
+        super().__init__(model)
+
+    def forward(self, input_sequences, reset, cond, spk, writer=None, iterations=None):
+        if reset:
+            self.reset_hidden_states()
+        dev = next(self.model.parameters()).device
+        H.need_cuda(torch.empty(0, device=dev))
+        input_sequences = input_sequences.to(dev).long().contiguous()
+        cond = cond.to(dev)
+        spk = spk.to(dev)
+        (batch_size, _) = input_sequences.size()
+        (_, _, cond_dim) = cond.size()
+        L = self.model.lookback
+        q = self.model.q_levels
+        mode = 0 if self.model.ulaw else 1
+        upper = None
+        for rnn in reversed(self.model.frame_level_rnns):
+            n = rnn.n_frame_samples
+            seg = input_sequences[:, L - n: input_sequences.shape[1] - n + 1].contiguous()
+            prev = utils._dequant(seg, q, 2.0, mode)                    # 2 * dequantize
+            prev = prev.view(batch_size, -1, n)
+            if upper is None:
+                c = cond.contiguous().view(batch_size, -1, cond_dim)
+                s = spk.contiguous().view(batch_size, -1)
+                upper = self.run_rnn(rnn, prev, None, c, s, writer, iterations)
+            else:
+                upper = self.run_rnn(rnn, prev, upper, None, None, writer, iterations)
+        fs0 = self.model.frame_level_rnns[0].frame_size
+        return self.model.sample_level_mlp(input_sequences[:, L - fs0:], upper)
+
+
+def generation_weights(model, dtype=None):
+    """Folded, device-resident weight layouts for srnn_generate (weight-norm applied once)."""
+    T = dtype or model.compute_dtype
+    D = model.dim
+    keep = []
+    m = H.SrnnModel()
+    m.n_tiers = len(model.frame_level_rnns)
+    m.n_rnn = model.n_rnn
+    m.dim = D
+    m.q_levels = model.q_levels
+    m.cond_dim = model.cond_dim
+    m.dtype = H.dcode(T)
+    with torch.no_grad():
+        for k, rnn in enumerate(model.frame_level_rnns):
+            t = m.tier[k]
+            nfs = rnn.n_frame_samples
+            t.frame_size = rnn.frame_size
+            t.n_frame_samples = nfs
+            W_ie = nn.weight_of(rnn.input_expand).reshape(D, nfs)
+            if rnn.is_cond:
+                C = model.cond_dim
+                W_c = nn.weight_of(rnn.cond_expand).reshape(D, C)
+                w_in = torch.empty((D, nfs + C), device=W_ie.device, dtype=T)
+                H.lib().call('srnn_copy2d', H.F32, H.dcode(T), D, nfs, H.ptr(W_ie.contiguous()),
+                             nfs, H.ptr(w_in), nfs + C, H.stream())
+                H.lib().call('srnn_copy2d', H.F32, H.dcode(T), D, C, H.ptr(W_c.contiguous()), C,
+                             H.ptr(w_in[:, nfs:]), nfs + C, H.stream())
+                t.in_dim = nfs + C
+            else:
+                w_in = H.cast(W_ie.contiguous(), T)
+                t.in_dim = nfs
+                b_in = rnn.input_expand.bias.detach().contiguous()
+                keep.append(b_in)
+                t.b_in = H.ptr(b_in).value
+            keep.append(w_in)
+            t.w_in = H.ptr(w_in).value
+            for l in range(model.n_rnn):
+                wih = H.cast(getattr(rnn.rnn, 'weight_ih_l%d' % l).detach().contiguous(), T)
+                whh = H.cast(getattr(rnn.rnn, 'weight_hh_l%d' % l).detach().contiguous(), T)
+                bih = getattr(rnn.rnn, 'bias_ih_l%d' % l).detach().contiguous()
+                bhh = getattr(rnn.rnn, 'bias_hh_l%d' % l).detach().contiguous()
+                keep += [wih, whh, bih, bhh]
+                t.w_ih[l], t.w_hh[l] = H.ptr(wih).value, H.ptr(whh).value
+                t.b_ih[l], t.b_hh[l] = H.ptr(bih).value, H.ptr(bhh).value
+            k_ = rnn.frame_size
+            w_up = H.permute3(nn.weight_of(rnn.upsampling.conv_t), (2, 1, 0), dtype=T)
+            b_up = H.permute3(rnn.upsampling.bias.detach().reshape(1, D, k_), (0, 2, 1))
+            h0 = rnn.h0.detach().float().contiguous()
+            keep += [w_up, b_up, h0]
+            t.w_up, t.b_up, t.h0 = H.ptr(w_up).value, H.ptr(b_up).value, H.ptr(h0).value
+        mlp = model.sample_level_mlp
+        tab = mlp.tab(T)
+        w_hid = H.cast(nn.weight_of(mlp.hidden).reshape(D, D).contiguous(), T)
+        w_out = H.cast(nn.weight_of(mlp.output).reshape(model.q_levels, D).contiguous(), T)
+        b_hid = mlp.hidden.bias.detach().contiguous()
+        b_out = mlp.output.bias.detach().contiguous()
+        keep += [tab, w_hid, w_out, b_hid, b_out]
+        m.tab, m.w_hid, m.w_out = H.ptr(tab).value, H.ptr(w_hid).value, H.ptr(w_out).value
+        m.b_hid, m.b_out = H.ptr(b_hid).value, H.ptr(b_out).value
+    return m, keep
+
+
+def top_row_bias(model, spk):
+    """(n_seqs, D): spk_expand(spk_embedding(spk)) + b_spk + b_cond + b_in for the top tier."""
+    top = model.frame_level_rnns[-1]
+    D, S = model.dim, model.spk_dim
+    dev = spk.device
+    with torch.no_grad():
+        n = spk.numel()
+        emb = torch.empty((n, S), device=dev, dtype=torch.float32)
+        H.lib().call('srnn_gather_rows', H.ptr(top.spk_embedding.weight), S,
+                     H.ptr(spk.reshape(-1).contiguous()), n, S, H.ptr(emb), H.F32, S, H.stream())
+        bias = torch.empty(D, device=dev, dtype=torch.float32)
+        H.lib().call('srnn_axpby', H.ptr(bias), H.ptr(top.spk_expand.bias),
+                     H.ptr(top.cond_expand.bias), 1.0, 1.0, D, H.stream())
+        H.lib().call('srnn_axpby', H.ptr(bias), H.ptr(bias), H.ptr(top.input_expand.bias), 1.0,
+                     1.0, D, H.stream())
+        W_s = nn.weight_of(top.spk_expand).reshape(D, S).contiguous()
+        return H.linear(emb, W_s, bias=bias)
+
+
+class Generator(Runner):
+    """model.py:439-520: autoregressive generation, the whole loop on the device.
+
+    __call__(n_seqs, seq_len, cond, spk) keeps the reference contract: `seq_len` is
+    ignored (recomputed as num_cond * lookback, model.py:455), `cond` is a (num_cond, C)
+    array shared by all rows (or (n_seqs, num_cond, C) per row), `spk` an int (or one per
+    row), and the result is a host float32 (n_seqs, num_cond * lookback) tensor of
+    dequantized samples.  Sampling is argmax(p / q), q ~ Exp(1), exactly what torch>=2's
+    CPU `multinomial(1)` computes: sampler='torch' draws q from torch's CPU generator in
+    the reference's order (bit-replay of the reference stream); sampler='philox' draws q
+    on the device (counter-based Philox4x32-10, seed) for long runs.  `cuda` is accepted
+    for API compatibility; the product path always runs on the GPU.
+    """
+
+    def __init__(self, model, cuda=False):
+        super().__init__(model)
+        self.cuda = cuda
+        self.last_sequences = None
+
+    def __call__(self, n_seqs, seq_len, cond, spk, sampler='torch', seed=0, noise=None,
+                 return_logp=False, use_graph=True, dtype=None):
+        model = self.model
+        self.reset_hidden_states()
+        dev = next(model.parameters()).device
+        H.need_cuda(torch.empty(0, device=dev))
+        cond = torch.as_tensor(np.asarray(cond) if not torch.is_tensor(cond) else cond)
+        if cond.dim() == 2:
+            cond = cond.unsqueeze(0).expand(n_seqs, *cond.shape)
+        cond = cond.to(dev, torch.float32).contiguous()
+        num_cond = cond.shape[1]
+        spk = torch.as_tensor(np.asarray(spk) if not torch.is_tensor(spk) else spk).reshape(-1)
+        if spk.numel() == 1:
+            spk = spk.expand(n_seqs)
+        spk = spk.to(dev, torch.long).contiguous()
+        L = model.lookback
+        T = num_cond * L
+        Q = model.q_levels
+        m, keep = generation_weights(model, dtype)
+        row_bias = top_row_bias(model, spk)
+        seq = torch.full((n_seqs, L + T), utils.q_zero(Q), dtype=torch.long, device=dev)
+        if noise is None and sampler == 'torch':
+            noise = torch.empty(T, n_seqs, Q).exponential_(1)
+        if noise is not None:
+            noise = torch.as_tensor(noise).to(dev, torch.float32).contiguous()
+            assert noise.shape == (T, n_seqs, Q), 'noise must be (T, n_seqs, Q)'
+        logp = torch.empty((T, n_seqs, Q), device=dev) if return_logp else None
+        sz = ctypes.c_size_t(0)
+        H.lib().call('srnn_gen_workspace_size', ctypes.byref(m), n_seqs, ctypes.byref(sz))
+        ws = torch.empty(sz.value, device=dev, dtype=torch.uint8)
+        H.lib().call('srnn_generate', ctypes.byref(m), n_seqs, num_cond, H.ptr(cond),
+                     H.ptr(row_bias), H.ptr(noise), int(seed) & ((1 << 64) - 1), H.ptr(seq),
+                     H.ptr(logp), H.ptr(ws), sz.value, 1 if use_graph else 0, H.stream())
+        del keep
+        self.last_sequences = seq
+        out = model.dequantize(seq[:, L:], Q).cpu()
+        if return_logp:
+            return out, logp.permute(1, 0, 2).contiguous()
+        return out

@@ -1,0 +1,165 @@
+"""Drop-in for the reference's nn.py (nn.py:1-70).
+
+LearnedUpsampling1d keeps the reference's parameters (conv_t = ConvTranspose1d with
+stride = kernel_size, plus a per-(channel, position) bias) and computes on the HIP
+GEMM; sequence_nll_loss_bits runs the HIP NLL kernels.  The init helpers are the
+reference's recipes (they only touch host tensors at construction time).
+"""
+import math
+
+import torch
+from torch import nn
+
+import samplernn_hip as H
+
+LOG2E = math.log(math.e, 2)
+
+
+def weight_of(mod):
+    """Effective weight of a conv/linear container: weight, or g * v / ||v|| when the
+    module carries weight_g / weight_v (torch weight_norm naming, dim=0)."""
+    if hasattr(mod, 'weight_g'):
+        return H.weight_norm(mod.weight_g, mod.weight_v)
+    return mod.weight
+
+
+def weight_grad_to_params(mod, dw):
+    """Map a gradient w.r.t. the effective weight to the module's parameters, in the
+    order returned by weight_params(mod)."""
+    if hasattr(mod, 'weight_g'):
+        return list(H.weight_norm_bwd(mod.weight_g, mod.weight_v, dw))
+    return [dw]
+
+
+def weight_params(mod):
+    if hasattr(mod, 'weight_g'):
+        return [mod.weight_g, mod.weight_v]
+    return [mod.weight]
+
+
+def apply_weight_norm(module, name='weight'):
+    """Same parameters as torch.nn.utils.weight_norm(module, name, dim=0) -- weight_g
+    (norm over all dims but 0) and weight_v -- without installing a forward hook: the
+    effective weight is recomputed on the device by the HIP kernels at each use."""
+    w = getattr(module, name)
+    del module._parameters[name]
+    with torch.no_grad():
+        g = w.reshape(w.shape[0], -1).norm(dim=1).reshape([-1] + [1] * (w.dim() - 1))
+    module.register_parameter(name + '_g', nn.Parameter(g.clone()))
+    module.register_parameter(name + '_v', nn.Parameter(w.data.clone()))
+    return module
+
+
+class _UpsampleFn(torch.autograd.Function):
+    """out[b, o, t*k + j] = sum_i x[b, i, t] W[i, o, j] + bias[o, j]  as one GEMM."""
+
+    @staticmethod
+    def forward(ctx, mod, x, *params):
+        B, Cin, Lx = x.shape
+        k = mod.conv_t.kernel_size[0]
+        Cout = mod.conv_t.out_channels
+        W = weight_of(mod.conv_t)                                  # (Cin, Cout, k)
+        Wg = H.permute3(W, (2, 1, 0))                              # (k*Cout, Cin)
+        xr = H.permute3(x.float(), (0, 2, 1)).reshape(B * Lx, Cin)  # (B*L, Cin)
+        bias = None
+        if mod.bias is not None:
+            bias = H.permute3(mod.bias.reshape(1, Cout, k), (0, 2, 1)).reshape(-1)
+        y = H.linear(xr, Wg.reshape(k * Cout, Cin), bias=bias)     # (B*L, k*Cout)
+        out = H.permute3(y.reshape(B, Lx * k, Cout), (0, 2, 1))     # (B, Cout, L*k)
+        ctx.mod = mod
+        ctx.save_for_backward(xr, Wg)
+        ctx.shape = (B, Cin, Lx, k, Cout)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        mod = ctx.mod
+        xr, Wg = ctx.saved_tensors
+        B, Cin, Lx, k, Cout = ctx.shape
+        dy = H.permute3(dout.float().contiguous(), (0, 2, 1)).reshape(B * Lx, k * Cout)
+        dWg = H.gemm(dy, xr, transA=True)                          # (k*Cout, Cin)
+        dx = H.gemm(dy, Wg.reshape(k * Cout, Cin))                 # (B*L, Cin)
+        dx = H.permute3(dx.reshape(B, Lx, Cin), (0, 2, 1))
+        dW = H.permute3(dWg.reshape(k, Cout, Cin), (2, 1, 0))      # (Cin, Cout, k)
+        grads = weight_grad_to_params(mod.conv_t, dW)
+        if mod.bias is not None:
+            db = H.colsum(dy, B * Lx, k * Cout)
+            grads.append(H.permute3(db.reshape(1, k, Cout), (0, 2, 1)).reshape(Cout, k))
+        return (None, dx) + tuple(grads)
+
+
+class LearnedUpsampling1d(nn.Module):
+    """nn.py:7-43."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, bias=True):
+        super().__init__()
+        self.conv_t = nn.ConvTranspose1d(
+            in_channels=in_channels, out_channels=out_channels, kernel_size=kernel_size,
+            stride=kernel_size, bias=False)
+        if bias:
+            self.bias = nn.Parameter(torch.FloatTensor(out_channels, kernel_size))
+        else:
+            self.register_parameter('bias', None)
+        self.reset_parameters()
+
+    def reset_parameters(self):
+        self.conv_t.reset_parameters()
+        if self.bias is not None:
+            nn.init.constant_(self.bias, 0)
+
+    def forward(self, input):
+        H.need_cuda(input)
+        params = weight_params(self.conv_t) + ([self.bias] if self.bias is not None else [])
+        return _UpsampleFn.apply(self, input, *params)
+
+
+def lecun_uniform(tensor):
+    """nn.py:46-48."""
+    fan_in = nn.init._calculate_correct_fan(tensor, 'fan_in')
+    nn.init.uniform_(tensor, -math.sqrt(3 / fan_in), math.sqrt(3 / fan_in))
+
+
+def concat_init(tensor, inits):
+    """nn.py:51-63."""
+    try:
+        tensor = tensor.data
+    except AttributeError:
+        pass
+    (length, fan_out) = tensor.size()
+    fan_in = length // len(inits)
+    chunk = tensor.new(fan_in, fan_out)
+    for (i, init) in enumerate(inits):
+        init(chunk)
+        tensor[i * fan_in: (i + 1) * fan_in, :] = chunk
+
+
+class _NllBitsFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logp, target):
+        B, T, Q = logp.shape
+        lp = logp.contiguous()
+        tg = target.reshape(B, T).contiguous()
+        rows = torch.empty(B * T, device=lp.device, dtype=torch.float32)
+        H.lib().call('srnn_nll_fwd', H.ptr(lp), Q, H.ptr(tg), T, T, B * T, H.ptr(rows), H.stream())
+        loss = H.colsum(rows, B * T, 1, alpha=LOG2E / (B * T))
+        ctx.save_for_backward(tg)
+        ctx.shape = (B, T, Q)
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        (tg,) = ctx.saved_tensors
+        B, T, Q = ctx.shape
+        d = torch.empty((B, T, Q), device=tg.device, dtype=torch.float32)
+        # gscale = g * log2(e) / N  (mean reduction); g is a 0-d device tensor
+        scale = float(g) * LOG2E / (B * T)
+        H.lib().call('srnn_nll_bwd', H.ptr(tg), T, T, B * T, Q, H.ptr(d), Q, scale, H.stream())
+        return d, None
+
+
+def sequence_nll_loss_bits(input, target, *args, **kwargs):
+    """nn.py:66-70: mean NLL of log-probs (B, T, Q) x log2(e), on the HIP kernels."""
+    if args or kwargs:
+        raise NotImplementedError('sequence_nll_loss_bits: extra nll_loss arguments')
+    H.need_cuda(input, target)
+    return _NllBitsFn.apply(input, target)

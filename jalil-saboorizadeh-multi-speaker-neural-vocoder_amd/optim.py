@@ -1,0 +1,76 @@
+"""Drop-in for the reference's optim.py (optim.py:1-21).
+
+gradient_clipping(optimizer, min, max) returns the same wrapper: step(closure) runs the
+closure, clamps every gradient to [min, max] in place (optim.py:11-13) and steps.  For
+torch.optim.Adam over device parameters (train.py:238) the clamp and the Adam update
+are ONE fused HIP kernel per parameter (srnn_adam_clip) operating on the optimizer's
+own state tensors (step / exp_avg / exp_avg_sq), so Adam.state_dict() stays valid.
+Parameters whose grad is None are treated as zero-grad, i.e. torch-0.4 zero_grad
+semantics: the learned h0 keeps moving on its Adam moments on non-reset steps, as it
+did in the reference's environment.  An optional `grad_sync` callable (set by
+distributed.py) all-reduces gradients after the closure and before the clamp.
+"""
+import torch
+
+import samplernn_hip as H
+
+
+def _fused_adam_step(optimizer, lo, hi):
+    for group in optimizer.param_groups:
+        if group.get('weight_decay', 0) != 0 or group.get('amsgrad', False) or \
+                group.get('maximize', False):
+            raise NotImplementedError('fused clip+Adam: weight_decay/amsgrad/maximize')
+        b1, b2 = group['betas']
+        for p in group['params']:
+            if not p.requires_grad:
+                continue
+            st = optimizer.state[p]
+            if len(st) == 0:
+                st['step'] = torch.tensor(0.0, dtype=torch.float32)
+                st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            st['step'] += 1
+            H.lib().call('srnn_adam_clip', H.ptr(p), H.ptr(p.grad), H.ptr(st['exp_avg']),
+                         H.ptr(st['exp_avg_sq']), None, p.numel(), float(lo), float(hi),
+                         float(group['lr']), float(b1), float(b2), float(group['eps']),
+                         int(st['step'].item()), H.stream())
+
+
+def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
+
+    class OptimizerWrapper(object):
+
+        def __init__(self):
+            self.grad_sync = grad_sync
+
+        def step(self, closure):
+            fused = isinstance(optimizer, torch.optim.Adam) and all(
+                p.is_cuda for g in optimizer.param_groups for p in g['params'])
+            if fused:
+                with torch.enable_grad():
+                    loss = closure()
+                if self.grad_sync is not None:
+                    self.grad_sync(optimizer)
+                with torch.no_grad():
+                    _fused_adam_step(optimizer, min, max)
+                return loss
+
+            def closure_wrapper():
+                loss = closure()
+                if self.grad_sync is not None:
+                    self.grad_sync(optimizer)
+                for group in optimizer.param_groups:
+                    for p in group['params']:
+                        if p.grad is None:
+                            p.grad = torch.zeros_like(p)
+                        p.grad.clamp_(min, max)
+                return loss
+
+            return optimizer.step(closure_wrapper)
+
+        def __getattr__(self, attr):
+            return getattr(optimizer, attr)
+
+    return OptimizerWrapper()

@@ -1,0 +1,229 @@
+"""ctypes binding of libsamplernn_hip.so (the C ABI in include/samplernn_hip.h).
+
+This is the ONLY compute path of the drop-in model.py / nn.py / utils.py / optim.py:
+there is no PyTorch or CPU fallback for device tensors.  If the library is missing or
+fails to load, `lib()` raises -- loudly -- and so does every op that needs it.
+PyTorch is used for device memory, streams and autograd bookkeeping only.
+"""
+import ctypes
+import os
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'libsamplernn_hip.so')
+
+F32, BF16 = 0, 1
+MAX_TIERS, MAX_RNN = 6, 4
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_int64
+_F = ctypes.c_float
+_D = ctypes.c_double
+_U64 = ctypes.c_uint64
+_SZ = ctypes.c_size_t
+
+# name -> argument types (all return int status)
+_SIGS = {
+    'srnn_uquantize_f32': [_P, _P, _L, _I, _P],
+    'srnn_uquantize_f64': [_P, _P, _L, _I, _P],
+    'srnn_udequantize': [_P, _P, _L, _I, _F, _I, _P],
+    'srnn_uquantize_f64_host': [_P, _P, _L, _I],
+    'srnn_uquantize_f32_host': [_P, _P, _L, _I],
+    'srnn_udequantize_host': [_P, _P, _L, _I],
+    'srnn_gemm': [_I, _I, _I, _I, _I, _I, _I, _F, _P, _L, _L, _P, _L, _L, _F, _P, _L, _L, _P, _L,
+                  _L, _P, _I, _I, _I, _I, _P, _L, _P],
+    'srnn_gru_cell': [_I, _I, _I, _I, _P, _L, _P, _P, _P, _L, _P, _L, _P, _L, _P, _P, _P, _L, _P,
+                      _L, _P, _L, _P],
+    'srnn_gru_cell_bwd': [_I, _I, _I, _P, _L, _P, _L, _P, _P, _P, _L, _P, _L, _P, _L, _P, _L, _P,
+                          _L, _P, _P],
+    'srnn_mlp_l1': [_I, _P, _P, _L, _I, _I, _I, _P, _L, _P, _L, _I, _I, _I, _P],
+    'srnn_mlp_dtab': [_I, _P, _L, _P, _L, _I, _I, _I, _P, _I, _I, _I, _P],
+    'srnn_logsoftmax_nll': [_P, _L, _P, _L, _I, _L, _I, _P, _P, _L, _P, _I, _L, _F, _P],
+    'srnn_logsoftmax_bwd': [_P, _L, _P, _L, _L, _I, _P, _I, _L, _P],
+    'srnn_nll_fwd': [_P, _L, _P, _L, _I, _L, _P, _P],
+    'srnn_nll_bwd': [_P, _L, _I, _L, _I, _P, _L, _F, _P],
+    'srnn_weight_norm_fwd': [_P, _P, _P, _P, _I, _L, _P],
+    'srnn_weight_norm_bwd': [_P, _P, _P, _P, _P, _I, _L, _I, _P],
+    'srnn_permute3': [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
+    'srnn_copy2d': [_I, _I, _I, _I, _P, _L, _P, _L, _P],
+    'srnn_gather_rows': [_P, _L, _P, _L, _I, _P, _I, _L, _P],
+    'srnn_scatter_add_rows': [_P, _L, _P, _L, _I, _P, _L, _P],
+    'srnn_axpby': [_P, _P, _P, _F, _F, _L, _P],
+    'srnn_add_bcast_rows': [_P, _P, _I, _I, _I, _L, _P],
+    'srnn_colsum': [_I, _P, _L, _L, _I, _P, _F, _I, _P, _L, _P],
+    'srnn_adam_clip': [_P, _P, _P, _P, _P, _L, _F, _F, _D, _D, _D, _D, _L, _P],
+    'srnn_gen_workspace_size': [_P, _I, ctypes.POINTER(_SZ)],
+    'srnn_generate': [_P, _I, _I, _P, _P, _P, _U64, _P, _P, _P, _SZ, _I, _P],
+}
+
+
+class SrnnTier(ctypes.Structure):
+    _fields_ = [('frame_size', _I), ('n_frame_samples', _I), ('in_dim', _I),
+                ('w_in', _P), ('b_in', _P),
+                ('w_ih', _P * MAX_RNN), ('b_ih', _P * MAX_RNN),
+                ('w_hh', _P * MAX_RNN), ('b_hh', _P * MAX_RNN),
+                ('w_up', _P), ('b_up', _P), ('h0', _P)]
+
+
+class SrnnModel(ctypes.Structure):
+    _fields_ = [('n_tiers', _I), ('n_rnn', _I), ('dim', _I), ('q_levels', _I),
+                ('cond_dim', _I), ('dtype', _I), ('tier', SrnnTier * MAX_TIERS),
+                ('tab', _P), ('w_hid', _P), ('b_hid', _P), ('w_out', _P), ('b_out', _P)]
+
+
+class _Lib:
+    def __init__(self, path):
+        if not os.path.exists(path):
+            raise ImportError('libsamplernn_hip.so not built (%s); run __graft_entry__.build()'
+                              % path)
+        self.dll = ctypes.CDLL(path)
+        self.dll.srnn_last_error.restype = ctypes.c_char_p
+        self.dll.srnn_last_error.argtypes = []
+        for name, args in _SIGS.items():
+            fn = getattr(self.dll, name)
+            fn.argtypes = args
+            fn.restype = _I
+
+    def call(self, name, *args):
+        rc = getattr(self.dll, name)(*args)
+        if rc != 0:
+            raise RuntimeError('%s failed (%d): %s' % (name, rc,
+                                                       self.dll.srnn_last_error().decode()))
+
+
+_LIB = None
+
+
+def lib():
+    """The loaded library (raises if absent: no fallback)."""
+    global _LIB
+    if _LIB is None:
+        _LIB = _Lib(LIB_PATH)
+    return _LIB
+
+
+def exported_symbols():
+    return sorted(_SIGS) + ['srnn_last_error', 'srnn_abi_version']
+
+
+# ------------------------------------------------------------------ helpers
+def ptr(t):
+    """Device/host pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dcode(t_or_dtype):
+    dt = t_or_dtype.dtype if isinstance(t_or_dtype, torch.Tensor) else t_or_dtype
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise TypeError('unsupported dtype %s' % dt)
+
+
+def need_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError('samplernn_hip: device tensor expected (got %s); the HIP path has '
+                               'no CPU fallback' % t.device)
+
+
+def gemm(a, b, transA=False, transB=False, out=None, out_dtype=torch.float32, bias=None,
+         bias_mode=1, relu=False, alpha=1.0, beta=0.0, cin=None, mask=None, M=None, N=None, K=None,
+         lda=None, ldb=None, ldc=None, ldcin=None, batch=1, sA=0, sB=0, sC=0, sCin=0, tile=-1):
+    """C = act(alpha op(A) op(B) + beta Cin + bias) on row-major 2-D views (or strided batches)."""
+    need_cuda(a, b)
+    if M is None:
+        M = a.shape[1] if transA else a.shape[0]
+        K = a.shape[0] if transA else a.shape[1]
+        N = b.shape[0] if transB else b.shape[1]
+    if lda is None:
+        lda = a.stride(0)
+    if ldb is None:
+        ldb = b.stride(0)
+    if out is None:
+        out = torch.empty((M, N), device=a.device, dtype=out_dtype)
+    if ldc is None:
+        ldc = out.stride(0) if out.dim() > 1 else N
+    if cin is not None and ldcin is None:
+        ldcin = cin.stride(0)
+    if a.dtype != b.dtype:
+        raise TypeError('gemm operands must share a dtype (%s vs %s)' % (a.dtype, b.dtype))
+    lib().call('srnn_gemm', dcode(a), dcode(out), int(transA), int(transB), M, N, K, alpha,
+               ptr(a), lda, sA, ptr(b), ldb, sB, beta, ptr(cin), ldcin or 0, sCin, ptr(out), ldc,
+               sC, ptr(bias), bias_mode, int(relu), batch, tile, ptr(mask),
+               (mask.stride(0) if mask is not None else 0), stream())
+    return out
+
+
+def linear(x, w, bias=None, relu=False, out_dtype=torch.float32, out=None, cin=None, beta=0.0):
+    """y = act(x . w^T + bias (+ beta * cin)) for 2-D x (M, K) and w (N, K)."""
+    return gemm(x, w, transB=True, bias=bias, relu=relu, out_dtype=out_dtype, out=out, cin=cin,
+                beta=beta)
+
+
+def colsum(x, rows, cols, lds=None, out=None, alpha=1.0, accumulate=False):
+    need_cuda(x)
+    if out is None:
+        out = torch.empty(cols, device=x.device, dtype=torch.float32)
+    lds = cols if lds is None else lds
+    work = torch.empty(max(1, (rows + 255) // 256) * cols + 256, device=x.device,
+                       dtype=torch.float32)
+    lib().call('srnn_colsum', dcode(x), ptr(x), lds, rows, cols, ptr(out), alpha, int(accumulate),
+               ptr(work), work.numel(), stream())
+    return out
+
+
+def cast(x, dtype):
+    """Dtype conversion through the HIP copy kernel (contiguous 2-D view)."""
+    need_cuda(x)
+    if x.dtype == dtype:
+        return x
+    x = x.contiguous()
+    out = torch.empty(x.shape, device=x.device, dtype=dtype)
+    cols = x.shape[-1] if x.dim() > 0 else 1
+    rows = x.numel() // max(cols, 1)
+    lib().call('srnn_copy2d', dcode(x), dcode(out), rows, cols, ptr(x), cols, ptr(out), cols,
+               stream())
+    return out
+
+
+def permute3(src, perm, dtype=torch.float32, out=None, accumulate=False):
+    """out = src.permute(perm).contiguous() (src fp32, 3-D) via the HIP permute kernel."""
+    need_cuda(src)
+    src = src.contiguous()
+    d = list(src.shape)
+    if out is None:
+        out = torch.empty([d[p] for p in perm], device=src.device, dtype=dtype)
+    lib().call('srnn_permute3', ptr(src), ptr(out), dcode(out), d[0], d[1], d[2], perm[0], perm[1],
+               perm[2], int(accumulate), stream())
+    return out
+
+
+def weight_norm(g, v):
+    """w = g * v / ||v|| (torch weight_norm, dim=0)."""
+    need_cuda(g, v)
+    v = v.contiguous()
+    w = torch.empty_like(v)
+    O = v.shape[0]
+    lib().call('srnn_weight_norm_fwd', ptr(g), ptr(v), ptr(w), None, O, v.numel() // O, stream())
+    return w
+
+
+def weight_norm_bwd(g, v, dw):
+    v = v.contiguous()
+    dw = dw.contiguous()
+    O = v.shape[0]
+    dg = torch.empty_like(g)
+    dv = torch.empty_like(v)
+    lib().call('srnn_weight_norm_bwd', ptr(g), ptr(v), ptr(dw), ptr(dg), ptr(dv), O,
+               v.numel() // O, 0, stream())
+    return dg, dv

