@@ -32,6 +32,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
     const T* B = reinterpret_cast<const T*>(g.B) + (int64_t)bz * g.sB;
     TO* Cp = reinterpret_cast<TO*>(g.C) + (int64_t)bz * g.sC;
     const float* Cin = g.Cin ? g.Cin + (int64_t)bz * g.sCin : nullptr;
+    const T* mask = g.mask ? reinterpret_cast<const T*>(g.mask) + (int64_t)bz * g.sC : nullptr;
     const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
     floatx4 acc[C::FM][C::FN];
 #pragma unroll
@@ -60,7 +61,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
                 if (g.bias_mode == 1) v += g.bias[col];
                 else if (g.bias_mode == 2) v += g.bias[row];
                 if (g.relu) v = fmaxf(v, 0.f);
-                if (g.mask && !(to_f(((const T*)g.mask)[(int64_t)row * g.ldmask + col]) > 0.f))
+                if (mask && !(to_f(mask[(int64_t)row * g.ldmask + col]) > 0.f))
                     v = 0.f;
                 Cp[(int64_t)row * g.ldc + col] = from_f<TO>(v);
             }
