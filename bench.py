@@ -1,0 +1,274 @@
+"""Benchmark of the SampleRNN hot path on MI355X (BASELINE.json metric).
+
+One JSON line (rank 0).  `value` = aggregate TBPTT training throughput (audio samples
+per second = ranks x B x T / step time) for configs[1]: 3-tier SampleRNN, dim 1024,
+frame_sizes [16, 4], 6-speaker + 43-d Ahocoder conditioning, T = 1024, B = 128 rows per
+GPU, bf16 MFMA (fp32 master weights / recurrences), one step = forward + backward +
+(all-reduce) + clipped Adam.  Weak scaling: every rank owns its own 128 stream rows.
+The line also carries `tbptt_steps_per_s`, the generation throughput of configs[2]
+(128 utterances x 3 s per GPU, replicas only), the roofline of the dominant kernel
+(measured with HIP events on the launching stream) and a bounded CPU baseline.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-gen] [--no-cpu]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, 'jalil-saboorizadeh-multi-speaker-neural-vocoder_amd')
+for p in (PKG, os.path.join(ROOT, 'tests', 'golden')):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+METRIC = ('audio samples/sec gen (3-tier dim1024) + TBPTT steps/sec @1/2/4/8 GPU')
+MI355X_HBM_TBS = 8.0          # TB/s spec (MI355X_MICROARCH.md)
+MI355X_BF16_TFLOPS = 2500.0   # dense bf16 MFMA spec
+MI355X_FP32_TFLOPS = 157.3    # fp32 MFMA / vector spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_model(dtype, seed=77977):
+    import model as M
+    torch.manual_seed(seed)
+    m = M.SampleRNN([16, 4], 1, 1024, True, 256, True, False, 43, 6)
+    m.compute_dtype = dtype
+    pred = M.Predictor(m)
+    return m, pred
+
+
+def synth_batches(B, T, L, n_chunks, row0, seed=0):
+    """Stateful TBPTT layout (dataset.py:155-163, 242-289) on synthetic 16 kHz streams:
+    sum of 3 sinusoids + Laplacian noise, float64 mu-law quantised, cond U[0,1), spk b%6."""
+    import recipe
+    import utils
+    total = n_chunks * T + L
+    audio = np.stack([recipe.synth_audio(total, seed + row0 + b) for b in range(B)])
+    idx = utils.uquantize(torch.from_numpy(audio), 256)           # host, float64 path
+    rng = np.random.Generator(np.random.PCG64(seed + 1000 + row0))
+    cond = rng.uniform(0, 1, (B, n_chunks * T // L, 43))
+    spk = ((np.arange(B) + row0) % 6).reshape(B, 1)
+    out = []
+    for n in range(n_chunks):
+        inp = idx[:, n * T: n * T + L + T - 1].contiguous()
+        tgt = idx[:, n * T + L: n * T + L + T].contiguous()
+        cnd = torch.from_numpy(np.ascontiguousarray(cond[:, n * T // L:(n + 1) * T // L]))
+        out.append((inp, n == 0, tgt, cnd, torch.from_numpy(spk)))
+    return out
+
+
+def gpu_batches(batches, dev):
+    return [(a.to(dev), r, t.to(dev), c.to(dev), s.to(dev)) for a, r, t, c, s in batches]
+
+
+def run_tbptt(args, dev, dist_mod):
+    import nn as snn
+    import optim
+    B, T, L = args.batch, 1024, 64
+    dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+    m, pred = make_model(dtype)
+    pred = pred.to(dev)
+    sync = dist_mod.GradAllReduce() if dist_mod.world() > 1 else None
+    opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3), grad_sync=sync)
+    rows = slice(0, B)
+    n_chunks = args.warmup + args.steps
+    batches = gpu_batches(synth_batches(B, T, L, n_chunks, dist_mod.rank() * B), dev)
+    losses = []
+
+    def step(n):
+        inp, reset, tgt, cnd, spk = batches[n]
+        for p in pred.parameters():
+            if p.grad is not None:
+                p.grad.zero_()
+
+        def closure():
+            lp = pred(inp, reset, cnd, spk)
+            loss = snn.sequence_nll_loss_bits(lp, tgt)
+            loss.backward()
+            return loss
+        return opt.step(closure)
+
+    for n in range(args.warmup):
+        losses.append(step(n))
+    torch.cuda.synchronize()
+    dist_mod.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for n in range(args.warmup, n_chunks):
+        losses.append(step(n))
+    torch.cuda.synchronize()
+    dist_mod.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt = dist_mod.max_over_ranks(dt, dev)
+    loss_vals = [float(l) for l in losses]
+    return dt, loss_vals, pred, m
+
+
+def run_gen(args, dev, n_seqs, n_cond, dtype):
+    import model as M
+    m, _ = make_model(dtype, seed=4242)
+    m = m.to(dev)
+    cond = torch.rand(n_seqs, n_cond, 43, generator=torch.Generator().manual_seed(1))
+    spk = np.arange(n_seqs) % 6
+    gen = M.Generator(m, True)
+    # warm-up (graph capture, kernel attributes) on a short run
+    gen(n_seqs, 0, cond[:, :4], spk, sampler='philox', seed=5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gen(n_seqs, 0, cond, spk, sampler='philox', seed=5)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0
+
+
+def kernel_roofline_gemm(dev, M, N, K, dtype, reps=20):
+    """Average duration of the dominant GEMM launch (same shape/layout/dtype as in the
+    step), timed with HIP events on the stream it is launched on."""
+    import samplernn_hip as H
+    a = torch.randn(M, K, device=dev).to(dtype)
+    w = torch.randn(N, K, device=dev).to(dtype)
+    bias = torch.zeros(N, device=dev)
+    out = torch.empty(M, N, device=dev, dtype=dtype)
+    for _ in range(3):
+        H.linear(a, w, bias=bias, relu=True, out=out)
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        H.linear(a, w, bias=bias, relu=True, out=out)
+    e1.record(s)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return ms
+
+
+def cpu_baseline(seconds_budget=20.0):
+    """The oracle (torch-CPU restatement of the reference) on the host cores: a bounded
+    TBPTT sample of the same workload (config B dims, T = 1024, B = 4 rows)."""
+    sys.path.insert(0, os.path.join(ROOT, 'oracle'))
+    import samplernn_oracle as O
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    m, pred = make_model(torch.float32)
+    sd = {k: v.detach().clone() for k, v in pred.state_dict().items()}
+    cfg = dict(frame_sizes=[16, 4], n_rnn=1, dim=1024, q_levels=256, weight_norm=False,
+               cond_dim=43, spk_dim=6)
+    om = O.from_state_dict(cfg, sd)
+    names = [k for k, p in pred.named_parameters()]
+    opt = O.OracleAdam([om.p[k] for k in names], lr=1e-3)
+    B = 4
+    batches = synth_batches(B, 1024, 64, 3, 0)
+    O.tbptt_step(om, opt, names, batches[0])          # warm-up
+    t0 = time.perf_counter()
+    n = 0
+    for b in batches[1:]:
+        O.tbptt_step(om, opt, names, b)
+        n += 1
+        if time.perf_counter() - t0 > seconds_budget:
+            break
+    dt = time.perf_counter() - t0
+    return {'value': round(n * B * 1024 / dt, 2), 'unit': 'samples/s', 'cores': threads,
+            'kind': 'port',
+            'sample': '%d TBPTT step(s) of the oracle (torch-CPU fp32 restatement) at config-B '
+                      'dims, B=%d rows x T=1024, %d threads' % (n, B, threads)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--batch', type=int, default=128)
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--gen-dtype', default='fp32', choices=['bf16', 'fp32'])
+    ap.add_argument('--gen-seqs', type=int, default=128)
+    ap.add_argument('--gen-cond', type=int, default=750)
+    ap.add_argument('--no-gen', action='store_true')
+    ap.add_argument('--no-cpu', action='store_true')
+    args = ap.parse_args()
+
+    import distributed as D
+    D.init()
+    dev = torch.device('cuda', D.local_rank())
+    torch.cuda.set_device(dev)
+    N = D.world()
+    if N != args.gpus:
+        log('warning: --gpus %d but WORLD_SIZE %d' % (args.gpus, N))
+
+    dt, losses, pred, m = run_tbptt(args, dev, D)
+    ms = dt / args.steps * 1000.0
+    rows = args.batch
+    samples = N * rows * 1024 * args.steps
+    value = samples / dt
+    log('tbptt: %.2f ms/step, losses %s' % (ms, ['%.3f' % l for l in losses]))
+    del pred, m
+    torch.cuda.empty_cache()
+
+    gen = None
+    if not args.no_gen:
+        gdt = torch.bfloat16 if args.gen_dtype == 'bf16' else torch.float32
+        t = run_gen(args, dev, args.gen_seqs, args.gen_cond, gdt)
+        t = D.max_over_ranks(t, dev)
+        gs = N * args.gen_seqs * args.gen_cond * 64 / t
+        steps_per_s = args.gen_cond * 64 / t
+        # algorithmic bytes per generation step: weights read once per step,
+        # tiers amortised by their clocks, + per-row activations
+        es = 2 if args.gen_dtype == 'bf16' else 4
+        W_step = 5571840 + 23110656 / 16 + 10616868 / 64
+        bytes_step = es * W_step + args.gen_seqs * (4 * (1024 + 256) + 8 * 16 + 8)
+        gen = {'value': round(gs, 1), 'unit': 'samples/s', 'x_realtime': round(gs / 16000, 1),
+               'x_realtime_per_gpu': round(gs / 16000 / N, 1), 'dtype': args.gen_dtype,
+               'seconds': round(t, 3), 'steps_per_s': round(steps_per_s, 1),
+               'config': {'workload': 'generate 3-tier dim1024 FS=[16,4], %d utt x %d cond '
+                                      'rows (%d samples) per GPU, Philox sampler'
+                                      % (args.gen_seqs, args.gen_cond, args.gen_cond * 64)},
+               'roofline': {'bound': 'hbm', 'achieved': round(bytes_step * steps_per_s / 1e9, 1),
+                            'peak': MI355X_HBM_TBS * 1000, 'unit': 'GB/s',
+                            'frac': round(bytes_step * steps_per_s / 1e9 / (MI355X_HBM_TBS * 1000),
+                                          4),
+                            'traffic': None}}
+        log('gen: %.3f s, %.0f samples/s (%.1fx realtime)' % (t, gs, gs / 16000))
+
+    # dominant kernel of the TBPTT step: the MLP hidden layer GEMM (B*T x D x D, bf16)
+    tdt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+    M_, N_, K_ = rows * 1024, 1024, 1024
+    kms = kernel_roofline_gemm(dev, M_, N_, K_, tdt)
+    flops = 2.0 * M_ * N_ * K_
+    ach = flops / (kms * 1e-3) / 1e12
+    peak = MI355X_BF16_TFLOPS if args.dtype == 'bf16' else MI355X_FP32_TFLOPS
+    roof = {'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
+            'frac': round(ach / peak, 4), 'traffic': None,
+            'kernel': 'gemm_kernel (MLP hidden layer %dx%dx%d %s, relu epilogue), %.3f ms/launch'
+                      % (M_, N_, K_, args.dtype, kms)}
+
+    cpu = None
+    if D.rank() == 0 and N == 1 and not args.no_cpu:
+        cpu = cpu_baseline()
+
+    if D.rank() == 0:
+        line = {'metric': METRIC, 'value': round(value, 1), 'unit': 'samples/s',
+                'n_gpus': N, 'steps': args.steps, 'warmup': args.warmup,
+                'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+                'vs_baseline': None, 'dtype': args.dtype, 'data': 'synthetic',
+                'config': {'workload': 'TBPTT step, 3-tier SampleRNN dim1024 FS=[16,4] n_rnn=1 '
+                                       'cond 43 spk 6, T=1024, B=%d rows/GPU, fwd+bwd+clip+Adam'
+                                       % rows,
+                           'global_batch': N * rows, 'seq_len': 1024,
+                           'parallelism': 'dp%d' % N},
+                'tbptt_steps_per_s': round(args.steps / dt, 3),
+                'roofline': roof, 'cpu_baseline': cpu, 'gen': gen,
+                'final_loss': round(losses[-1], 4)}
+        print(json.dumps(line), flush=True)
+    D.barrier()
+
+
+if __name__ == '__main__':
+    main()
