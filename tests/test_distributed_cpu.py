@@ -1,0 +1,108 @@
+"""world_size-2 gloo tests of the data-parallel TBPTT layer (distributed.py) on CPU.
+
+The HIP model needs a GPU, so the DP mechanics are exercised with a CPU stand-in
+recurrent model: rank r owns stream rows shard_rows(B, r, 2), gradients are averaged
+by GradAllReduce before the [-1, 1] clamp, and the result must equal a single-process
+full-batch step."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class _Toy(torch.nn.Module):
+    """Row-independent recurrent stand-in: h_t = tanh(W x_t + U h_{t-1}), loss = mean."""
+
+    def __init__(self):
+        super().__init__()
+        g = torch.Generator().manual_seed(0)
+        self.W = torch.nn.Parameter(torch.randn(5, 3, generator=g))
+        self.U = torch.nn.Parameter(torch.randn(5, 5, generator=g) * 0.3)
+        self.h0 = torch.nn.Parameter(torch.zeros(5))
+
+    def forward(self, x, h):
+        B, T, _ = x.shape
+        if h is None:
+            h = self.h0.expand(B, 5)
+        out = []
+        for t in range(T):
+            h = torch.tanh(x[:, t] @ self.W.t() + h @ self.U.t())
+            out.append(h)
+        return torch.stack(out, 1), h.detach()
+
+
+def _data(B=8, T=6, chunks=3):
+    g = torch.Generator().manual_seed(1)
+    return torch.randn(chunks, B, T, 3, generator=g) * 3
+
+
+def _train(model, data, rows, grad_sync):
+    import optim
+    opt = optim.gradient_clipping(torch.optim.SGD(model.parameters(), lr=0.1), -1, 1,
+                                  grad_sync=grad_sync)
+    h = None
+    losses = []
+    for n in range(data.shape[0]):
+        x = data[n][rows]
+
+        def closure():
+            nonlocal h
+            out, h_new = model(x, h if n > 0 else None)
+            loss = (out ** 2).mean() * 40.0          # large grads so the clamp is active
+            loss.backward()
+            closure.h = h_new
+            return loss
+        opt.zero_grad(set_to_none=False)
+        losses.append(float(opt.step(closure)))
+        h = closure.h
+    return losses, [p.detach().clone() for p in model.parameters()]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import distributed as D
+    D.init(backend='gloo')
+    data = _data()
+    rows = D.shard_rows(data.shape[1])
+    losses, params = _train(_Toy(), data, rows, D.GradAllReduce(bucket_mb=0.0001))
+    loss_t = torch.tensor(losses)
+    dist.all_reduce(loss_t)
+    if rank == 0:
+        q.put(((loss_t / world).tolist(), [p.tolist() for p in params]))
+    dist.destroy_process_group()
+
+
+def test_dp_two_ranks_equals_full_batch():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    losses_dp, params_dp = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    losses, params = _train(_Toy(), _data(), slice(0, 8), None)
+    assert torch.allclose(torch.tensor(losses_dp), torch.tensor(losses), atol=1e-5)
+    for a, b in zip(params_dp, params):
+        assert torch.allclose(torch.tensor(a), b, atol=1e-5)
+
+
+def test_shard_rows():
+    import distributed as D
+    assert D.shard_rows(512, 3, 8) == slice(192, 256)
+    with pytest.raises(ValueError):
+        D.shard_rows(10, 0, 3)
