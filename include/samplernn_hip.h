@@ -58,12 +58,14 @@ int srnn_gru_cell(int dtype, int B, int D, int Din, const void* x, int64_t ldx, 
                   int64_t ldho, void* hout_lp, int64_t ldhl, float* gates, int64_t ldgt,
                   void* stream);
 /* Backward of one step: dh_t = dy_t + dh_direct_{t+1} + dgh_{t+1} . W_hh, then the gate
- * backward.  Writes dgh_t (fp32 + optional T copy), dgi_t (fp32), dh_direct_t = z*dh_t. */
+ * backward.  Writes dgh_t (fp32 + optional T copy), dgi_t (fp32), dh_direct_t = z*dh_t.
+ * Pass W_hh (3D, D) and/or its transpose (D, 3D); the transpose enables the deep-ring
+ * kernel.                                                                                */
 int srnn_gru_cell_bwd(int dtype, int B, int D, const float* dy, int64_t lddy,
                       const void* dgh_next, int64_t lddgn, const float* ddir_next,
-                      const void* whh, const float* gates, int64_t ldgt, const float* hprev,
-                      int64_t ldhp, float* dgh, int64_t lddgh, void* dgh_lp, int64_t lddghl,
-                      float* dgi, int64_t lddgi, float* ddir, void* stream);
+                      const void* whh, const void* whh_t, const float* gates, int64_t ldgt,
+                      const float* hprev, int64_t ldhp, float* dgh, int64_t lddgh, void* dgh_lp,
+                      int64_t lddghl, float* dgi, int64_t lddgi, float* ddir, void* stream);
 
 /* ---- SampleLevelMLP (model.py:308-325) ----------------------------------------------
  * a1[b*Tlen+t] = relu(sum_k tab[k][x[b*ldx + xoff + t + k]] + upper[b*Tlen+t])          */

@@ -3,6 +3,7 @@
 // cond_expand / spk_expand conv-k1, GRU input projection, LearnedUpsampling1d, the
 // MLP hidden/output conv-k1 layers) and their backward dgrad/wgrad products.
 #include "gemm_core.hpp"
+#include "ring_core.hpp"
 #include "samplernn_hip_internal.hpp"
 
 struct GemmArgs {
@@ -68,6 +69,65 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
         }
 }
 
+// Skinny NT path (M = batch rows, e.g. the generation loop's y = x W^T with M = 128):
+// small tiles so >= 256 workgroups exist, and the deep glds ring of ring_core.hpp so a
+// workgroup's K chain is not one exposed memory latency per stage.
+template <typename T, typename TO, int BM, int BN, int WM, int WN, int WK>
+__global__ __launch_bounds__(256) void skinny_kernel(GemmArgs g) {
+    typedef Ring<T, BM, BN, WM, WN, WK, 4> R;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    floatx4 acc[R::FM][R::FN];
+#pragma unroll
+    for (int i = 0; i < R::FM; ++i)
+#pragma unroll
+        for (int j = 0; j < R::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    ring_core<T, BM, BN, WM, WN, WK, 4>((const T*)g.A, g.lda, RowClamp{m0, g.M}, (const T*)g.B,
+                                        g.ldb, RowClamp{n0, g.N}, g.K, smem, acc);
+    ring_reduce<T, BM, BN, WM, WN, WK, 4>(smem, acc);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
+    if (wk != 0) return;
+    TO* Cp = reinterpret_cast<TO*>(g.C);
+    const T* mask = reinterpret_cast<const T*>(g.mask);
+#pragma unroll
+    for (int fm = 0; fm < R::FM; ++fm)
+#pragma unroll
+        for (int fn = 0; fn < R::FN; ++fn) {
+            const int col = n0 + wn * R::FN * 16 + fn * 16 + (lane & 15);
+            if (col >= g.N) continue;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = m0 + wm * R::FM * 16 + fm * 16 + (lane >> 4) * 4 + i;
+                if (row >= g.M) continue;
+                float v = g.alpha * acc[fm][fn][i];
+                if (g.beta != 0.f) v += g.beta * g.Cin[(int64_t)row * g.ldcin + col];
+                if (g.bias_mode == 1) v += g.bias[col];
+                else if (g.bias_mode == 2) v += g.bias[row];
+                if (g.relu) v = fmaxf(v, 0.f);
+                if (mask && !(to_f(mask[(int64_t)row * g.ldmask + col]) > 0.f)) v = 0.f;
+                Cp[(int64_t)row * g.ldc + col] = from_f<TO>(v);
+            }
+        }
+}
+
+template <typename T, typename TO>
+static int launch_skinny(const GemmArgs& g, hipStream_t s) {
+    // 32 x 16 tiles (waves: 2 along M, 2 along K) unless 32 x 32 already gives 512 tiles
+    const int64_t t32 = (int64_t)cdiv(g.M, 32) * cdiv(g.N, 32);
+    if (t32 >= 512) {
+        typedef Ring<T, 32, 32, 2, 2, 1, 4> R;
+        dim3 grid(cdiv(g.N, 32), cdiv(g.M, 32));
+        hipLaunchKernelGGL((skinny_kernel<T, TO, 32, 32, 2, 2, 1>), grid, dim3(256), R::LDS, s, g);
+    } else {
+        typedef Ring<T, 32, 16, 2, 1, 2, 4> R;
+        dim3 grid(cdiv(g.N, 16), cdiv(g.M, 32));
+        hipLaunchKernelGGL((skinny_kernel<T, TO, 32, 16, 2, 1, 2>), grid, dim3(256), R::LDS, s, g);
+    }
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
 template <typename T, typename TO, int BM, int BN, int KS, int WM, int WN, int WK, bool KCA,
           bool KCB>
 static int launch_t(const GemmArgs& g, int batch, hipStream_t s) {
@@ -104,6 +164,21 @@ static int launch_types(const GemmArgs& g, int transA, int transB, int batch, in
     return launch_layout<T, TO, false, false>(g, batch, tile, s);
 }
 
+int srnn_gemm2_try(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
+                   float alpha, const void* A, int64_t lda, const void* B, int64_t ldb,
+                   float beta, const float* Cin, int64_t ldcin, void* C, int64_t ldc,
+                   const float* bias, int bias_mode, int relu, const void* mask, int64_t ldmask,
+                   hipStream_t s);
+
+static bool g_use_gemm2() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SRNN_GEMM2");
+        v = (e && e[0] == '0') ? 0 : 1;
+    }
+    return v == 1;
+}
+
 static int pick_tile(int M, int N, int batch) {
     const int64_t t128 = (int64_t)cdiv(M, 128) * cdiv(N, 128) * batch;
     if (t128 >= 256) return 0;
@@ -137,7 +212,28 @@ int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int 
     };
     g.vecA = aligned(A, lda, strideA);
     g.vecB = aligned(B, ldb, strideB);
-    if (tile < 0) tile = pick_tile(M, N, batch);
+    // skinny NT problems (M = batch rows): small-tile deep-ring kernel; tile 4 forces it
+    {
+        const int KBr = 256 / es;
+        const bool ok = batch == 1 && !transA && transB && K % KBr == 0 && K > 0 && g.vecA &&
+                        g.vecB && ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0);
+        if ((tile == 4 || (tile < 0 && M <= 256 && g_use_gemm2())) && ok) {
+            if (dtype == SRNN_F32)
+                return out_dtype == SRNN_F32 ? launch_skinny<float, float>(g, s)
+                                             : launch_skinny<float, bf16>(g, s);
+            return out_dtype == SRNN_F32 ? launch_skinny<bf16, float>(g, s)
+                                         : launch_skinny<bf16, bf16>(g, s);
+        }
+        SRNN_REQUIRE(tile != 4, "gemm: shape not eligible for the skinny path");
+    }
+    // large aligned problems: the glds-ring kernel (gemm2.hip); tile 3 forces it
+    if ((tile < 0 || tile == 3) && batch == 1 && g_use_gemm2()) {
+        int rc = srnn_gemm2_try(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, B, ldb,
+                                beta, Cin, ldcin, C, ldc, bias, bias_mode, relu, mask, ldmask, s);
+        if (rc >= 0) return rc;
+        SRNN_REQUIRE(tile != 3, "gemm: shape not eligible for the gemm2 path");
+    }
+    if (tile < 0 || tile == 3) tile = pick_tile(M, N, batch);
     if (dtype == SRNN_F32) {
         if (out_dtype == SRNN_F32) return launch_types<float, float>(g, transA, transB, batch, tile, s);
         return launch_types<float, bf16>(g, transA, transB, batch, tile, s);

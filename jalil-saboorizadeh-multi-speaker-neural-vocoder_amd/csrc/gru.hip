@@ -10,6 +10,7 @@
 // image: dh_t = dy_t + dh_direct + dgh_{t+1} . W_hh (MFMA over K = 3D), then the gate
 // backward in the epilogue.
 #include "gemm_core.hpp"
+#include "ring_core.hpp"
 #include "samplernn_hip_internal.hpp"
 
 struct GruCellArgs {
@@ -105,8 +106,79 @@ static inline bool al16(const void* p, int64_t ld, int es) {
     return ((uintptr_t)p % 16 == 0) && ((ld * es) % 16 == 0);
 }
 
+// Ring variant (ring_core.hpp): same tile (32 rows x 3 gates x 16 units), NS-1 k-stages
+// of both operands in flight.  Needs D (and Din) multiples of the ring stage.
+template <typename T>
+__global__ __launch_bounds__(256) void gru_cell_ring_kernel(GruCellArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int u0 = blockIdx.x * 16, m0 = blockIdx.y * 32;
+    floatx4 acc_h[1][3], acc_i[1][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc_h[0][j] = acc_i[0][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    const RowGateClamp gmap{u0, 16, a.D};
+    if (a.x)
+        ring_core<T, 32, 48, 2, 1, 2, 4>((const T*)a.x, a.ldx, RowClamp{m0, a.B}, (const T*)a.wih,
+                                         a.Din, gmap, a.Din, smem, acc_i);
+    ring_core<T, 32, 48, 2, 1, 2, 4>((const T*)a.h, a.ldh, RowClamp{m0, a.B}, (const T*)a.whh, a.D,
+                                     gmap, a.D, smem, acc_h);
+    if (a.x) ring_reduce<T, 32, 48, 2, 1, 2, 4>(smem, acc_i);
+    ring_reduce<T, 32, 48, 2, 1, 2, 4>(smem, acc_h);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wm = wave % 2, wk = wave / 2;
+    if (wk != 0) return;
+    const int u = u0 + (lane & 15);
+    if (u >= a.D) return;
+    const int D = a.D;
+    const float bhr = a.bhh[u], bhz = a.bhh[D + u], bhn = a.bhh[2 * D + u];
+    float bir = 0.f, biz = 0.f, bin = 0.f;
+    if (a.x) { bir = a.bih[u]; biz = a.bih[D + u]; bin = a.bih[2 * D + u]; }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wm * 16 + (lane >> 4) * 4 + i;
+        if (row >= a.B) continue;
+        float gir, giz, gin;
+        if (a.x) {
+            gir = acc_i[0][0][i] + bir; giz = acc_i[0][1][i] + biz; gin = acc_i[0][2][i] + bin;
+        } else {
+            const float* g = a.gi + (int64_t)row * a.ldgi;
+            gir = g[u]; giz = g[D + u]; gin = g[2 * D + u];
+        }
+        const float ghr = acc_h[0][0][i] + bhr;
+        const float ghz = acc_h[0][1][i] + bhz;
+        const float ghn = acc_h[0][2][i] + bhn;
+        const float r = 1.0f / (1.0f + expf(-(ghr + gir)));
+        const float z = 1.0f / (1.0f + expf(-(ghz + giz)));
+        const float n = tanhf(gin + ghn * r);
+        const float hp = a.hf[(int64_t)row * a.ldhf + u];
+        const float hn = (hp - n) * z + n;
+        a.hout[(int64_t)row * a.ldho + u] = hn;
+        if (a.hout_lp) ((T*)a.hout_lp)[(int64_t)row * a.ldhl + u] = from_f<T>(hn);
+        if (a.gates) {
+            float* gt = a.gates + (int64_t)row * a.ldgt;
+            gt[u] = r; gt[D + u] = z; gt[2 * D + u] = n; gt[3 * D + u] = ghn;
+        }
+    }
+}
+
 template <typename T, int BM>
 static int launch_cell(GruCellArgs& a, hipStream_t s) {
+    typedef Ring<T, 32, 48, 2, 1, 2, 4> R;
+    const int es = (int)sizeof(T);
+    const bool ring = a.D % R::KB == 0 && (!a.x || a.Din % R::KB == 0) && a.vec_h && a.vec_whh &&
+                      (!a.x || (a.vec_x && a.vec_wih));
+    if (ring) {
+        static bool attr = false;
+        if (!attr) {
+            SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)gru_cell_ring_kernel<T>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, R::LDS));
+            attr = true;
+        }
+        dim3 grid(cdiv(a.D, 16), cdiv(a.B, 32));
+        hipLaunchKernelGGL((gru_cell_ring_kernel<T>), grid, dim3(256), R::LDS, s, a);
+        SRNN_LAUNCH_CHECK();
+        (void)es;
+        return 0;
+    }
     constexpr int WM = BM / 16, WK = 4 / WM;
     typedef GemmCfg<T, BM, 48, 4, WM, 1, WK> C;
     dim3 grid(cdiv(a.D, 16), cdiv(a.B, BM));
@@ -146,7 +218,8 @@ struct GruBwdArgs {
     const float* dy; int64_t lddy;
     const void* dgh_next; int64_t lddgn;
     const float* ddir_next;        // (B, D) contiguous or null
-    const void* whh;
+    const void* whh;               // (3D, D) or null
+    const void* whh_t;             // (D, 3D) = W_hh^T or null (ring path)
     const float* gates; int64_t ldgt;
     const float* hprev; int64_t ldhp;
     float* dgh; int64_t lddgh;
@@ -154,8 +227,34 @@ struct GruBwdArgs {
     float* dgi; int64_t lddgi;
     float* ddir;                   // (B, D) contiguous
     int B, D;
-    int vec_dgn, vec_whh;
+    int vec_dgn, vec_whh, vec_wt;
 };
+
+template <typename T>
+__device__ __forceinline__ void gru_bwd_epilogue(const GruBwdArgs& a, int row, int u, float acc) {
+    const int D = a.D;
+    float dh = acc + a.dy[(int64_t)row * a.lddy + u];
+    if (a.ddir_next) dh += a.ddir_next[(int64_t)row * D + u];
+    const float* g = a.gates + (int64_t)row * a.ldgt;
+    const float r = g[u], z = g[D + u], n = g[2 * D + u], ghn = g[3 * D + u];
+    const float hp = a.hprev[(int64_t)row * a.ldhp + u];
+    const float dn = dh * (1.0f - z);
+    const float dz = dh * (hp - n);
+    const float dan = dn * (1.0f - n * n);
+    const float dr = dan * ghn;
+    const float dar = dr * r * (1.0f - r);
+    const float daz = dz * z * (1.0f - z);
+    const float dghn = dan * r;
+    float* dgh = a.dgh + (int64_t)row * a.lddgh;
+    dgh[u] = dar; dgh[D + u] = daz; dgh[2 * D + u] = dghn;
+    if (a.dgh_lp) {
+        T* dl = (T*)a.dgh_lp + (int64_t)row * a.lddghl;
+        dl[u] = from_f<T>(dar); dl[D + u] = from_f<T>(daz); dl[2 * D + u] = from_f<T>(dghn);
+    }
+    float* dgi = a.dgi + (int64_t)row * a.lddgi;
+    dgi[u] = dar; dgi[D + u] = daz; dgi[2 * D + u] = dan;
+    a.ddir[(int64_t)row * D + u] = dh * z;
+}
 
 template <typename T, int BM>
 __global__ __launch_bounds__(256) void gru_bwd_kernel(GruBwdArgs a) {
@@ -183,33 +282,52 @@ __global__ __launch_bounds__(256) void gru_bwd_kernel(GruBwdArgs a) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = m0 + wm * C::FM * 16 + fm * 16 + (lane >> 4) * 4 + i;
-            if (row >= a.B) continue;
-            float dh = acc[fm][0][i] + a.dy[(int64_t)row * a.lddy + u];
-            if (a.ddir_next) dh += a.ddir_next[(int64_t)row * D + u];
-            const float* g = a.gates + (int64_t)row * a.ldgt;
-            const float r = g[u], z = g[D + u], n = g[2 * D + u], ghn = g[3 * D + u];
-            const float hp = a.hprev[(int64_t)row * a.ldhp + u];
-            const float dn = dh * (1.0f - z);
-            const float dz = dh * (hp - n);
-            const float dan = dn * (1.0f - n * n);
-            const float dr = dan * ghn;
-            const float dar = dr * r * (1.0f - r);
-            const float daz = dz * z * (1.0f - z);
-            const float dghn = dan * r;
-            float* dgh = a.dgh + (int64_t)row * a.lddgh;
-            dgh[u] = dar; dgh[D + u] = daz; dgh[2 * D + u] = dghn;
-            if (a.dgh_lp) {
-                T* dl = (T*)a.dgh_lp + (int64_t)row * a.lddghl;
-                dl[u] = from_f<T>(dar); dl[D + u] = from_f<T>(daz); dl[2 * D + u] = from_f<T>(dghn);
-            }
-            float* dgi = a.dgi + (int64_t)row * a.lddgi;
-            dgi[u] = dar; dgi[D + u] = daz; dgi[2 * D + u] = dan;
-            a.ddir[(int64_t)row * D + u] = dh * z;
+            if (row < a.B) gru_bwd_epilogue<T>(a, row, u, acc[fm][0][i]);
         }
+}
+
+// ring variant: dgh_next (B, 3D) . W_hh^T^T with W_hh^T (D, 3D) k-contiguous
+template <typename T>
+__global__ __launch_bounds__(256) void gru_bwd_ring_kernel(GruBwdArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int u0 = blockIdx.x * 16, m0 = blockIdx.y * 32;
+    const int D = a.D;
+    floatx4 acc[1][1];
+    acc[0][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+    if (a.dgh_next) {
+        ring_core<T, 32, 16, 2, 1, 2, 4>((const T*)a.dgh_next, a.lddgn, RowClamp{m0, a.B},
+                                         (const T*)a.whh_t, 3 * D, RowClamp{u0, D}, 3 * D, smem,
+                                         acc);
+        ring_reduce<T, 32, 16, 2, 1, 2, 4>(smem, acc);
+    }
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wm = wave % 2, wk = wave / 2;
+    if (wk != 0) return;
+    const int u = u0 + (lane & 15);
+    if (u >= D) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int row = m0 + wm * 16 + (lane >> 4) * 4 + i;
+        if (row < a.B) gru_bwd_epilogue<T>(a, row, u, acc[0][0][i]);
+    }
 }
 
 template <typename T, int BM>
 static int launch_bwd(GruBwdArgs& a, hipStream_t s) {
+    typedef Ring<T, 32, 16, 2, 1, 2, 4> R;
+    if (a.whh_t && (3 * a.D) % R::KB == 0 && a.vec_wt && (!a.dgh_next || a.vec_dgn)) {
+        static bool attr = false;
+        if (!attr) {
+            SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)gru_bwd_ring_kernel<T>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, R::LDS));
+            attr = true;
+        }
+        dim3 grid(cdiv(a.D, 16), cdiv(a.B, 32));
+        hipLaunchKernelGGL((gru_bwd_ring_kernel<T>), grid, dim3(256), R::LDS, s, a);
+        SRNN_LAUNCH_CHECK();
+        return 0;
+    }
+    SRNN_REQUIRE(a.whh, "gru_cell_bwd: W_hh needed for this shape");
     constexpr int WM = BM / 16, WK = 4 / WM;
     typedef GemmCfg<T, BM, 16, 4, WM, 1, WK> C;
     dim3 grid(cdiv(a.D, 16), cdiv(a.B, BM));
@@ -220,21 +338,23 @@ static int launch_bwd(GruBwdArgs& a, hipStream_t s) {
 
 extern "C" int srnn_gru_cell_bwd(int dtype, int B, int D, const float* dy, int64_t lddy,
                                  const void* dgh_next, int64_t lddgn, const float* ddir_next,
-                                 const void* whh, const float* gates, int64_t ldgt,
-                                 const float* hprev, int64_t ldhp, float* dgh, int64_t lddgh,
-                                 void* dgh_lp, int64_t lddghl, float* dgi, int64_t lddgi,
-                                 float* ddir, void* stream) {
+                                 const void* whh, const void* whh_t, const float* gates,
+                                 int64_t ldgt, const float* hprev, int64_t ldhp, float* dgh,
+                                 int64_t lddgh, void* dgh_lp, int64_t lddghl, float* dgi,
+                                 int64_t lddgi, float* ddir, void* stream) {
     SRNN_REQUIRE(B > 0 && D > 0 && dy && gates && hprev && dgh && dgi && ddir,
                  "gru_cell_bwd: bad args");
     SRNN_REQUIRE(ddir != ddir_next, "gru_cell_bwd: ddir must not alias ddir_next");
+    SRNN_REQUIRE(whh || whh_t, "gru_cell_bwd: need W_hh or W_hh^T");
     const int es = dtype == SRNN_F32 ? 4 : 2;
     GruBwdArgs a;
     a.dy = dy; a.lddy = lddy; a.dgh_next = dgh_next; a.lddgn = lddgn; a.ddir_next = ddir_next;
-    a.whh = whh; a.gates = gates; a.ldgt = ldgt; a.hprev = hprev; a.ldhp = ldhp;
+    a.whh = whh; a.whh_t = whh_t; a.gates = gates; a.ldgt = ldgt; a.hprev = hprev; a.ldhp = ldhp;
     a.dgh = dgh; a.lddgh = lddgh; a.dgh_lp = dgh_lp; a.lddghl = lddghl;
     a.dgi = dgi; a.lddgi = lddgi; a.ddir = ddir; a.B = B; a.D = D;
     a.vec_dgn = dgh_next ? al16(dgh_next, lddgn, es) : 0;
-    a.vec_whh = al16(whh, D, es);
+    a.vec_whh = whh ? al16(whh, D, es) : 0;
+    a.vec_wt = whh_t ? al16(whh_t, 3 * (int64_t)D, es) : 0;
     if (dtype == SRNN_F32) return launch_bwd<float, 32>(a, (hipStream_t)stream);
     return launch_bwd<bf16, 32>(a, (hipStream_t)stream);
 }

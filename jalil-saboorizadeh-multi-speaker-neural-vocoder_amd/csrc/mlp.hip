@@ -12,6 +12,8 @@
 // The generation sampler draws  argmax(exp(logp) / q), q ~ Exp(1)  -- exactly how
 // torch>=2 implements `multinomial(1)` on CPU (model.py:514-517) -- with q either
 // supplied (bit-replay of the reference's RNG) or from a counter-based Philox4x32-10.
+#include <algorithm>
+
 #include "samplernn_hip_internal.hpp"
 
 // ------------------------------------------------------------------ L1 gather
@@ -347,8 +349,12 @@ extern "C" int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int6
     if (rows <= 0) return 0;
     const int lds = FS0 * Q * 8 * 4;
     SRNN_REQUIRE(lds <= 160 * 1024, "dtab: FS0*Q too large for LDS");
-    const int rpb = 2048;
-    dim3 grid(cdiv(D, 8), cdiv(rows, rpb));
+    // ~1024 workgroups: each flushes its FS0*Q*8 LDS accumulator with global atomics
+    // once, so fewer, longer row blocks keep the flush traffic (not the LDS atomics) small
+    const int nslices = cdiv(D, 8);
+    const int nrb = std::max(1, std::min(cdiv(rows, 256), 1024 / std::max(1, nslices)));
+    const int rpb = cdiv(rows, nrb);
+    dim3 grid(nslices, cdiv(rows, rpb));
     hipStream_t s = (hipStream_t)stream;
     static bool attr = false;
     if (!attr) {

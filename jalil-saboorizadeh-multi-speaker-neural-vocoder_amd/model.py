@@ -315,6 +315,8 @@ class _TierFn(torch.autograd.Function):
             dGHT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T) if lp else dGH
             dGI = torch.empty((B, Fr, 3 * D), device=dev, dtype=torch.float32)
             ddir = [torch.empty((B, D), device=dev, dtype=torch.float32) for _ in range(2)]
+            # W_hh^T (D, 3D): k-contiguous operand for the deep-ring backward kernel
+            WhhT = H.permute3(Whh[l].float().reshape(1, 3 * D, D), (0, 2, 1), dtype=T)
             for t in reversed(range(Fr)):
                 nxt = t + 1 < Fr
                 if t > 0:
@@ -324,7 +326,7 @@ class _TierFn(torch.autograd.Function):
                 H.lib().call('srnn_gru_cell_bwd', H.dcode(T), B, D, H.ptr(dOut[:, t]), Fr * D,
                              H.ptr(dGHT[:, t + 1]) if nxt else None, Fr * 3 * D,
                              H.ptr(ddir[(t + 1) % 2]) if nxt else None, H.ptr(Whh[l]),
-                             H.ptr(gates[l][:, t]), Fr * 4 * D, H.ptr(hp), ldhp,
+                             H.ptr(WhhT), H.ptr(gates[l][:, t]), Fr * 4 * D, H.ptr(hp), ldhp,
                              H.ptr(dGH[:, t]), Fr * 3 * D,
                              H.ptr(dGHT[:, t]) if lp else None, Fr * 3 * D,
                              H.ptr(dGI[:, t]), Fr * 3 * D, H.ptr(ddir[t % 2]), st())

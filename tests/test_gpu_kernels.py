@@ -40,6 +40,45 @@ def test_gemm_layouts(hip, dtype, transA, transB, tile, M, N, K):
     torch.testing.assert_close(out.cpu(), ref, atol=tol, rtol=1e-4)
 
 
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('transA,transB', [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize('M,N,K,epi', [(256, 384, 512, True), (384, 128, 256, True),
+                                       (128, 256, 8192, False)])
+def test_gemm2_ring_kernel(hip, dtype, transA, transB, M, N, K, epi):
+    """The glds-ring kernel (tile 3 forces it): all layouts, epilogue and split-K paths."""
+    A = _rand(K, M, seed=1) if transA else _rand(M, K, seed=1)
+    B = _rand(N, K, seed=2) if transB else _rand(K, N, seed=2)
+    Ad, Bd = A.to(DEV, dtype), B.to(DEV, dtype)
+    Af, Bf = Ad.float().cpu(), Bd.float().cpu()
+    ref = (Af.t() if transA else Af) @ (Bf.t() if transB else Bf)
+    if epi:
+        bias = _rand(N, seed=3)
+        cin = _rand(M, N, seed=4)
+        out = hip.gemm(Ad, Bd, transA=bool(transA), transB=bool(transB), bias=bias.to(DEV),
+                       cin=cin.to(DEV), beta=0.5, relu=True, tile=3)
+        ref = (ref + 0.5 * cin + bias).clamp_min(0)
+    else:   # plain fp32 output with few tiles -> split-K with atomics
+        out = hip.gemm(Ad, Bd, transA=bool(transA), transB=bool(transB), tile=3)
+    tol = 1e-4 * np.sqrt(K) if dtype == torch.float32 else 2e-3 * np.sqrt(K)
+    torch.testing.assert_close(out.cpu(), ref, atol=tol, rtol=1e-4)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('M,N,K', [(128, 1024, 1024), (67, 256, 512), (128, 40, 256),
+                                   (256, 2048, 256)])
+def test_gemm_skinny_ring(hip, dtype, M, N, K):
+    """Skinny NT deep-ring kernel (tile 4 forces it), with the full epilogue."""
+    A, W = _rand(M, K, seed=1), _rand(N, K, seed=2)
+    bias, cin, mask = _rand(N, seed=3), _rand(M, N, seed=4), _rand(M, N, seed=5)
+    Ad, Wd = A.to(DEV, dtype), W.to(DEV, dtype)
+    out = hip.gemm(Ad, Wd, transB=True, bias=bias.to(DEV), cin=cin.to(DEV), beta=0.25,
+                   relu=True, mask=mask.to(DEV, dtype), tile=4)
+    ref = ((Ad.float().cpu() @ Wd.float().cpu().t()) + 0.25 * cin + bias).clamp_min(0)
+    ref = ref * (mask.to(dtype).float() > 0)
+    tol = 1e-4 * np.sqrt(K) if dtype == torch.float32 else 2e-3 * np.sqrt(K)
+    torch.testing.assert_close(out.cpu(), ref, atol=tol, rtol=1e-4)
+
+
 def test_gemm_bf16_out_batched_mask(hip):
     Bt, M, N, K = 3, 40, 72, 48
     A = _rand(Bt, M, K, seed=5).to(DEV)
@@ -54,8 +93,9 @@ def test_gemm_bf16_out_batched_mask(hip):
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('with_x', [False, True])
-def test_gru_cell(hip, dtype, with_x):
-    B, D = 67, 80
+@pytest.mark.parametrize('D', [80, 256])     # 256: deep-ring kernel path
+def test_gru_cell(hip, dtype, with_x, D):
+    B = 67
     x = _rand(B, D, seed=1).to(DEV)
     h = _rand(B, D, seed=2).to(DEV)
     wih = _rand(3 * D, D, scale=0.3, seed=3).to(DEV)
@@ -83,9 +123,10 @@ def test_gru_cell(hip, dtype, with_x):
     torch.testing.assert_close(gates[:, 3 * D:].cpu(), gh_r[:, 2 * D:], atol=tol * 10, rtol=0)
 
 
-def test_gru_cell_bwd(hip):
+@pytest.mark.parametrize('D,ring', [(48, False), (256, True)])
+def test_gru_cell_bwd(hip, D, ring):
     """Gate backward + dgh . W_hh against autograd of the torch formula (fp32)."""
-    B, D = 33, 48
+    B = 33
     h = _rand(B, D, seed=2).requires_grad_(True)
     gi = _rand(B, 3 * D, seed=3)
     whh = _rand(3 * D, D, scale=0.3, seed=4)
@@ -105,9 +146,28 @@ def test_gru_cell_bwd(hip):
     hd = h.detach().to(DEV)
     dyd = dy.to(DEV)
     hip.lib().call('srnn_gru_cell_bwd', hip.F32, B, D, hip.ptr(dyd), D, None, 0, None,
-                   hip.ptr(whh.to(DEV)), hip.ptr(gates), 4 * D, hip.ptr(hd), D, hip.ptr(dgh),
+                   hip.ptr(whh.to(DEV)), None, hip.ptr(gates), 4 * D, hip.ptr(hd), D, hip.ptr(dgh),
                    3 * D, None, 0, hip.ptr(dgi), 3 * D, hip.ptr(ddir), hip.stream())
     torch.testing.assert_close(dgh.cpu(), gh.grad, atol=1e-5, rtol=1e-4)
+    # a second step consuming dgh as dgh_next exercises the dgh . W_hh product (ring path
+    # when W_hh^T is given)
+    whh_d = whh.to(DEV)
+    whh_t = whh_d.t().contiguous() if ring else None
+    dgh2 = torch.empty_like(dgh)
+    dgi2 = torch.empty_like(dgi)
+    ddir2 = torch.empty_like(ddir)
+    hip.lib().call('srnn_gru_cell_bwd', hip.F32, B, D, hip.ptr(dyd), D, hip.ptr(dgh), 3 * D,
+                   hip.ptr(ddir), hip.ptr(whh_d), hip.ptr(whh_t), hip.ptr(gates), 4 * D,
+                   hip.ptr(hd), D, hip.ptr(dgh2), 3 * D, None, 0, hip.ptr(dgi2), 3 * D,
+                   hip.ptr(ddir2), hip.stream())
+    dh2 = dy + ddir.cpu() + dgh.cpu() @ whh
+    g = gates.cpu()
+    r_, z_, n_, ghn_ = g[:, :D], g[:, D:2 * D], g[:, 2 * D:3 * D], g[:, 3 * D:]
+    dan = dh2 * (1 - z_) * (1 - n_ * n_)
+    ref_dgh2 = torch.cat([dan * ghn_ * r_ * (1 - r_), dh2 * (h.detach() - n_) * z_ * (1 - z_),
+                          dan * r_], 1)
+    torch.testing.assert_close(dgh2.cpu(), ref_dgh2, atol=2e-5, rtol=1e-4)
+    torch.testing.assert_close(ddir2.cpu(), dh2 * z_, atol=2e-5, rtol=1e-4)
     # dh_prev = z*dy + dgh . W_hh  ==  autograd's h.grad
     dh = hip.gemm(dgh, whh.to(DEV), cin=ddir, beta=1.0)
     torch.testing.assert_close(dh.cpu(), h.grad, atol=1e-5, rtol=1e-4)

@@ -1,0 +1,51 @@
+"""Microbenchmark of libsamplernn_hip GEMM shapes used by the TBPTT step (HIP events)."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, 'jalil-saboorizadeh-multi-speaker-neural-vocoder_amd'))
+import samplernn_hip as H  # noqa: E402
+
+DEV = 'cuda'
+
+
+def timeit(fn, reps=10):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def run(M, N, K, tA, tB, dtype, out_dtype, tile, tag):
+    A = torch.randn(K, M, device=DEV).to(dtype) if tA else torch.randn(M, K, device=DEV).to(dtype)
+    B = torch.randn(N, K, device=DEV).to(dtype) if tB else torch.randn(K, N, device=DEV).to(dtype)
+    out = torch.empty(M, N, device=DEV, dtype=out_dtype)
+    ms = timeit(lambda: H.gemm(A, B, transA=tA, transB=tB, out=out, tile=tile))
+    tf = 2.0 * M * N * K / ms / 1e9
+    print('%-34s tile=%2d %7.3f ms %8.1f TFLOP/s' % (tag, tile, ms, tf), flush=True)
+
+
+if __name__ == '__main__':
+    bf, f32 = torch.bfloat16, torch.float32
+    shapes = [
+        (131072, 1024, 1024, False, True, bf, bf, 'mlp hidden fwd NT'),
+        (131072, 256, 1024, False, True, bf, f32, 'mlp out fwd NT'),
+        (131072, 1024, 1024, False, False, bf, f32, 'mlp dgrad NN'),
+        (1024, 1024, 131072, True, False, bf, f32, 'mlp wgrad TN'),
+        (8192, 16384, 1024, False, True, bf, f32, 'upsample fwd NT'),
+        (8192, 1024, 16384, False, False, bf, f32, 'upsample dgrad NN'),
+        (16384, 1024, 8192, True, False, bf, f32, 'upsample wgrad TN'),
+        (8192, 3072, 1024, False, True, bf, f32, 'gru gi fwd NT'),
+        (3072, 1024, 8192, True, False, bf, f32, 'gru wgrad TN'),
+        (128, 1024, 1024, False, True, f32, f32, 'gen L2 fp32 NT (skinny)'),
+    ]
+    for (M, N, K, tA, tB, dt, odt, tag) in shapes:
+        for tile in (-1, 0):
+            run(M, N, K, tA, tB, dt, odt, tile, tag)
