@@ -35,11 +35,19 @@ __global__ __launch_bounds__(256) void mlp_l1_kernel(const T* __restrict__ tab,
     const float* ur = upper + r * ldu + o0;
 #pragma unroll
     for (int j = 0; j < VPT; ++j) acc[j] = ur[j];
-    for (int k = 0; k < FS0; ++k) {
-        const int64_t q = xr[k];
-        const T* tr = tab + ((int64_t)k * Q + q) * D + o0;
+    // all index loads first, then all table-row loads: one exposed latency, not FS0
+    constexpr int KMAX = 32;
+    int qs[KMAX];
 #pragma unroll
-        for (int j = 0; j < VPT; ++j) acc[j] += to_f(tr[j]);
+    for (int k = 0; k < KMAX; ++k)
+        if (k < FS0) qs[k] = (int)xr[k];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k) {
+        if (k < FS0) {
+            const T* tr = tab + ((int64_t)k * Q + qs[k]) * D + o0;
+#pragma unroll
+            for (int j = 0; j < VPT; ++j) acc[j] += to_f(tr[j]);
+        }
     }
     T* orow = out + r * ldo + o0;
 #pragma unroll
@@ -50,6 +58,7 @@ int srnn_mlp_l1_impl(int dtype, const void* tab, const int64_t* x, int64_t ldx, 
                      const int* base, int B, int Tlen, const float* upper, int64_t ldu, void* out,
                      int64_t ldo, int D, int FS0, int Q, hipStream_t s) {
     SRNN_REQUIRE(D % 4 == 0, "mlp_l1: D must be a multiple of 4");
+    SRNN_REQUIRE(FS0 <= 32, "mlp_l1: frame_sizes[0] must be <= 32");
     dim3 grid(cdiv(D, 256 * 4), (int64_t)B * Tlen);
     if (dtype == SRNN_F32)
         hipLaunchKernelGGL((mlp_l1_kernel<float, 4>), grid, dim3(256), 0, s, (const float*)tab, x,
@@ -304,72 +313,103 @@ int srnn_sample_impl(const float* z, int64_t ldz, int B, const float* noise, uin
 }
 
 // ------------------------------------------------------------------ dTab scatter
-// dTab[x_{b, t+k}][k][:] += da[b, t, :]  over all rows: per (row block, 64-column slice)
-// the workgroup accumulates into an LDS copy of dTab[:, :, slice] (FS0*Q*64 fp32 would be
-// 1 MiB for FS0=16, so the slice is 8 columns: 16*256*8*4 = 128 KiB) with LDS atomics,
-// then flushes it with global atomics.
-template <typename T>
+// dTab[x_{b, t+k}][k][:] += da[b, t, :] over all rows (backward of the folded
+// embedding . conv).  A workgroup owns a slice of CW columns and a block of nb whole batch
+// rows: it stages the block's sample indices in LDS as bytes (one read per index instead
+// of one global load per (row, tap, column)), keeps dTab[:, :, slice] (Q x FS0 x CW fp32)
+// in LDS, and gives every thread a fixed (tap k, column c): per row it does one global
+// load of da (coalesced over c, L1-shared over k), one LDS byte read and one LDS atomic
+// add; the accumulator is flushed with global atomics once per workgroup.
+template <typename T, int CW>
 __global__ __launch_bounds__(256) void dtab_kernel(const T* __restrict__ da, int64_t ldda,
                                                    const int64_t* __restrict__ x, int64_t ldx,
-                                                   int xoff, int Tlen, int64_t rows,
-                                                   int rows_per_block, float* __restrict__ dtab,
-                                                   int D, int FS0, int Q) {
+                                                   int xoff, int Tlen, int B, int nb,
+                                                   float* __restrict__ dtab, int D, int FS0,
+                                                   int Q) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* acc = reinterpret_cast<float*>(smem);   // [FS0][Q][8]
-    const int c0 = blockIdx.x * 8;
-    const int n = FS0 * Q * 8;
-    for (int i = threadIdx.x; i < n; i += 256) acc[i] = 0.f;
+    float* acc = reinterpret_cast<float*>(smem);                       // [Q][FS0][CW]
+    unsigned char* idx = reinterpret_cast<unsigned char*>(smem + Q * FS0 * CW * 4);
+    const int tid = threadIdx.x;
+    const int c0 = blockIdx.x * CW;
+    const int b0 = blockIdx.y * nb;
+    const int nbb = min(nb, B - b0);
+    const int W = Tlen + FS0 - 1;
+    const int nacc = Q * FS0 * CW;
+    for (int i = tid; i < nacc; i += 256) acc[i] = 0.f;
+    for (int i = tid; i < nbb * W; i += 256) {
+        const int b = i / W, p = i - b * W;
+        idx[i] = (unsigned char)x[(int64_t)(b0 + b) * ldx + xoff + p];
+    }
     __syncthreads();
-    const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
-    const int64_t r1 = min(rows, r0 + rows_per_block);
-    // each thread: one (row, column) pair per iteration; 32 rows x 8 cols per pass
-    const int cc = threadIdx.x & 7;
-    for (int64_t r = r0 + (threadIdx.x >> 3); r < r1; r += 32) {
-        const int b = r / Tlen, t = r % Tlen;
-        const int64_t* xr = x + (int64_t)b * ldx + xoff + t;
-        const float g = (c0 + cc < D) ? to_f(da[r * ldda + c0 + cc]) : 0.f;
-        if (g != 0.f) {
-            for (int k = 0; k < FS0; ++k) atomicAdd(&acc[(k * Q + (int)xr[k]) * 8 + cc], g);
+    const int per_row = FS0 * CW;
+    const int rpp = 256 / per_row;                 // rows per pass
+    if (tid < rpp * per_row) {
+        const int rem = tid % per_row;
+        const int k = rem / CW, c = rem % CW;
+        const bool cok = c0 + c < D;
+        int b = 0, t = tid / per_row;
+        const int nrows = nbb * Tlen;
+        const T* dab = da + (int64_t)b0 * Tlen * ldda + c0 + c;
+        float* ak = acc + k * CW + c;
+        for (int r = tid / per_row; r < nrows; r += rpp) {
+            const float g = cok ? to_f(dab[(int64_t)r * ldda]) : 0.f;
+            const int q = idx[b * W + t + k];
+            atomicAdd(ak + q * FS0 * CW, g);
+            t += rpp;
+            while (t >= Tlen) { t -= Tlen; ++b; }
         }
     }
     __syncthreads();
-    // flush q-major: dtab[(q * FS0 + k) * D + c]  (the layout the dE GEMM consumes)
-    for (int i = threadIdx.x; i < n; i += 256) {
+    for (int i = tid; i < nacc; i += 256) {
         const float v = acc[i];
-        const int c = c0 + (i & 7);
-        const int kq = i >> 3, k = kq / Q, q = kq % Q;
-        if (v != 0.f && c < D) atomicAdd(&dtab[((int64_t)q * FS0 + k) * D + c], v);
+        const int c = i % CW, qk = i / CW;         // qk = q * FS0 + k
+        if (v != 0.f && c0 + c < D) atomicAdd(&dtab[(int64_t)qk * D + c0 + c], v);
     }
+}
+
+template <typename T, int CW>
+static int launch_dtab(const void* da, int64_t ldda, const int64_t* x, int64_t ldx, int xoff,
+                       int B, int Tlen, float* dtab, int D, int FS0, int Q, hipStream_t s) {
+    const int acc_bytes = Q * FS0 * CW * 4;
+    const int W = Tlen + FS0 - 1;
+    const int nb_cap = std::max(1, (160 * 1024 - acc_bytes) / W);
+    const int nslices = cdiv(D, CW);
+    // enough row blocks to give ~1024 workgroups, as few as LDS allows otherwise
+    int nblk = std::max(1, 1024 / nslices);
+    int nb = std::min(B, std::max(cdiv(B, nblk), 1));
+    nb = std::min(nb, nb_cap);
+    const int lds = acc_bytes + ((nb * W + 15) / 16) * 16;
+    static bool attr = false;
+    if (!attr) {
+        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_kernel<T, CW>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    dim3 grid(nslices, cdiv(B, nb));
+    hipLaunchKernelGGL((dtab_kernel<T, CW>), grid, dim3(256), lds, s, (const T*)da, ldda, x, ldx,
+                       xoff, Tlen, B, nb, dtab, D, FS0, Q);
+    SRNN_LAUNCH_CHECK();
+    return 0;
 }
 
 extern "C" int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x,
                              int64_t ldx, int xoff, int B, int Tlen, float* dtab, int D, int FS0,
                              int Q, void* stream) {
-    const int64_t rows = (int64_t)B * Tlen;
-    if (rows <= 0) return 0;
-    const int lds = FS0 * Q * 8 * 4;
-    SRNN_REQUIRE(lds <= 160 * 1024, "dtab: FS0*Q too large for LDS");
-    // ~1024 workgroups: each flushes its FS0*Q*8 LDS accumulator with global atomics
-    // once, so fewer, longer row blocks keep the flush traffic (not the LDS atomics) small
-    const int nslices = cdiv(D, 8);
-    const int nrb = std::max(1, std::min(cdiv(rows, 256), 1024 / std::max(1, nslices)));
-    const int rpb = cdiv(rows, nrb);
-    dim3 grid(nslices, cdiv(rows, rpb));
+    if ((int64_t)B * Tlen <= 0) return 0;
+    SRNN_REQUIRE(Q <= 256, "dtab: q_levels must be <= 256 (byte indices)");
+    const int W = Tlen + FS0 - 1;
     hipStream_t s = (hipStream_t)stream;
-    static bool attr = false;
-    if (!attr) {
-        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_kernel<float>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_kernel<bf16>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
+    int cw = 8;
+    while (cw > 1 && (Q * FS0 * cw * 4 + W > 160 * 1024 || FS0 * cw > 256)) cw /= 2;
+    SRNN_REQUIRE(Q * FS0 * cw * 4 + W <= 160 * 1024 && FS0 * cw <= 256, "dtab: FS0 too large");
+    if (dtype == SRNN_F32) {
+        if (cw == 8) return launch_dtab<float, 8>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
+        if (cw == 4) return launch_dtab<float, 4>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
+        if (cw == 2) return launch_dtab<float, 2>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
+        return launch_dtab<float, 1>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
     }
-    if (dtype == SRNN_F32)
-        hipLaunchKernelGGL((dtab_kernel<float>), grid, dim3(256), lds, s, (const float*)da, ldda, x,
-                           ldx, xoff, Tlen, rows, rpb, dtab, D, FS0, Q);
-    else
-        hipLaunchKernelGGL((dtab_kernel<bf16>), grid, dim3(256), lds, s, (const bf16*)da, ldda, x,
-                           ldx, xoff, Tlen, rows, rpb, dtab, D, FS0, Q);
-    SRNN_LAUNCH_CHECK();
-    return 0;
+    if (cw == 8) return launch_dtab<bf16, 8>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
+    if (cw == 4) return launch_dtab<bf16, 4>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
+    if (cw == 2) return launch_dtab<bf16, 2>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
+    return launch_dtab<bf16, 1>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
 }
