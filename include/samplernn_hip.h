@@ -75,7 +75,9 @@ int srnn_mlp_l1(int dtype, const void* tab, const int64_t* x, int64_t ldx, int x
 /* dtab[x_{t+k}][k][:] += da_t  (Q, FS0, D) fp32 accumulate; backward of the folded     *
  * embedding+conv                                                                        */
 int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x, int64_t ldx,
-                  int xoff, int B, int Tlen, float* dtab, int D, int FS0, int Q, void* stream);
+                  int xoff, int B, int Tlen, void* dtab, int out_dtype, int D, int FS0, int Q,
+                  void* work, size_t work_bytes, void* stream);
+/* (deterministic: 2^-40 fixed-point int64 accumulation; work >= Q*FS0*D*8 bytes)        */
 /* log_softmax (model.py:324-325) + NLL rows (nn.py:66-70) + dlogits (softmax-onehot)*g  */
 /* dz = dlogp - exp(logp) * rowsum(dlogp)   (log_softmax backward, rows of Q)          */
 int srnn_logsoftmax_bwd(const float* dlogp, int64_t lddl, const float* logp, int64_t ldl,

@@ -312,104 +312,3 @@ int srnn_sample_impl(const float* z, int64_t ldz, int B, const float* noise, uin
     return 0;
 }
 
-// ------------------------------------------------------------------ dTab scatter
-// dTab[x_{b, t+k}][k][:] += da[b, t, :] over all rows (backward of the folded
-// embedding . conv).  A workgroup owns a slice of CW columns and a block of nb whole batch
-// rows: it stages the block's sample indices in LDS as bytes (one read per index instead
-// of one global load per (row, tap, column)), keeps dTab[:, :, slice] (Q x FS0 x CW fp32)
-// in LDS, and gives every thread a fixed (tap k, column c): per row it does one global
-// load of da (coalesced over c, L1-shared over k), one LDS byte read and one LDS atomic
-// add; the accumulator is flushed with global atomics once per workgroup.
-template <typename T, int CW>
-__global__ __launch_bounds__(256) void dtab_kernel(const T* __restrict__ da, int64_t ldda,
-                                                   const int64_t* __restrict__ x, int64_t ldx,
-                                                   int xoff, int Tlen, int B, int nb,
-                                                   float* __restrict__ dtab, int D, int FS0,
-                                                   int Q) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float* acc = reinterpret_cast<float*>(smem);                       // [Q][FS0][CW]
-    unsigned char* idx = reinterpret_cast<unsigned char*>(smem + Q * FS0 * CW * 4);
-    const int tid = threadIdx.x;
-    const int c0 = blockIdx.x * CW;
-    const int b0 = blockIdx.y * nb;
-    const int nbb = min(nb, B - b0);
-    const int W = Tlen + FS0 - 1;
-    const int nacc = Q * FS0 * CW;
-    for (int i = tid; i < nacc; i += 256) acc[i] = 0.f;
-    for (int i = tid; i < nbb * W; i += 256) {
-        const int b = i / W, p = i - b * W;
-        idx[i] = (unsigned char)x[(int64_t)(b0 + b) * ldx + xoff + p];
-    }
-    __syncthreads();
-    const int per_row = FS0 * CW;
-    const int rpp = 256 / per_row;                 // rows per pass
-    if (tid < rpp * per_row) {
-        const int rem = tid % per_row;
-        const int k = rem / CW, c = rem % CW;
-        const bool cok = c0 + c < D;
-        int b = 0, t = tid / per_row;
-        const int nrows = nbb * Tlen;
-        const T* dab = da + (int64_t)b0 * Tlen * ldda + c0 + c;
-        float* ak = acc + k * CW + c;
-        for (int r = tid / per_row; r < nrows; r += rpp) {
-            const float g = cok ? to_f(dab[(int64_t)r * ldda]) : 0.f;
-            const int q = idx[b * W + t + k];
-            atomicAdd(ak + q * FS0 * CW, g);
-            t += rpp;
-            while (t >= Tlen) { t -= Tlen; ++b; }
-        }
-    }
-    __syncthreads();
-    for (int i = tid; i < nacc; i += 256) {
-        const float v = acc[i];
-        const int c = i % CW, qk = i / CW;         // qk = q * FS0 + k
-        if (v != 0.f && c0 + c < D) atomicAdd(&dtab[(int64_t)qk * D + c0 + c], v);
-    }
-}
-
-template <typename T, int CW>
-static int launch_dtab(const void* da, int64_t ldda, const int64_t* x, int64_t ldx, int xoff,
-                       int B, int Tlen, float* dtab, int D, int FS0, int Q, hipStream_t s) {
-    const int acc_bytes = Q * FS0 * CW * 4;
-    const int W = Tlen + FS0 - 1;
-    const int nb_cap = std::max(1, (160 * 1024 - acc_bytes) / W);
-    const int nslices = cdiv(D, CW);
-    // enough row blocks to give ~1024 workgroups, as few as LDS allows otherwise
-    int nblk = std::max(1, 1024 / nslices);
-    int nb = std::min(B, std::max(cdiv(B, nblk), 1));
-    nb = std::min(nb, nb_cap);
-    const int lds = acc_bytes + ((nb * W + 15) / 16) * 16;
-    static bool attr = false;
-    if (!attr) {
-        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_kernel<T, CW>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
-    dim3 grid(nslices, cdiv(B, nb));
-    hipLaunchKernelGGL((dtab_kernel<T, CW>), grid, dim3(256), lds, s, (const T*)da, ldda, x, ldx,
-                       xoff, Tlen, B, nb, dtab, D, FS0, Q);
-    SRNN_LAUNCH_CHECK();
-    return 0;
-}
-
-extern "C" int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x,
-                             int64_t ldx, int xoff, int B, int Tlen, float* dtab, int D, int FS0,
-                             int Q, void* stream) {
-    if ((int64_t)B * Tlen <= 0) return 0;
-    SRNN_REQUIRE(Q <= 256, "dtab: q_levels must be <= 256 (byte indices)");
-    const int W = Tlen + FS0 - 1;
-    hipStream_t s = (hipStream_t)stream;
-    int cw = 8;
-    while (cw > 1 && (Q * FS0 * cw * 4 + W > 160 * 1024 || FS0 * cw > 256)) cw /= 2;
-    SRNN_REQUIRE(Q * FS0 * cw * 4 + W <= 160 * 1024 && FS0 * cw <= 256, "dtab: FS0 too large");
-    if (dtype == SRNN_F32) {
-        if (cw == 8) return launch_dtab<float, 8>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
-        if (cw == 4) return launch_dtab<float, 4>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
-        if (cw == 2) return launch_dtab<float, 2>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
-        return launch_dtab<float, 1>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
-    }
-    if (cw == 8) return launch_dtab<bf16, 8>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
-    if (cw == 4) return launch_dtab<bf16, 4>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
-    if (cw == 2) return launch_dtab<bf16, 2>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
-    return launch_dtab<bf16, 1>(da, ldda, x, ldx, xoff, B, Tlen, dtab, D, FS0, Q, s);
-}

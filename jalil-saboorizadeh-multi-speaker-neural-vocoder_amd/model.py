@@ -480,10 +480,10 @@ class _MlpFn(torch.autograd.Function):
         db_hid = H.colsum(da2, M, D)
         da1 = H.gemm(da2, W_hid, mask=a1)                                # (M, D) fp32
         # folded embedding . conv backward: dTab[q][k][:] += da1[t] for x_{t+k} = q
-        dtab = torch.zeros((Q, FS0, D), device=dev, dtype=torch.float32)
+        dtabT = torch.empty((Q, FS0 * D), device=dev, dtype=T)
+        work = torch.empty(Q * FS0 * D, device=dev, dtype=torch.int64)
         H.lib().call('srnn_mlp_dtab', H.F32, H.ptr(da1), D, H.ptr(x), x.shape[1], 0, B, Tl,
-                     H.ptr(dtab), D, FS0, Q, st())
-        dtabT = H.cast(dtab.reshape(Q, FS0 * D), T)
+                     H.ptr(dtabT), H.dcode(T), D, FS0, Q, H.ptr(work), work.numel() * 8, st())
         dE = H.gemm(dtabT, Wp.reshape(FS0 * D, Q))                       # (Q, Q)
         dWp = torch.empty((FS0, D, Q), device=dev, dtype=torch.float32)
         H.gemm(dtabT, ET, transA=True, out=dWp, M=D, N=Q, K=Q, lda=FS0 * D, ldb=Q, ldc=Q,
