@@ -197,7 +197,7 @@ def main():
 
     import distributed as D
     D.init()
-    dev = torch.device('cuda', D.local_rank())
+    dev = torch.device('cuda', D.device_index())
     torch.cuda.set_device(dev)
     N = D.world()
     if N != args.gpus:

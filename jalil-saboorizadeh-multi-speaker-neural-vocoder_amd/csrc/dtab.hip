@@ -20,6 +20,20 @@
 #define DTAB_NT 1024
 #define DTAB_SCALE 1099511627776.0          // 2^40
 
+// round(g * 2^40) as int64 from the float bits (no f64 path): |g| < 2^23 assumed;
+// below 2^-40 the value truncates to 0 (the accumulator's resolution).
+__device__ __forceinline__ long long fx40(float g) {
+    const unsigned u = __float_as_uint(g);
+    const int e = (int)((u >> 23) & 0xFF) - 127 - 23 + 40;   // shift of the 24-bit mantissa
+    const long long m = (long long)((u & 0x7FFFFFu) | 0x800000u);
+    long long v;
+    if (e >= 0) v = m << (e < 62 ? e : 62);
+    else if (e > -25) v = (m + (1ll << (-e - 1))) >> (-e);    // round half up
+    else v = 0;
+    if (((u >> 23) & 0xFF) == 0) v = 0;                      // zero / denormal
+    return (u >> 31) ? -v : v;
+}
+
 template <typename T, int CW>
 __global__ __launch_bounds__(DTAB_NT) void dtab_fx_kernel(
     const T* __restrict__ da, int64_t ldda, const int64_t* __restrict__ x, int64_t ldx, int xoff,
@@ -50,8 +64,11 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_fx_kernel(
         unsigned long long* ak = acc + k * CW + c;
         const unsigned char* ik = idx + k;
         constexpr int U = 8;
-        const float inv_T = 1.0f / (float)Tlen;
-        for (int r0 = tid / per_row; r0 < nrows; r0 += U * rpp) {
+        // the row index is the same for every lane of a (k, c) group; walk it with a
+        // running (b, t) pair instead of a per-element division
+        int r0 = tid / per_row;
+        int b = r0 / Tlen, t = r0 - b * Tlen;
+        for (; r0 < nrows; r0 += U * rpp) {
             float g[U];
             int q[U];
 #pragma unroll
@@ -59,21 +76,18 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_fx_kernel(
                 const int r = r0 + u * rpp;
                 g[u] = (cok && r < nrows) ? to_f(dab[(int64_t)r * ldda]) : 0.f;
             }
+            int bb = b, tt = t;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int r = min(r0 + u * rpp, nrows - 1);
-                int b = (int)((float)r * inv_T);          // fixed up to the exact quotient
-                if (b * Tlen > r) --b;
-                if ((b + 1) * Tlen <= r) ++b;
-                q[u] = ik[r + b * (FS0 - 1)];            // = idx[b * W + t + k]
+                q[u] = (r0 + u * rpp < nrows) ? ik[bb * W + tt] : 0;
+                tt += rpp;
+                while (tt >= Tlen) { tt -= Tlen; ++bb; }
             }
+            b = bb;
+            t = tt;
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (r0 + u * rpp < nrows && g[u] != 0.f) {
-                    const long long v = __double2ll_rn((double)g[u] * DTAB_SCALE);
-                    atomicAdd(ak + q[u] * FS0 * CW, (unsigned long long)v);
-                }
-            }
+            for (int u = 0; u < U; ++u)
+                if (g[u] != 0.f) atomicAdd(ak + q[u] * FS0 * CW, (unsigned long long)fx40(g[u]));
         }
     }
     __syncthreads();

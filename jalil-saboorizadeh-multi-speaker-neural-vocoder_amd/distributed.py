@@ -32,16 +32,26 @@ def local_rank():
     return int(os.environ.get('LOCAL_RANK', '0'))
 
 
+def device_index():
+    """GPU of this rank: LOCAL_RANK (modulo the visible devices, so a multi-rank rehearsal
+    can share one GPU with the gloo backend)."""
+    n = torch.cuda.device_count()
+    return local_rank() % n if n > 0 else 0
+
+
 def init(backend=None):
-    """Initialise the process group from torchrun's env (no-op for a single process)."""
+    """Initialise the process group from torchrun's env (no-op for a single process).
+    Backend: 'nccl' (= RCCL on ROCm) when GPUs are present, else 'gloo';
+    SRNN_DIST_BACKEND overrides (e.g. gloo for a rehearsal on one GPU)."""
     if world() <= 1 or (dist.is_available() and dist.is_initialized()):
         return
     if backend is None:
-        backend = 'nccl' if torch.cuda.is_available() else 'gloo'
+        backend = os.environ.get('SRNN_DIST_BACKEND') or \
+            ('nccl' if torch.cuda.device_count() > 0 else 'gloo')
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
     if backend == 'nccl':
-        torch.cuda.set_device(local_rank())
-        dist.init_process_group(backend, device_id=torch.device('cuda', local_rank()))
+        torch.cuda.set_device(device_index())
+        dist.init_process_group(backend, device_id=torch.device('cuda', device_index()))
     else:
         dist.init_process_group(backend)
 
