@@ -85,9 +85,7 @@ def run_tbptt(args, dev, dist_mod):
 
     def step(n):
         inp, reset, tgt, cnd, spk = batches[n]
-        for p in pred.parameters():
-            if p.grad is not None:
-                p.grad.zero_()
+        opt.zero_grad()     # fused clip+Adam: grads dropped, None == zero
 
         def closure():
             lp = pred(inp, reset, cnd, spk)

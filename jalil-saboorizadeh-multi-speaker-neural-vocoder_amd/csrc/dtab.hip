@@ -6,7 +6,8 @@
 // only 0.3 lane-ops/clk/CU, integer LDS atomics 14.6 (u32) / 9.9 (u64).  So the scatter
 // accumulates in 64-bit FIXED POINT (value * 2^40, rounded) with ds_add_u64: fast, and
 // exact/order-independent, which makes dTab bit-deterministic across runs and workgroup
-// schedules.  Resolution 2^-40 ~ 9e-13 absolute per term, range +-2^23.
+// schedules.  Resolution 2^-40 ~ 9e-13 absolute per term (terms clamped to +-2^11),
+// range of a sum +-2^23.
 //
 // A workgroup (1024 threads) owns CW columns and a block of whole batch rows: it stages
 // the block's sample indices in LDS as bytes, gives each thread a fixed (tap k, column c)
@@ -20,80 +21,79 @@
 #define DTAB_NT 1024
 #define DTAB_SCALE 1099511627776.0          // 2^40
 
-// round(g * 2^40) as int64 from the float bits (no f64 path): |g| < 2^23 assumed;
-// below 2^-40 the value truncates to 0 (the accumulator's resolution).
+// round(g * 2^40) as int64 in four instructions: the f64 fma against 1.5 * 2^52 leaves
+// the rounded (to nearest even) integer in the low mantissa bits, and subtracting the
+// magic's bit pattern recovers it.  Exact for |g| < 2^11 (terms are clamped there; the
+// per-sample gradients reaching the table are many orders of magnitude smaller).
 __device__ __forceinline__ long long fx40(float g) {
-    const unsigned u = __float_as_uint(g);
-    const int e = (int)((u >> 23) & 0xFF) - 127 - 23 + 40;   // shift of the 24-bit mantissa
-    const long long m = (long long)((u & 0x7FFFFFu) | 0x800000u);
-    long long v;
-    if (e >= 0) v = m << (e < 62 ? e : 62);
-    else if (e > -25) v = (m + (1ll << (-e - 1))) >> (-e);    // round half up
-    else v = 0;
-    if (((u >> 23) & 0xFF) == 0) v = 0;                      // zero / denormal
-    return (u >> 31) ? -v : v;
+    g = __builtin_amdgcn_fmed3f(g, -2047.0f, 2047.0f);
+    const double d = __builtin_fma((double)g, DTAB_SCALE, 6755399441055744.0);
+    return __double_as_longlong(d) - 0x4338000000000000ll;
 }
 
-template <typename T, int CW>
+// FSC: compile-time FS0 (0 = runtime).  When FS0 * CW == 64 one wave owns one row per
+// pass, so the row walk (b, t) is wave-uniform and lives in scalar registers.
+template <typename T, int CW, int FSC>
 __global__ __launch_bounds__(DTAB_NT) void dtab_fx_kernel(
     const T* __restrict__ da, int64_t ldda, const int64_t* __restrict__ x, int64_t ldx, int xoff,
     int Tlen, int B, int nb, unsigned long long* __restrict__ fx, int D, int FS0, int Q) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [Q][FS0][CW]
-    unsigned char* idx = reinterpret_cast<unsigned char*>(smem + (size_t)Q * FS0 * CW * 8);
+    const int FS = FSC ? FSC : FS0;
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [Q][FS][CW]
+    unsigned char* idx = reinterpret_cast<unsigned char*>(smem + (size_t)Q * FS * CW * 8);
     const int tid = threadIdx.x;
     const int c0 = blockIdx.x * CW;
     const int b0 = blockIdx.y * nb;
     const int nbb = min(nb, B - b0);
-    const int W = Tlen + FS0 - 1;
-    const int nacc = Q * FS0 * CW;
+    const int W = Tlen + FS - 1;
+    const int nacc = Q * FS * CW;
     for (int i = tid; i < nacc; i += DTAB_NT) acc[i] = 0ull;
     for (int i = tid; i < nbb * W; i += DTAB_NT) {
         const int b = i / W, p = i - b * W;
         idx[i] = (unsigned char)x[(int64_t)(b0 + b) * ldx + xoff + p];
     }
     __syncthreads();
-    const int per_row = FS0 * CW;
+    const int per_row = FS * CW;
     const int rpp = DTAB_NT / per_row;
     if (tid < rpp * per_row) {
         const int rem = tid % per_row;
         const int k = rem / CW, c = rem % CW;
-        const bool cok = c0 + c < D;
         const int nrows = nbb * Tlen;
-        const T* dab = da + (int64_t)b0 * Tlen * ldda + c0 + c;
+        // columns past D read column D - 1 and add into accumulators that are never flushed
+        const T* dab = da + (int64_t)b0 * Tlen * ldda + min(c0 + c, D - 1);
         unsigned long long* ak = acc + k * CW + c;
         const unsigned char* ik = idx + k;
         constexpr int U = 8;
-        // the row index is the same for every lane of a (k, c) group; walk it with a
-        // running (b, t) pair instead of a per-element division
         int r0 = tid / per_row;
+        if constexpr (FSC * CW == 64) r0 = __builtin_amdgcn_readfirstlane(r0);
         int b = r0 / Tlen, t = r0 - b * Tlen;
-        for (; r0 < nrows; r0 += U * rpp) {
+        // full blocks of U rows: no bounds checks, so the U loads and index reads issue
+        // back to back before the first conversion needs them
+        for (; r0 + (U - 1) * rpp < nrows; r0 += U * rpp) {
             float g[U];
             int q[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const int r = r0 + u * rpp;
-                g[u] = (cok && r < nrows) ? to_f(dab[(int64_t)r * ldda]) : 0.f;
+                g[u] = to_f(dab[(int64_t)(r0 + u * rpp) * ldda]);
+                q[u] = ik[b * W + t];
+                t += rpp;
+                while (t >= Tlen) { t -= Tlen; ++b; }
             }
-            int bb = b, tt = t;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                q[u] = (r0 + u * rpp < nrows) ? ik[bb * W + tt] : 0;
-                tt += rpp;
-                while (tt >= Tlen) { tt -= Tlen; ++bb; }
-            }
-            b = bb;
-            t = tt;
 #pragma unroll
             for (int u = 0; u < U; ++u)
-                if (g[u] != 0.f) atomicAdd(ak + q[u] * FS0 * CW, (unsigned long long)fx40(g[u]));
+                atomicAdd(ak + q[u] * (FS * CW), (unsigned long long)fx40(g[u]));
+        }
+        for (; r0 < nrows; r0 += rpp) {
+            atomicAdd(ak + ik[b * W + t] * (FS * CW),
+                      (unsigned long long)fx40(to_f(dab[(int64_t)r0 * ldda])));
+            t += rpp;
+            while (t >= Tlen) { t -= Tlen; ++b; }
         }
     }
     __syncthreads();
     for (int i = tid; i < nacc; i += DTAB_NT) {
         const unsigned long long v = acc[i];
-        const int c = i % CW, qk = i / CW;         // qk = q * FS0 + k
+        const int c = i % CW, qk = i / CW;         // qk = q * FS + k
         if (v != 0ull && c0 + c < D) atomicAdd(&fx[(int64_t)qk * D + c0 + c], v);
     }
 }
@@ -106,7 +106,7 @@ __global__ void dtab_fx_convert_kernel(const unsigned long long* __restrict__ fx
     out[i] = from_f<TO>((float)((double)(long long)fx[i] * (1.0 / DTAB_SCALE)));
 }
 
-template <typename T, int CW>
+template <typename T, int CW, int FSC>
 static int launch_dtab(const void* da, int64_t ldda, const int64_t* x, int64_t ldx, int xoff,
                        int B, int Tlen, unsigned long long* fx, int D, int FS0, int Q,
                        hipStream_t s) {
@@ -120,12 +120,12 @@ static int launch_dtab(const void* da, int64_t ldda, const int64_t* x, int64_t l
     const int lds = acc_bytes + ((nb * W + 15) / 16) * 16;
     static bool attr = false;
     if (!attr) {
-        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_fx_kernel<T, CW>,
+        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_fx_kernel<T, CW, FSC>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
     dim3 grid(nslices, cdiv(B, nb));
-    hipLaunchKernelGGL((dtab_fx_kernel<T, CW>), grid, dim3(DTAB_NT), lds, s, (const T*)da, ldda, x,
+    hipLaunchKernelGGL((dtab_fx_kernel<T, CW, FSC>), grid, dim3(DTAB_NT), lds, s, (const T*)da, ldda, x,
                        ldx, xoff, Tlen, B, nb, fx, D, FS0, Q);
     SRNN_LAUNCH_CHECK();
     return 0;
@@ -149,14 +149,14 @@ extern "C" int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int6
         SRNN_REQUIRE(Q * FS0 * cw * 8 + W <= 160 * 1024 && FS0 * cw <= DTAB_NT,
                      "dtab: FS0 too large");
         int rc;
+#define DTAB_GO(TT, CWV, FSV) launch_dtab<TT, CWV, FSV>(da, ldda, x, ldx, xoff, B, Tlen, fx, D, FS0, Q, s)
         if (dtype == SRNN_F32)
-            rc = cw == 4 ? launch_dtab<float, 4>(da, ldda, x, ldx, xoff, B, Tlen, fx, D, FS0, Q, s)
-               : cw == 2 ? launch_dtab<float, 2>(da, ldda, x, ldx, xoff, B, Tlen, fx, D, FS0, Q, s)
-                         : launch_dtab<float, 1>(da, ldda, x, ldx, xoff, B, Tlen, fx, D, FS0, Q, s);
+            rc = (cw == 4 && FS0 == 16) ? DTAB_GO(float, 4, 16)
+               : cw == 4 ? DTAB_GO(float, 4, 0) : cw == 2 ? DTAB_GO(float, 2, 0) : DTAB_GO(float, 1, 0);
         else
-            rc = cw == 4 ? launch_dtab<bf16, 4>(da, ldda, x, ldx, xoff, B, Tlen, fx, D, FS0, Q, s)
-               : cw == 2 ? launch_dtab<bf16, 2>(da, ldda, x, ldx, xoff, B, Tlen, fx, D, FS0, Q, s)
-                         : launch_dtab<bf16, 1>(da, ldda, x, ldx, xoff, B, Tlen, fx, D, FS0, Q, s);
+            rc = (cw == 4 && FS0 == 16) ? DTAB_GO(bf16, 4, 16)
+               : cw == 4 ? DTAB_GO(bf16, 4, 0) : cw == 2 ? DTAB_GO(bf16, 2, 0) : DTAB_GO(bf16, 1, 0);
+#undef DTAB_GO
         if (rc) return rc;
     }
     if (out_dtype == SRNN_F32)

@@ -170,12 +170,26 @@ int srnn_gemm2_try(int dtype, int out_dtype, int transA, int transB, int M, int 
                    const float* bias, int bias_mode, int relu, const void* mask, int64_t ldmask,
                    hipStream_t s);
 
+int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
+                   float alpha, const void* A, int64_t lda, const void* B, int64_t ldb,
+                   float beta, const float* Cin, int64_t ldcin, void* C, int64_t ldc,
+                   const float* bias, int bias_mode, int relu, const void* mask, int64_t ldmask,
+                   int force, hipStream_t s);
+
+static bool env_on(const char* name) {
+    const char* e = getenv(name);
+    return !(e && e[0] == '0');
+}
+
 static bool g_use_gemm2() {
     static int v = -1;
-    if (v < 0) {
-        const char* e = getenv("SRNN_GEMM2");
-        v = (e && e[0] == '0') ? 0 : 1;
-    }
+    if (v < 0) v = env_on("SRNN_GEMM2") ? 1 : 0;
+    return v == 1;
+}
+
+static bool g_use_gemm3() {
+    static int v = -1;
+    if (v < 0) v = env_on("SRNN_GEMM3") ? 1 : 0;
     return v == 1;
 }
 
@@ -225,6 +239,14 @@ int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int 
                                          : launch_skinny<bf16, bf16>(g, s);
         }
         SRNN_REQUIRE(tile != 4, "gemm: shape not eligible for the skinny path");
+    }
+    // large aligned bf16 problems: the 256x256 8-wave kernel (gemm3.hip); tile 5 forces it
+    if ((tile < 0 || tile == 5) && batch == 1 && (tile == 5 || g_use_gemm3())) {
+        int rc = srnn_gemm3_try(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, B, ldb,
+                                beta, Cin, ldcin, C, ldc, bias, bias_mode, relu, mask, ldmask,
+                                tile == 5, s);
+        if (rc >= 0) return rc;
+        SRNN_REQUIRE(tile != 5, "gemm: shape not eligible for the gemm3 path");
     }
     // large aligned problems: the glds-ring kernel (gemm2.hip); tile 3 forces it
     if ((tile < 0 || tile == 3) && batch == 1 && g_use_gemm2()) {

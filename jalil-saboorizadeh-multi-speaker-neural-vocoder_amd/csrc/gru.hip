@@ -13,6 +13,10 @@
 #include "ring_core.hpp"
 #include "samplernn_hip_internal.hpp"
 
+// ring depth of the per-step GRU kernels: 8 slots (7 k-stages in flight) fit the 160 KiB
+// LDS and put nearly the whole W_hh slice + h rows of a step in flight at once
+#define GRU_NS 8
+
 struct GruCellArgs {
     const void* x;      // layer input (T), row stride ldx; null -> use gi
     int64_t ldx;
@@ -117,12 +121,12 @@ __global__ __launch_bounds__(256) void gru_cell_ring_kernel(GruCellArgs a) {
     for (int j = 0; j < 3; ++j) acc_h[0][j] = acc_i[0][j] = floatx4{0.f, 0.f, 0.f, 0.f};
     const RowGateClamp gmap{u0, 16, a.D};
     if (a.x)
-        ring_core<T, 32, 48, 2, 1, 2, 4>((const T*)a.x, a.ldx, RowClamp{m0, a.B}, (const T*)a.wih,
+        ring_core<T, 32, 48, 2, 1, 2, GRU_NS>((const T*)a.x, a.ldx, RowClamp{m0, a.B}, (const T*)a.wih,
                                          a.Din, gmap, a.Din, smem, acc_i);
-    ring_core<T, 32, 48, 2, 1, 2, 4>((const T*)a.h, a.ldh, RowClamp{m0, a.B}, (const T*)a.whh, a.D,
+    ring_core<T, 32, 48, 2, 1, 2, GRU_NS>((const T*)a.h, a.ldh, RowClamp{m0, a.B}, (const T*)a.whh, a.D,
                                      gmap, a.D, smem, acc_h);
-    if (a.x) ring_reduce<T, 32, 48, 2, 1, 2, 4>(smem, acc_i);
-    ring_reduce<T, 32, 48, 2, 1, 2, 4>(smem, acc_h);
+    if (a.x) ring_reduce<T, 32, 48, 2, 1, 2, GRU_NS>(smem, acc_i);
+    ring_reduce<T, 32, 48, 2, 1, 2, GRU_NS>(smem, acc_h);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = wave % 2, wk = wave / 2;
     if (wk != 0) return;
@@ -162,7 +166,7 @@ __global__ __launch_bounds__(256) void gru_cell_ring_kernel(GruCellArgs a) {
 
 template <typename T, int BM>
 static int launch_cell(GruCellArgs& a, hipStream_t s) {
-    typedef Ring<T, 32, 48, 2, 1, 2, 4> R;
+    typedef Ring<T, 32, 48, 2, 1, 2, GRU_NS> R;
     const int es = (int)sizeof(T);
     const bool ring = a.D % R::KB == 0 && (!a.x || a.Din % R::KB == 0) && a.vec_h && a.vec_whh &&
                       (!a.x || (a.vec_x && a.vec_wih));
@@ -295,10 +299,10 @@ __global__ __launch_bounds__(256) void gru_bwd_ring_kernel(GruBwdArgs a) {
     floatx4 acc[1][1];
     acc[0][0] = floatx4{0.f, 0.f, 0.f, 0.f};
     if (a.dgh_next) {
-        ring_core<T, 32, 16, 2, 1, 2, 4>((const T*)a.dgh_next, a.lddgn, RowClamp{m0, a.B},
+        ring_core<T, 32, 16, 2, 1, 2, GRU_NS>((const T*)a.dgh_next, a.lddgn, RowClamp{m0, a.B},
                                          (const T*)a.whh_t, 3 * D, RowClamp{u0, D}, 3 * D, smem,
                                          acc);
-        ring_reduce<T, 32, 16, 2, 1, 2, 4>(smem, acc);
+        ring_reduce<T, 32, 16, 2, 1, 2, GRU_NS>(smem, acc);
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = wave % 2, wk = wave / 2;
@@ -314,7 +318,7 @@ __global__ __launch_bounds__(256) void gru_bwd_ring_kernel(GruBwdArgs a) {
 
 template <typename T, int BM>
 static int launch_bwd(GruBwdArgs& a, hipStream_t s) {
-    typedef Ring<T, 32, 16, 2, 1, 2, 4> R;
+    typedef Ring<T, 32, 16, 2, 1, 2, GRU_NS> R;
     if (a.whh_t && (3 * a.D) % R::KB == 0 && a.vec_wt && (!a.dgh_next || a.vec_dgn)) {
         static bool attr = false;
         if (!attr) {

@@ -19,6 +19,17 @@ __device__ __forceinline__ void rc_wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
+// wait until at most min(ahead, I) stages of PER loads each remain in flight
+template <int PER, int I>
+__device__ __forceinline__ void rc_wait_sel(int ahead) {
+    if constexpr (I == 0) {
+        rc_wait_vm<0>();
+    } else {
+        if (ahead >= I) rc_wait_vm<I * PER>();
+        else rc_wait_sel<PER, I - 1>(ahead);
+    }
+}
+
 struct RowClamp {
     int base, limit;
     __device__ __forceinline__ int operator()(int i) const {
@@ -91,10 +102,7 @@ __device__ __forceinline__ void ring_core(
         if (s < nk) issue(s);
     const int lr = lane & 15, lh = lane >> 4;
     for (int kt = 0; kt < nk; ++kt) {
-        const int ahead = nk - 1 - kt;
-        if (ahead >= NS - 2) rc_wait_vm<(NS - 2) * (R::IA + R::IB)>();
-        else if (NS > 3 && ahead == 1) rc_wait_vm<(R::IA + R::IB)>();
-        else rc_wait_vm<0>();
+        rc_wait_sel<R::IA + R::IB, NS - 2>(nk - 1 - kt);
         __builtin_amdgcn_s_barrier();
         if (kt + NS - 1 < nk) issue(kt + NS - 1);
         const char* ia = smem + (kt % NS) * R::SLOT;

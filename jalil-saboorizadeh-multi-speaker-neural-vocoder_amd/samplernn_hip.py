@@ -6,6 +6,8 @@ fails to load, `lib()` raises -- loudly -- and so does every op that needs it.
 PyTorch is used for device memory, streams and autograd bookkeeping only.
 """
 import ctypes
+import sys
+import time
 import os
 
 import torch
@@ -136,6 +138,9 @@ def need_cuda(*ts):
                                'no CPU fallback' % t.device)
 
 
+_GEMM_LOG = os.environ.get('SRNN_GEMM_LOG', '0') == '1'
+
+
 def gemm(a, b, transA=False, transB=False, out=None, out_dtype=torch.float32, bias=None,
          bias_mode=1, relu=False, alpha=1.0, beta=0.0, cin=None, mask=None, M=None, N=None, K=None,
          lda=None, ldb=None, ldc=None, ldcin=None, batch=1, sA=0, sB=0, sC=0, sCin=0, tile=-1):
@@ -157,10 +162,21 @@ def gemm(a, b, transA=False, transB=False, out=None, out_dtype=torch.float32, bi
         ldcin = cin.stride(0)
     if a.dtype != b.dtype:
         raise TypeError('gemm operands must share a dtype (%s vs %s)' % (a.dtype, b.dtype))
+    if _GEMM_LOG:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
     lib().call('srnn_gemm', dcode(a), dcode(out), int(transA), int(transB), M, N, K, alpha,
                ptr(a), lda, sA, ptr(b), ldb, sB, beta, ptr(cin), ldcin or 0, sCin, ptr(out), ldc,
                sC, ptr(bias), bias_mode, int(relu), batch, tile, ptr(mask),
                (mask.stride(0) if mask is not None else 0), stream())
+    if _GEMM_LOG:
+        torch.cuda.synchronize()
+        us = (time.perf_counter() - t0) * 1e6
+        sys.stderr.write('gemm M=%d N=%d K=%d batch=%d tA=%d tB=%d %s->%s mask=%d bias=%d relu=%d '
+                         'cin=%d %.1f us %.1f TF/s\n' % (
+                             M, N, K, batch, transA, transB, a.dtype, out.dtype, mask is not None,
+                             bias is not None, relu, cin is not None, us,
+                             2.0 * M * N * K * batch / us / 1e6))
     return out
 
 

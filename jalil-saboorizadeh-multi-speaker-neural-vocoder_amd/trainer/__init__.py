@@ -65,6 +65,9 @@ class Trainer(object):
             self.call_plugins('epoch', self.epochs)
 
     def _zero_grad(self):
+        if hasattr(self.optimizer, 'grad_sync'):    # optim.gradient_clipping wrapper
+            self.optimizer.zero_grad()
+            return
         try:
             self.optimizer.zero_grad(set_to_none=False)
         except TypeError:

@@ -63,6 +63,35 @@ def test_gemm2_ring_kernel(hip, dtype, transA, transB, M, N, K, epi):
     torch.testing.assert_close(out.cpu(), ref, atol=tol, rtol=1e-4)
 
 
+@pytest.mark.parametrize('out_dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('transA,transB', [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize('M,N,K,epi', [(512, 768, 320, 'full'), (256, 512, 96, 'rowbias'),
+                                       (256, 256, 8192, 'plain'), (768, 256, 1024, 'plain')])
+def test_gemm3_256_kernel(hip, out_dtype, transA, transB, M, N, K, epi):
+    """The 256x256 8-wave bf16 kernel (tile 5 forces it): all layouts, vectorised epilogue
+    (Cin, column/row bias, ReLU, mask) and the split-K atomic path."""
+    dtype = torch.bfloat16
+    A = _rand(K, M, seed=1) if transA else _rand(M, K, seed=1)
+    B = _rand(N, K, seed=2) if transB else _rand(K, N, seed=2)
+    Ad, Bd = A.to(DEV, dtype), B.to(DEV, dtype)
+    Af, Bf = Ad.float().cpu(), Bd.float().cpu()
+    ref = (Af.t() if transA else Af) @ (Bf.t() if transB else Bf)
+    kw = dict(transA=bool(transA), transB=bool(transB), tile=5, out_dtype=out_dtype)
+    if epi == 'full':
+        bias, cin, mask = _rand(N, seed=3), _rand(M, N, seed=4), _rand(M, N, seed=5)
+        out = hip.gemm(Ad, Bd, bias=bias.to(DEV), cin=cin.to(DEV), beta=0.5, relu=True,
+                       mask=mask.to(DEV, dtype), alpha=1.5, **kw)
+        ref = (1.5 * ref + 0.5 * cin + bias).clamp_min(0) * (mask.to(dtype).float() > 0)
+    elif epi == 'rowbias':
+        bias = _rand(M, seed=3)
+        out = hip.gemm(Ad, Bd, bias=bias.to(DEV), bias_mode=2, **kw)
+        ref = ref + bias[:, None]
+    else:
+        out = hip.gemm(Ad, Bd, **kw)
+    tol = 2e-3 * np.sqrt(K) if out_dtype == torch.float32 else 1e-2 * np.sqrt(K)
+    torch.testing.assert_close(out.float().cpu(), ref, atol=tol, rtol=1e-2)
+
+
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('M,N,K', [(128, 1024, 1024), (67, 256, 512), (128, 40, 256),
                                    (256, 2048, 256)])
@@ -213,6 +242,33 @@ def test_logsoftmax_and_sampler(hip):
     hip.lib().call('srnn_logsoftmax_nll', hip.ptr(z), Q, None, 0, 1, R, Q, None, hip.ptr(logp), Q,
                    None, hip.F32, 0, 0.0, hip.stream())
     torch.testing.assert_close(logp.cpu(), torch.log_softmax(z.cpu(), 1), atol=2e-6, rtol=0)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('B,Tl,D,FS0,Q', [(3, 37, 72, 16, 256), (5, 64, 1024, 16, 256),
+                                          (2, 50, 40, 20, 256), (4, 30, 33, 4, 64), (0, 8, 16, 16, 256)])
+def test_mlp_dtab_scatter(hip, dtype, B, Tl, D, FS0, Q):
+    """dTab[q][k][:] = sum over (b, t) with x[b, t + k] == q of da[b, t, :] -- the
+    embedding . conv backward (model.py:274-285).  Fixed-point accumulation: within 2^-40
+    per term of the fp64 sum, and bit-identical from run to run."""
+    g = torch.Generator().manual_seed(B * 1000 + D)
+    x = torch.randint(0, Q, (max(B, 1), Tl + FS0 - 1 + 3), generator=g)[:B]
+    x[:, 5:12] = 7                                  # runs of equal indices (silence)
+    da = (_rand(max(B, 1) * Tl, D, scale=1e-3, seed=D)[:B * Tl]).to(dtype)
+    ref = torch.zeros(Q, FS0, D, dtype=torch.float64)
+    for k in range(FS0):
+        ref[:, k].index_add_(0, x[:, k:k + Tl].reshape(-1), da.double())
+    work = torch.empty(Q * FS0 * D, device=DEV, dtype=torch.int64)
+    outs = []
+    for _ in range(2):
+        out = torch.empty(Q, FS0, D, device=DEV, dtype=torch.float32)
+        xd, dad = x.to(DEV).contiguous(), da.to(DEV).contiguous()
+        hip.lib().call('srnn_mlp_dtab', hip.dcode(dtype), hip.ptr(dad), D, hip.ptr(xd), x.shape[1],
+                       0, B, Tl, hip.ptr(out), hip.F32, D, FS0, Q, hip.ptr(work), work.numel() * 8,
+                       hip.stream())
+        outs.append(out.cpu())
+    assert torch.equal(outs[0], outs[1])
+    torch.testing.assert_close(outs[0].double(), ref, atol=1e-9 + 1e-12 * B * Tl, rtol=1e-6)
 
 
 def test_adam_clip_matches_torch(hip):

@@ -44,8 +44,10 @@ if __name__ == '__main__':
         (16384, 1024, 8192, True, False, bf, f32, 'upsample wgrad TN'),
         (8192, 3072, 1024, False, True, bf, f32, 'gru gi fwd NT'),
         (3072, 1024, 8192, True, False, bf, f32, 'gru wgrad TN'),
-        (128, 1024, 1024, False, True, f32, f32, 'gen L2 fp32 NT (skinny)'),
+        (131072, 1024, 256, False, False, bf, bf, 'mlp dgrad out NN K256'),
+        (256, 1024, 131072, True, False, bf, f32, 'mlp out wgrad TN'),
     ]
+    tiles = [int(t) for t in os.environ.get('TILES', '5,3').split(',')]
     for (M, N, K, tA, tB, dt, odt, tag) in shapes:
-        for tile in (-1, 0):
+        for tile in tiles:
             run(M, N, K, tA, tB, dt, odt, tile, tag)
