@@ -63,23 +63,18 @@ __device__ __forceinline__ void g3_wait_sel(int ahead) {
     }
 }
 
+// per-lane source of DMA piece c (1 KiB of the stage image) at k = k0
 template <bool KC>
-__device__ __forceinline__ void g3_issue(const bf16* __restrict__ base, int64_t ld, int r0, int k0,
-                                         char* img, int wave, int lane) {
-#pragma unroll
-    for (int i = 0; i < g3::GLW; ++i) {
-        const int c = wave * g3::GLW + i;              // 1-KiB chunk of the image
-        const bf16* src;
-        if constexpr (KC) {
-            const int row = c * 16 + (lane >> 2);
-            const int slot = (lane & 3) ^ ((row >> 2) & 3);
-            src = base + (int64_t)(r0 + row) * ld + k0 + slot * 8;
-        } else {
-            const int kr = c * 2 + (lane >> 5);
-            const int slot = (lane & 31) ^ (2 * (kr & 3) + 8 * ((kr >> 3) & 1));
-            src = base + (int64_t)(k0 + kr) * ld + r0 + slot * 8;
-        }
-        __builtin_amdgcn_global_load_lds(G3_GLB(src), G3_LDS(img + c * 1024), 16, 0, 0);
+__device__ __forceinline__ const bf16* g3_src(const bf16* __restrict__ base, int64_t ld, int r0,
+                                              int k0, int c, int lane) {
+    if constexpr (KC) {
+        const int row = c * 16 + (lane >> 2);
+        const int slot = (lane & 3) ^ ((row >> 2) & 3);
+        return base + (int64_t)(r0 + row) * ld + k0 + slot * 8;
+    } else {
+        const int kr = c * 2 + (lane >> 5);
+        const int slot = (lane & 31) ^ (2 * (kr & 3) + 8 * ((kr >> 3) & 1));
+        return base + (int64_t)(k0 + kr) * ld + r0 + slot * 8;
     }
 }
 
@@ -141,62 +136,12 @@ __device__ __forceinline__ void g3_store4(bf16* p, const float (&v)[4]) {
 // SW: operands swapped in the MFMA (vector epilogue); !SW: the plain split-K partial
 // path, where a lane's 4 values are 4 rows of one column and each atomic instruction
 // covers 16 consecutive columns (64 B) of 4 rows instead of 16 rows x 4 B.
-template <typename TO, bool KCA, bool KCB, bool SW>
-__global__ __launch_bounds__(512, 1) void gemm3_kernel(Gemm3Args g) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int wm = wave & 1, wn = wave >> 1;
-    const int ntm = g.M / g3::BM, ntn = g.N / g3::BN;
-    const int t = g3_xcd_remap(blockIdx.x, ntm * ntn);
-    const int tm = t / ntn, tn = t % ntn;
-    const int m0 = tm * g3::BM, n0 = tn * g3::BN;
-    const int kslice = g.K / g.ksplit;
-    const int kbeg = blockIdx.z * kslice;
-    const int nk = kslice / g3::BK;
-    const bf16* A = reinterpret_cast<const bf16*>(g.A);
-    const bf16* B = reinterpret_cast<const bf16*>(g.B);
-
-    floatx4 acc[8][4];
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-    auto issue = [&](int kt, int slot) {
-        char* img = smem + slot * g3::SLOT;
-        const int k0 = kbeg + kt * g3::BK;
-        g3_issue<KCA>(A, g.lda, m0, k0, img, wave, lane);
-        g3_issue<KCB>(B, g.ldb, n0, k0, img + g3::OPB, wave, lane);
-    };
-#pragma unroll
-    for (int s = 0; s < g3::NS - 1; ++s)
-        if (s < nk) issue(s, s);
-
-    int rs = 0, ws = g3::NS - 1;
-    for (int kt = 0; kt < nk; ++kt) {
-        g3_wait_sel<2 * g3::GLW, g3::NS - 2>(nk - 1 - kt);
-        __builtin_amdgcn_s_barrier();
-        if (kt + g3::NS - 1 < nk) issue(kt + g3::NS - 1, ws);
-        ws = ws == g3::NS - 1 ? 0 : ws + 1;
-        const char* ia = smem + rs * g3::SLOT;
-        const char* ib = ia + g3::OPB;
-        rs = rs == g3::NS - 1 ? 0 : rs + 1;
-        bf16x8 a[8], b[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) b[j] = g3_frag<KCB>(ib, wn * 64 + j * 16, lane);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = g3_frag<KCA>(ia, wm * 128 + i * 16, lane);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0)
-                               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-    }
-
+// epilogue of one finished tile (registers -> C); zeroes the accumulators
+template <typename TO, bool SW>
+__device__ __forceinline__ void g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
+                                            int n0, int wm, int wn, int lane) {
     if constexpr (!SW) {
+        // plain fp32 partials: lane holds 4 rows x 1 column per fragment
         float* Cf = reinterpret_cast<float*>(g.C);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -210,64 +155,472 @@ __global__ __launch_bounds__(512, 1) void gemm3_kernel(Gemm3Args g) {
                     if (g.ksplit > 1) atomicAdd(dst, g.alpha * acc[i][j][e]);
                     else *dst = g.alpha * acc[i][j][e];
                 }
+                acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
             }
         return;
     }
-
-    // epilogue: lane holds C[row][col .. col+3] of each fragment
+    // lane holds C[row][col .. col+3] of each fragment.  Every operand the epilogue needs
+    // (bias, ReLU mask) is loaded up front with ONE wait: a load waited for between the
+    // stores would also wait for every older store and in-flight DMA piece (vmcnt is in
+    // order), serialising 32 round trips per tile.  Exactly 32 stores per wave follow.
     TO* Cp = reinterpret_cast<TO*>(g.C);
     const bf16* mask = reinterpret_cast<const bf16*>(g.mask);
+    const int rbase = m0 + wm * 128 + (lane & 15);
+    const int cbase = n0 + wn * 64 + (lane >> 4) * 4;
+    floatx4 bcol[4];
+    float brow[8];
+    if (g.bias_mode == 1) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const int row = m0 + wm * 128 + i * 16 + (lane & 15);
+        for (int j = 0; j < 4; ++j) bcol[j] = *reinterpret_cast<const floatx4*>(g.bias + cbase + j * 16);
+    } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int col = n0 + wn * 64 + j * 16 + (lane >> 4) * 4;
-            float v[4];
+        for (int j = 0; j < 4; ++j) bcol[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (g.bias_mode == 2) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = g.alpha * acc[i][j][e];
-            if (g.beta != 0.f) {
-                float c[4];
-                g3_load4(g.Cin + (int64_t)row * g.ldcin + col, c);
+        for (int i = 0; i < 8; ++i) brow[i] = g.bias[rbase + i * 16];
+    } else {
 #pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += g.beta * c[e];
+        for (int i = 0; i < 8; ++i) brow[i] = 0.f;
+    }
+    // the mask in two halves of 16 fragments (register budget): two waits per tile
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        u16x4 mk[4][4];
+        if (mask) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    mk[i][j] = *reinterpret_cast<const u16x4*>(
+                        mask + (int64_t)(rbase + (4 * h + i) * 16) * g.ldmask + cbase + j * 16);
+        }
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+            const int i = 4 * h + ii;
+            const int row = rbase + i * 16;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int col = cbase + j * 16;
+                float v[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = g.alpha * acc[i][j][e];
+                acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+                if (g.beta != 0.f) {     // (no model GEMM on this path uses Cin)
+                    float c[4];
+                    g3_load4(g.Cin + (int64_t)row * g.ldcin + col, c);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] += g.beta * c[e];
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] += bcol[j][e] + brow[i];
+                if (g.relu) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                }
+                if (mask) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        v[e] = __uint_as_float((unsigned)mk[ii][j][e] << 16) > 0.f ? v[e] : 0.f;
+                }
+                g3_store4(Cp + (int64_t)row * g.ldc + col, v);
             }
-            if (g.bias_mode == 1) {
-                float bb[4];
-                g3_load4(g.bias + col, bb);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += bb[e];
-            } else if (g.bias_mode == 2) {
-                const float bb = g.bias[row];
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] += bb;
-            }
-            if (g.relu) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-            }
-            if (mask) {
-                float mk[4];
-                g3_load4(mask + (int64_t)row * g.ldmask + col, mk);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) v[e] = mk[e] > 0.f ? v[e] : 0.f;
-            }
-            g3_store4(Cp + (int64_t)row * g.ldc + col, v);
         }
     }
 }
 
+// Persistent: workgroup w owns work units w, w + G, ... (unit = output tile x k-slice);
+// the k-stages of all its units form ONE stream through the ring, so the DMA of the next
+// tile's first stages runs under the current tile's last MFMAs and epilogue.
+template <typename TO, bool KCA, bool KCB, bool SW>
+__global__ __launch_bounds__(512, 1) void gemm3_kernel(Gemm3Args g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int ntm = g.M / g3::BM, ntn = g.N / g3::BN;
+    const int ntiles = ntm * ntn;
+    const int nunits = ntiles * g.ksplit;
+    const int G = gridDim.x;
+    const int nmine = (nunits - (int)blockIdx.x + G - 1) / G;
+    const int kslice = g.K / g.ksplit;
+    const int nk = kslice / g3::BK;
+    const int S = nmine * nk;                  // stages of this workgroup
+    const bf16* A = reinterpret_cast<const bf16*>(g.A);
+    const bf16* B = reinterpret_cast<const bf16*>(g.B);
+
+    // unit i of this workgroup -> (m0, n0, kbeg); units on one XCD walk adjacent tiles
+    auto unit = [&](int i, int& m0, int& n0, int& kbeg) {
+        const int v = (int)blockIdx.x + i * G;
+        const int z = v / ntiles;
+        const int t = g3_xcd_remap(v - z * ntiles, ntiles);
+        m0 = (t / ntn) * g3::BM;
+        n0 = (t % ntn) * g3::BN;
+        kbeg = z * kslice;
+    };
+
+    floatx4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // issue cursor: unit iu, stage kti; per-lane sources of this wave's 4 DMA pieces
+    int iu = 0, kti = 0;
+    const bf16* srcA[g3::GLW];
+    const bf16* srcB[g3::GLW];
+    auto set_src = [&]() {
+        int m0, n0, kb;
+        unit(iu, m0, n0, kb);
+#pragma unroll
+        for (int i = 0; i < g3::GLW; ++i) {
+            const int c = wave * g3::GLW + i;
+            srcA[i] = g3_src<KCA>(A, g.lda, m0, kb, c, lane);
+            srcB[i] = g3_src<KCB>(B, g.ldb, n0, kb, c, lane);
+        }
+    };
+    set_src();
+    auto glds = [&](const bf16* src, int64_t koff, char* img, int i) {
+        __builtin_amdgcn_global_load_lds(G3_GLB(src + koff), G3_LDS(img + (wave * g3::GLW + i) * 1024),
+                                         16, 0, 0);
+    };
+    auto koffA = [&](int kt) { return KCA ? (int64_t)kt * g3::BK : (int64_t)kt * g3::BK * g.lda; };
+    auto koffB = [&](int kt) { return KCB ? (int64_t)kt * g3::BK : (int64_t)kt * g3::BK * g.ldb; };
+    auto advance_issue = [&]() {
+        if (++kti == nk) {
+            kti = 0;
+            ++iu;
+            if (iu < nmine) set_src();
+        }
+    };
+    int ws = 0;
+    auto next_ws = [&]() { ws = ws == g3::NS - 1 ? 0 : ws + 1; };
+#pragma unroll
+    for (int s = 0; s < g3::NS - 1; ++s)
+        if (s < S) {
+            char* img = smem + ws * g3::SLOT;
+            const int64_t oa = koffA(kti), ob = koffB(kti);
+#pragma unroll
+            for (int i = 0; i < g3::GLW; ++i) glds(srcA[i], oa, img, i);
+#pragma unroll
+            for (int i = 0; i < g3::GLW; ++i) glds(srcB[i], ob, img + g3::OPB, i);
+            next_ws();
+            advance_issue();
+        }
+
+    constexpr int PER = 2 * g3::GLW;
+    int rs = 0;
+    bf16x8 a[8], b[4];
+    auto read_stage = [&]() {
+        const char* ia = smem + rs * g3::SLOT;
+        const char* ib = ia + g3::OPB;
+        rs = rs == g3::NS - 1 ? 0 : rs + 1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = g3_frag<KCB>(ib, wn * 64 + j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = g3_frag<KCA>(ia, wm * 128 + i * 16, lane);
+    };
+    auto mfma_row = [&](int i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0)
+                           : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    };
+    // compute cursor: unit ic, stage ktc
+    int ic = 0, ktc = 0;
+    bool epi = false;
+    auto finish_stage = [&]() {
+        if (++ktc == nk) {
+            int m0, n0, kb;
+            unit(ic, m0, n0, kb);
+            g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+            ktc = 0;
+            ++ic;
+            epi = true;
+        }
+    };
+    // Steady state: every stage issues the DMA pieces of stage s+NS-1 into the slot freed
+    // by stage s-1, one piece after each of the first four 4-MFMA groups, so the issue
+    // cost of the LDS-DMA hides behind the matrix pipe instead of stalling all waves
+    // right after the barrier.
+    int s = 0;
+    for (; s + g3::NS - 1 < S; ++s) {
+        // the 32 epilogue stores of a just-finished tile are younger than the pieces
+        // waited for here: leave them in flight
+        if (SW && epi) g3_wait_vm<(g3::NS - 2) * PER + 32>();
+        else g3_wait_vm<(g3::NS - 2) * PER>();
+        epi = false;
+        __builtin_amdgcn_s_barrier();
+        char* img = smem + ws * g3::SLOT;
+        next_ws();
+        const int64_t oa = koffA(kti), ob = koffB(kti);
+        const bf16* a0 = srcA[0];
+        const bf16* a1 = srcA[1];
+        const bf16* b0 = srcB[0];
+        const bf16* b1 = srcB[1];
+        advance_issue();
+        read_stage();
+        __builtin_amdgcn_s_setprio(1);
+        mfma_row(0);
+        glds(a0, oa, img, 0);
+        mfma_row(1);
+        glds(a1, oa, img, 1);
+        mfma_row(2);
+        glds(b0, ob, img + g3::OPB, 0);
+        mfma_row(3);
+        glds(b1, ob, img + g3::OPB, 1);
+#pragma unroll
+        for (int i = 4; i < 8; ++i) mfma_row(i);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+        finish_stage();
+    }
+    // tail: nothing left to issue, the in-flight stages drain
+    for (; s < S; ++s) {
+        g3_wait_sel<PER, g3::NS - 2>(S - 1 - s);
+        __builtin_amdgcn_s_barrier();
+        read_stage();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mfma_row(i);
+        __builtin_amdgcn_s_setprio(0);
+        finish_stage();
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Pair mode: 64-deep stages, 2 slots x 64 KiB.  A k-contiguous operand keeps 128-B rows
+// (a whole cache line per row per stage: every DMA piece is 8 rows x 128 B, half the L1
+// tag lookups / L2 requests of 64-B half lines), two slots of 64 KiB
+// with one stage of look-ahead (stage s+1 streams in while stage s computes), the
+// structure of the 256 x 256 templates in the CDNA4 guide.
+namespace g3p {
+constexpr int BK = 64;
+constexpr int OPB = 256 * BK * 2;       // 32 KiB per operand image
+constexpr int SLOT = 2 * OPB;
+constexpr int LDS = 2 * SLOT;           // 128 KiB
+constexpr int GLW = 4;                  // glds per wave per operand per stage
+}  // namespace g3p
+
+// per-lane source of DMA piece c at k = k0
+template <bool KC>
+__device__ __forceinline__ const bf16* g3p_src(const bf16* __restrict__ base, int64_t ld, int r0,
+                                               int k0, int c, int lane) {
+    if constexpr (KC) {
+        const int row = c * 8 + (lane >> 3);
+        const int slot = (lane & 7) ^ ((row >> 1) & 7);
+        return base + (int64_t)(r0 + row) * ld + k0 + slot * 8;
+    } else {
+        const int kr = c * 2 + (lane >> 5);
+        const int slot = (lane & 31) ^ (2 * (kr & 3) + 8 * ((kr >> 3) & 1));
+        return base + (int64_t)(k0 + kr) * ld + r0 + slot * 8;
+    }
+}
+
+// fragment rows f0..f0+15, k-unit u (0..1: 32 k each) of the stage
+template <bool KC>
+__device__ __forceinline__ bf16x8 g3p_frag(const char* img, int f0, int u, int lane) {
+    if constexpr (KC) {
+        const int r = f0 + (lane & 15);
+        const int slot = (u * 4 + (lane >> 4)) ^ ((r >> 1) & 7);
+        return *reinterpret_cast<const bf16x8*>(img + r * 128 + slot * 16);
+    } else {
+        return g3_frag<false>(img + u * 32 * 512, f0, lane);
+    }
+}
+
+template <typename TO, bool KCA, bool KCB, bool SW>
+__global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int ntm = g.M / g3::BM, ntn = g.N / g3::BN;
+    const int ntiles = ntm * ntn;
+    const int nunits = ntiles * g.ksplit;
+    const int G = gridDim.x;
+    const int nmine = (nunits - (int)blockIdx.x + G - 1) / G;
+    const int kslice = g.K / g.ksplit;
+    const int nk = kslice / g3p::BK;
+    const int S = nmine * nk;
+    const bf16* A = reinterpret_cast<const bf16*>(g.A);
+    const bf16* B = reinterpret_cast<const bf16*>(g.B);
+
+    auto unit = [&](int i, int& m0, int& n0, int& kbeg) {
+        const int v = (int)blockIdx.x + i * G;
+        const int z = v / ntiles;
+        const int t = g3_xcd_remap(v - z * ntiles, ntiles);
+        m0 = (t / ntn) * g3::BM;
+        n0 = (t % ntn) * g3::BN;
+        kbeg = z * kslice;
+    };
+
+    floatx4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // pieces i and i+2 of a wave differ by a fixed row (k-row) offset, so two per-lane
+    // pointers per operand cover all four
+    const int64_t stepA = KCA ? (int64_t)16 * g.lda : (int64_t)4 * g.lda;
+    const int64_t stepB = KCB ? (int64_t)16 * g.ldb : (int64_t)4 * g.ldb;
+    int iu = 0, kti = 0;
+    const bf16* srcA[2];
+    const bf16* srcB[2];
+    auto set_src = [&]() {
+        int m0, n0, kb;
+        unit(iu, m0, n0, kb);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = wave * g3p::GLW + i;
+            srcA[i] = g3p_src<KCA>(A, g.lda, m0, kb, c, lane);
+            srcB[i] = g3p_src<KCB>(B, g.ldb, n0, kb, c, lane);
+        }
+    };
+    set_src();
+    auto glds = [&](const bf16* src, char* img, int i) {
+        __builtin_amdgcn_global_load_lds(G3_GLB(src), G3_LDS(img + (wave * g3p::GLW + i) * 1024),
+                                         16, 0, 0);
+    };
+    auto koffA = [&](int kt) { return KCA ? (int64_t)kt * g3p::BK : (int64_t)kt * g3p::BK * g.lda; };
+    auto koffB = [&](int kt) { return KCB ? (int64_t)kt * g3p::BK : (int64_t)kt * g3p::BK * g.ldb; };
+    auto advance_issue = [&]() {
+        if (++kti == nk) {
+            kti = 0;
+            ++iu;
+            if (iu < nmine) set_src();
+        }
+    };
+    auto issue_all = [&](char* img) {
+        const int64_t oa = koffA(kti), ob = koffB(kti);
+#pragma unroll
+        for (int i = 0; i < g3p::GLW; ++i) glds(srcA[i & 1] + oa + (i >> 1) * stepA, img, i);
+#pragma unroll
+        for (int i = 0; i < g3p::GLW; ++i)
+            glds(srcB[i & 1] + ob + (i >> 1) * stepB, img + g3p::OPB, i);
+        advance_issue();
+    };
+    if (S > 0) issue_all(smem);
+
+    bf16x8 a[8], b[4];
+    int ic = 0, ktc = 0;
+    bool epi = false;
+    auto read_unit = [&](const char* img, int u) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = g3p_frag<KCB>(img + g3p::OPB, wn * 64 + j * 16, u, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = g3p_frag<KCA>(img, wm * 128 + i * 16, u, lane);
+    };
+    auto mfma_row = [&](int i) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0)
+                           : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    };
+    auto finish_stage = [&]() {
+        if (++ktc == nk) {
+            int m0, n0, kb;
+            unit(ic, m0, n0, kb);
+            g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+            ktc = 0;
+            ++ic;
+            epi = true;
+        }
+    };
+    // Stage s+1 is issued right after the barrier that opens stage s, into the slot
+    // stage s-1 just vacated, two DMA pieces per MFMA group of the first k-unit.
+    int s = 0;
+    for (; s + 1 < S; ++s) {
+        const char* img = smem + (s & 1) * g3p::SLOT;
+        char* nimg = smem + ((s + 1) & 1) * g3p::SLOT;
+        if (SW && epi) g3_wait_vm<32>();
+        else g3_wait_vm<0>();
+        epi = false;
+        __builtin_amdgcn_s_barrier();
+        const int64_t oa = koffA(kti), ob = koffB(kti);
+        const bf16* pa0 = srcA[0] + oa;
+        const bf16* pa1 = srcA[1] + oa;
+        const bf16* pb0 = srcB[0] + ob;
+        const bf16* pb1 = srcB[1] + ob;
+        advance_issue();
+        read_unit(img, 0);
+        __builtin_amdgcn_s_setprio(1);
+        mfma_row(0); glds(pa0, nimg, 0); glds(pa1, nimg, 1);
+        mfma_row(1); glds(pa0 + stepA, nimg, 2); glds(pa1 + stepA, nimg, 3);
+        mfma_row(2); glds(pb0, nimg + g3p::OPB, 0); glds(pb1, nimg + g3p::OPB, 1);
+        mfma_row(3); glds(pb0 + stepB, nimg + g3p::OPB, 2); glds(pb1 + stepB, nimg + g3p::OPB, 3);
+#pragma unroll
+        for (int i = 4; i < 8; ++i) mfma_row(i);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+            __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        read_unit(img, 1);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) mfma_row(i);
+        __builtin_amdgcn_s_setprio(0);
+        finish_stage();
+    }
+    if (s < S) {
+        const char* img = smem + (s & 1) * g3p::SLOT;
+        g3_wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            read_unit(img, u);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) mfma_row(i);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        finish_stage();
+    }
+}
+
+static int g3_mode() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("SRNN_G3MODE");
+        v = e ? atoi(e) : 2;
+    }
+    return v;
+}
+
 template <typename TO, bool KCA, bool KCB, bool SW>
 static int launch3(const Gemm3Args& g, hipStream_t s) {
-    auto k = gemm3_kernel<TO, KCA, KCB, SW>;
-    static bool attr = false;
-    if (!attr) {
+    // mode 0: 32-deep 5-slot ring; 1: 64-deep pair mode; 2 (default): pair mode when an
+    // operand is k-contiguous (full-line DMA pieces), the ring otherwise
+    const int mode = g3_mode();
+    const bool pair = (mode == 1 || (mode == 2 && (KCA || KCB))) && (g.K / g.ksplit) % g3p::BK == 0;
+    auto k = pair ? gemm3p_kernel<TO, KCA, KCB, SW> : gemm3_kernel<TO, KCA, KCB, SW>;
+    const int lds = pair ? g3p::LDS : g3::LDS;
+    static bool attr[2] = {false, false};
+    if (!attr[pair]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, g3::LDS));
-        attr = true;
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+        attr[pair] = true;
     }
-    dim3 grid((g.M / g3::BM) * (g.N / g3::BN), 1, g.ksplit);
-    hipLaunchKernelGGL(k, grid, dim3(g3::NT), g3::LDS, s, g);
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        SRNN_CHECK_HIP(hipGetDevice(&dev));
+        SRNN_CHECK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int units = (g.M / g3::BM) * (g.N / g3::BN) * g.ksplit;
+    dim3 grid(units < ncu ? units : ncu);
+    hipLaunchKernelGGL(k, grid, dim3(g3::NT), lds, s, g);
     SRNN_LAUNCH_CHECK();
     return 0;
 }
@@ -286,7 +639,7 @@ static int g3_pick_split(int tiles, int K) {
     int best = 1;
     double best_cost = 1e30;
     for (int ks = 1; ks <= 64; ks *= 2) {
-        if (K % (ks * g3::BK) || K / ks < 8 * g3::BK) break;
+        if (K % (ks * (ks > 1 ? g3p::BK : g3::BK)) || K / ks < 8 * g3::BK) break;
         const int rounds = (tiles * ks + 255) / 256;
         const double cost = rounds * (K / ks / (double)g3::BK + (ks > 1 ? 24.0 : 8.0));
         if (cost < best_cost * 0.97) {

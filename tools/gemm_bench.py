@@ -11,8 +11,8 @@ import samplernn_hip as H  # noqa: E402
 DEV = 'cuda'
 
 
-def timeit(fn, reps=10):
-    for _ in range(3):
+def timeit(fn, reps=30):
+    for _ in range(10):
         fn()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -27,7 +27,13 @@ def run(M, N, K, tA, tB, dtype, out_dtype, tile, tag):
     A = torch.randn(K, M, device=DEV).to(dtype) if tA else torch.randn(M, K, device=DEV).to(dtype)
     B = torch.randn(N, K, device=DEV).to(dtype) if tB else torch.randn(K, N, device=DEV).to(dtype)
     out = torch.empty(M, N, device=DEV, dtype=out_dtype)
-    ms = timeit(lambda: H.gemm(A, B, transA=tA, transB=tB, out=out, tile=tile))
+    kw = {}
+    if '+mask' in tag:
+        kw['mask'] = torch.randn(M, N, device=DEV).to(dtype)
+    if '+bias' in tag:
+        kw['bias'] = torch.randn(N, device=DEV)
+        kw['relu'] = True
+    ms = timeit(lambda: H.gemm(A, B, transA=tA, transB=tB, out=out, tile=tile, **kw))
     tf = 2.0 * M * N * K / ms / 1e9
     print('%-34s tile=%2d %7.3f ms %8.1f TFLOP/s' % (tag, tile, ms, tf), flush=True)
 
@@ -45,9 +51,18 @@ if __name__ == '__main__':
         (8192, 3072, 1024, False, True, bf, f32, 'gru gi fwd NT'),
         (3072, 1024, 8192, True, False, bf, f32, 'gru wgrad TN'),
         (131072, 1024, 256, False, False, bf, bf, 'mlp dgrad out NN K256'),
+        (131072, 1024, 1024, False, True, bf, f32, 'mlp hidden fwd NT f32out'),
+        (131072, 1024, 1024, False, True, bf, bf, 'mlp hidden fwd NT +bias'),
+        (131072, 1024, 1024, False, False, bf, f32, 'mlp dgrad NN +mask'),
+        (131072, 1024, 256, False, False, bf, bf, 'mlp dgrad out NN K256 +mask'),
+        (16384, 1024, 8192, False, True, bf, f32, 'mlp hidden NT K8192'),
+        (131072, 1024, 1024, True, False, bf, bf, 'mlp hidden TN bf16out'),
         (256, 1024, 131072, True, False, bf, f32, 'mlp out wgrad TN'),
     ]
     tiles = [int(t) for t in os.environ.get('TILES', '5,3').split(',')]
+    only = os.environ.get('ONLY')
     for (M, N, K, tA, tB, dt, odt, tag) in shapes:
+        if only and only not in tag:
+            continue
         for tile in tiles:
             run(M, N, K, tA, tB, dt, odt, tile, tag)
