@@ -2,6 +2,8 @@
 // weight-norm forward/backward (torch weight_norm, model.py:119-131,177-178,303-306),
 // layout permutes for the folded weights, row gathers (nn.Embedding), column sums
 // (bias grads), and the fused clip + Adam update (optim.py:4-21, train.py:238).
+#include <algorithm>
+
 #include "samplernn_hip_internal.hpp"
 #include "ulaw_tables.h"
 
@@ -245,47 +247,98 @@ extern "C" int srnn_weight_norm_bwd(const float* g, const float* v, const float*
 }
 
 // ------------------------------------------------------------------ layout permutes
-// dst[p-order index] = src[(i0, i1, i2)], src dims (d0, d1, d2) row-major; `perm` gives
-// which src axis becomes dst axis 0/1/2.  Converts fp32 -> fp32 / bf16.
+// dst = src.permute(p0, p1, p2) made contiguous, src (d0, d1, d2) row-major fp32; dst
+// fp32 (optionally accumulated) or bf16.  When the innermost axis changes (o = p2 != 2)
+// the copy is a batch of 2-D transposes between src axis o and src axis 2, done through
+// 32 x 32 LDS tiles so that both the reads and the writes are coalesced.
+struct Perm3 {
+    int64_t S[3];    // src stride of src axis a
+    int64_t Dd[3];   // dst stride of src axis a
+    int d[3];
+    int o, b;        // src axis innermost in dst; remaining (batch) axis
+};
+
 template <typename TO, bool ACC>
-__global__ void permute3_kernel(const float* __restrict__ src, TO* __restrict__ dst, int d0,
-                                int d1, int d2, int p0, int p1, int p2) {
-    const int64_t n = (int64_t)d0 * d1 * d2;
-    int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void permute3_tiled_kernel(const float* __restrict__ src,
+                                                             TO* __restrict__ dst, Perm3 P) {
+    __shared__ float tile[32][33];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    const int nt2 = (P.d[2] + 31) / 32;
+    const int t2 = blockIdx.x % nt2;
+    const int64_t bi = blockIdx.x / nt2;
+    const int i0 = t2 * 32, o0 = blockIdx.y * 32;
+    const float* sb = src + bi * P.S[P.b];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int oi = o0 + ty + 8 * k, ii = i0 + tx;
+        if (oi < P.d[P.o] && ii < P.d[2]) tile[ty + 8 * k][tx] = sb[(int64_t)oi * P.S[P.o] + ii];
+    }
+    __syncthreads();
+    TO* db = dst + bi * P.Dd[P.b];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int ii = i0 + ty + 8 * k, oi = o0 + tx;
+        if (oi < P.d[P.o] && ii < P.d[2]) {
+            TO* q = db + (int64_t)ii * P.Dd[2] + oi;
+            const float v = tile[tx][ty + 8 * k];
+            if (ACC) *q = from_f<TO>(to_f(*q) + v);
+            else *q = from_f<TO>(v);
+        }
+    }
+}
+
+// innermost axis kept: walk src order (coalesced reads), dst rows of d2 stay contiguous
+template <typename TO, bool ACC>
+__global__ void permute3_copy_kernel(const float* __restrict__ src, TO* __restrict__ dst, Perm3 P) {
+    const int64_t n = (int64_t)P.d[0] * P.d[1] * P.d[2];
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= n) return;
-    const int dims[3] = {d0, d1, d2};
-    const int od1 = dims[p1], od2 = dims[p2];
-    const int a2 = idx % od2;
-    const int a1 = (idx / od2) % od1;
-    const int a0 = idx / ((int64_t)od2 * od1);
-    int s[3];
-    s[p0] = a0; s[p1] = a1; s[p2] = a2;
-    const float val = src[((int64_t)s[0] * d1 + s[1]) * d2 + s[2]];
-    if (ACC) dst[idx] = from_f<TO>(to_f(dst[idx]) + val);
-    else dst[idx] = from_f<TO>(val);
+    const int i2 = idx % P.d[2];
+    const int64_t q = idx / P.d[2];
+    const int i1 = q % P.d[1];
+    const int i0 = q / P.d[1];
+    TO* o = dst + i0 * P.Dd[0] + i1 * P.Dd[1] + i2;
+    if (ACC) *o = from_f<TO>(to_f(*o) + src[idx]);
+    else *o = from_f<TO>(src[idx]);
+}
+
+template <typename TO, bool ACC>
+static int permute3_launch(const float* src, TO* dst, const Perm3& P, hipStream_t s) {
+    if (P.o == 2) {
+        const int64_t n = (int64_t)P.d[0] * P.d[1] * P.d[2];
+        hipLaunchKernelGGL((permute3_copy_kernel<TO, ACC>), dim3(cdiv(n, 256)), dim3(256), 0, s,
+                           src, dst, P);
+    } else {
+        const int64_t gx = (int64_t)cdiv(P.d[2], 32) * P.d[P.b];
+        SRNN_REQUIRE(gx < (1ll << 31), "permute3: too large");
+        hipLaunchKernelGGL((permute3_tiled_kernel<TO, ACC>), dim3((unsigned)gx, cdiv(P.d[P.o], 32)),
+                           dim3(256), 0, s, src, dst, P);
+    }
+    SRNN_LAUNCH_CHECK();
+    return 0;
 }
 
 extern "C" int srnn_permute3(const float* src, void* dst, int dst_dtype, int d0, int d1, int d2,
                              int p0, int p1, int p2, int accumulate, void* stream) {
     const int64_t n = (int64_t)d0 * d1 * d2;
     if (n <= 0) return 0;
-    SRNN_REQUIRE(p0 + p1 + p2 == 3 && p0 != p1 && p1 != p2 && p0 != p2, "permute3: bad perm");
-    dim3 grid(cdiv(n, 256));
+    SRNN_REQUIRE(p0 + p1 + p2 == 3 && p0 != p1 && p1 != p2 && p0 != p2 && p0 >= 0 && p1 >= 0 &&
+                 p2 >= 0, "permute3: bad perm");
+    Perm3 P;
+    P.d[0] = d0; P.d[1] = d1; P.d[2] = d2;
+    P.S[0] = (int64_t)d1 * d2; P.S[1] = d2; P.S[2] = 1;
+    const int pr[3] = {p0, p1, p2};
+    const int64_t ds[3] = {(int64_t)P.d[p1] * P.d[p2], P.d[p2], 1};
+    for (int j = 0; j < 3; ++j) P.Dd[pr[j]] = ds[j];
+    P.o = p2;
+    P.b = p2 == 2 ? 0 : 1 - p2;       // the axis that is neither 2 nor o
     hipStream_t s = (hipStream_t)stream;
     if (dst_dtype == SRNN_F32) {
-        if (accumulate)
-            hipLaunchKernelGGL((permute3_kernel<float, true>), grid, dim3(256), 0, s, src,
-                               (float*)dst, d0, d1, d2, p0, p1, p2);
-        else
-            hipLaunchKernelGGL((permute3_kernel<float, false>), grid, dim3(256), 0, s, src,
-                               (float*)dst, d0, d1, d2, p0, p1, p2);
-    } else {
-        SRNN_REQUIRE(!accumulate, "permute3: accumulate needs fp32 dst");
-        hipLaunchKernelGGL((permute3_kernel<bf16, false>), grid, dim3(256), 0, s, src, (bf16*)dst,
-                           d0, d1, d2, p0, p1, p2);
+        if (accumulate) return permute3_launch<float, true>(src, (float*)dst, P, s);
+        return permute3_launch<float, false>(src, (float*)dst, P, s);
     }
-    SRNN_LAUNCH_CHECK();
-    return 0;
+    SRNN_REQUIRE(!accumulate, "permute3: accumulate needs fp32 dst");
+    return permute3_launch<bf16, false>(src, (bf16*)dst, P, s);
 }
 
 // 2-D strided copy with dtype conversion (fp32 -> fp32/bf16, bf16 -> fp32)
@@ -405,49 +458,103 @@ extern "C" int srnn_add_bcast_rows(float* x, const float* v, int B, int F, int D
 }
 
 // ------------------------------------------------------------------ column sums
-// partial[rb, c] = sum_{r in row block rb} src[r, c]  then out[c] (+)= sum_rb partial
-template <typename T>
-__global__ void colsum_partial_kernel(const T* __restrict__ src, int64_t lds, int64_t rows,
-                                      int cols, int rows_per_block, float* __restrict__ partial) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= cols) return;
-    const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
-    const int64_t r1 = min(rows, r0 + rows_per_block);
-    float s = 0.f;
-    for (int64_t r = r0; r < r1; ++r) s += to_f(src[r * lds + c]);
-    partial[(int64_t)blockIdx.y * cols + c] = s;
+// partial[rb, c] = sum_{r in row block rb} src[r, c]  then out[c] (+)= alpha * sum_rb partial.
+// A 256-thread block owns 64 columns (16 lanes x 4 adjacent columns, vector loads when
+// aligned) and 16 row lanes that stride its row block; the 16 row sums meet in LDS.  The
+// final pass is the same kernel over the partial matrix.  Fixed summation order: the
+// result is deterministic.
+typedef unsigned short cs_u16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void cs_ld4(const float* p, float (&v)[4]) {
+    const floatx4 x = *reinterpret_cast<const floatx4*>(p);
+    v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3];
+}
+__device__ __forceinline__ void cs_ld4(const bf16* p, float (&v)[4]) {
+    const cs_u16x4 x = *reinterpret_cast<const cs_u16x4*>(p);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = __uint_as_float((unsigned)x[e] << 16);
 }
 
-__global__ void colsum_final_kernel(const float* __restrict__ partial, int nrb, int cols,
-                                    float* __restrict__ out, float alpha, int accumulate) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= cols) return;
-    float s = 0.f;
-    for (int i = 0; i < nrb; ++i) s += partial[(int64_t)i * cols + c];
-    out[c] = accumulate ? out[c] + alpha * s : alpha * s;
+template <typename T, bool VEC, bool FINAL>
+__global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ src, int64_t lds,
+                                                     int64_t rows, int cols, int64_t rpb,
+                                                     float* __restrict__ dst, float alpha,
+                                                     int accumulate) {
+    __shared__ float red[16][65];
+    const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+    const int c = blockIdx.x * 64 + tx * 4;
+    const int64_t r0 = (int64_t)blockIdx.y * rpb;
+    const int64_t r1 = min(rows, r0 + rpb);
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    if (VEC && c + 3 < cols) {
+        for (int64_t r = r0 + ty; r < r1; r += 16) {
+            float v[4];
+            cs_ld4(src + r * lds + c, v);
+            s0 += v[0]; s1 += v[1]; s2 += v[2]; s3 += v[3];
+        }
+    } else {
+        for (int64_t r = r0 + ty; r < r1; r += 16) {
+            const T* p = src + r * lds;
+            if (c < cols) s0 += to_f(p[c]);
+            if (c + 1 < cols) s1 += to_f(p[c + 1]);
+            if (c + 2 < cols) s2 += to_f(p[c + 2]);
+            if (c + 3 < cols) s3 += to_f(p[c + 3]);
+        }
+    }
+    red[ty][tx * 4 + 0] = s0; red[ty][tx * 4 + 1] = s1;
+    red[ty][tx * 4 + 2] = s2; red[ty][tx * 4 + 3] = s3;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const int cc = blockIdx.x * 64 + threadIdx.x;
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) t += red[i][threadIdx.x];
+        if (cc < cols) {
+            if (FINAL) dst[cc] = accumulate ? dst[cc] + alpha * t : alpha * t;
+            else dst[(int64_t)blockIdx.y * cols + cc] = t;
+        }
+    }
+}
+
+template <typename T>
+static void colsum_pass(const T* src, int64_t lds, int64_t rows, int cols, int64_t rpb, int nrb,
+                        float* dst, float alpha, int accumulate, bool final_, hipStream_t s) {
+    const bool vec = (lds % 4 == 0) && ((uintptr_t)src % (4 * sizeof(T)) == 0);
+    dim3 grid(cdiv(cols, 64), nrb);
+    if (final_) {
+        if (vec) hipLaunchKernelGGL((colsum_kernel<T, true, true>), grid, dim3(256), 0, s, src, lds, rows, cols, rpb, dst, alpha, accumulate);
+        else hipLaunchKernelGGL((colsum_kernel<T, false, true>), grid, dim3(256), 0, s, src, lds, rows, cols, rpb, dst, alpha, accumulate);
+    } else {
+        if (vec) hipLaunchKernelGGL((colsum_kernel<T, true, false>), grid, dim3(256), 0, s, src, lds, rows, cols, rpb, dst, alpha, accumulate);
+        else hipLaunchKernelGGL((colsum_kernel<T, false, false>), grid, dim3(256), 0, s, src, lds, rows, cols, rpb, dst, alpha, accumulate);
+    }
 }
 
 int srnn_colsum_impl(int dtype, const void* src, int64_t lds, int64_t rows, int cols, float* out,
                      float alpha, int accumulate, float* work, int64_t work_elems, hipStream_t s) {
     if (cols <= 0) return 0;
-    int rpb = 256;
-    int nrb = (int)((rows + rpb - 1) / rpb);
-    while ((int64_t)nrb * cols > work_elems && rpb < (1 << 30)) {
-        rpb *= 2;
-        nrb = (int)((rows + rpb - 1) / rpb);
+    const int cblk = cdiv(cols, 64);
+    // ~2048 blocks in the first pass, at least 64 rows per block, partials within `work`
+    int64_t nrb = std::max<int64_t>(1, std::min<int64_t>(2048 / cblk, rows / 64));
+    nrb = std::min<int64_t>(nrb, work_elems / cols);
+    if (rows <= 0 || nrb <= 1) {
+        if (dtype == SRNN_F32)
+            colsum_pass<float>((const float*)src, lds, rows, cols, std::max<int64_t>(rows, 1), 1,
+                               out, alpha, accumulate, true, s);
+        else
+            colsum_pass<bf16>((const bf16*)src, lds, rows, cols, std::max<int64_t>(rows, 1), 1,
+                              out, alpha, accumulate, true, s);
+        SRNN_LAUNCH_CHECK();
+        return 0;
     }
-    SRNN_REQUIRE((int64_t)nrb * cols <= work_elems, "colsum: workspace too small");
-    if (nrb == 0) nrb = 1;
-    dim3 g1(cdiv(cols, 256), nrb);
+    const int64_t rpb = (rows + nrb - 1) / nrb;
+    nrb = (rows + rpb - 1) / rpb;
+    SRNN_REQUIRE(nrb * cols <= work_elems, "colsum: workspace too small");
     if (dtype == SRNN_F32)
-        hipLaunchKernelGGL((colsum_partial_kernel<float>), g1, dim3(256), 0, s, (const float*)src,
-                           lds, rows, cols, rpb, work);
+        colsum_pass<float>((const float*)src, lds, rows, cols, rpb, (int)nrb, work, 1.f, 0, false, s);
     else
-        hipLaunchKernelGGL((colsum_partial_kernel<bf16>), g1, dim3(256), 0, s, (const bf16*)src,
-                           lds, rows, cols, rpb, work);
+        colsum_pass<bf16>((const bf16*)src, lds, rows, cols, rpb, (int)nrb, work, 1.f, 0, false, s);
     SRNN_LAUNCH_CHECK();
-    hipLaunchKernelGGL(colsum_final_kernel, dim3(cdiv(cols, 256)), dim3(256), 0, s, work, nrb, cols,
-                       out, alpha, accumulate);
+    colsum_pass<float>(work, cols, nrb, cols, nrb, 1, out, alpha, accumulate, true, s);
     SRNN_LAUNCH_CHECK();
     return 0;
 }

@@ -191,8 +191,9 @@ def colsum(x, rows, cols, lds=None, out=None, alpha=1.0, accumulate=False):
     if out is None:
         out = torch.empty(cols, device=x.device, dtype=torch.float32)
     lds = cols if lds is None else lds
-    work = torch.empty(max(1, (rows + 255) // 256) * cols + 256, device=x.device,
-                       dtype=torch.float32)
+    # the first pass writes at most ~2048 / ceil(cols / 64) partial rows
+    nrb = max(1, min((rows + 63) // 64, 2048 // max(1, (cols + 63) // 64)))
+    work = torch.empty(nrb * cols + 256, device=x.device, dtype=torch.float32)
     lib().call('srnn_colsum', dcode(x), ptr(x), lds, rows, cols, ptr(out), alpha, int(accumulate),
                ptr(work), work.numel(), stream())
     return out

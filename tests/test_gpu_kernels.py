@@ -271,6 +271,36 @@ def test_mlp_dtab_scatter(hip, dtype, B, Tl, D, FS0, Q):
     torch.testing.assert_close(outs[0].double(), ref, atol=1e-9 + 1e-12 * B * Tl, rtol=1e-6)
 
 
+@pytest.mark.parametrize('perm', [(0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1),
+                                  (2, 1, 0)])
+@pytest.mark.parametrize('shape', [(3, 37, 70), (16, 64, 33), (1, 1, 5)])
+def test_permute3(hip, perm, shape):
+    x = _rand(*shape, seed=sum(shape)).to(DEV)
+    ref = x.permute(perm).contiguous()
+    torch.testing.assert_close(hip.permute3(x, perm), ref, atol=0, rtol=0)
+    torch.testing.assert_close(hip.permute3(x, perm, dtype=torch.bfloat16), ref.to(torch.bfloat16),
+                               atol=0, rtol=0)
+    acc = _rand(*ref.shape, seed=3).to(DEV)
+    want = acc + ref
+    hip.permute3(x, perm, out=acc, accumulate=True)
+    torch.testing.assert_close(acc, want, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('rows,cols', [(131072, 256), (8192, 1024), (100, 37), (1, 1030), (0, 8),
+                                       (5000, 16384)])
+def test_colsum(hip, dtype, rows, cols):
+    x = _rand(max(rows, 1), cols + 4, seed=rows + cols)[:rows].to(DEV, dtype)
+    view = x[:, 2:cols + 2] if dtype == torch.float32 else x[:, :cols]
+    ref = view.double().sum(0).float().cpu()
+    out = hip.colsum(view, rows, cols, lds=x.stride(0))
+    torch.testing.assert_close(out.cpu(), ref, atol=1e-5 * max(rows, 1) ** 0.5, rtol=1e-5)
+    out2 = torch.ones(cols, device=DEV)
+    hip.colsum(view, rows, cols, lds=x.stride(0), out=out2, alpha=0.5, accumulate=True)
+    torch.testing.assert_close(out2.cpu(), 1 + 0.5 * ref, atol=1e-5 * max(rows, 1) ** 0.5,
+                               rtol=1e-5)
+
+
 def test_adam_clip_matches_torch(hip):
     n = 10007
     p0 = _rand(n, seed=1)
