@@ -54,11 +54,101 @@ __global__ __launch_bounds__(256) void mlp_l1_kernel(const T* __restrict__ tab,
     for (int j = 0; j < VPT; ++j) orow[j] = from_f<T>(fmaxf(acc[j], 0.f));
 }
 
+// XCD-sliced variant for the training shape (many rows, D a multiple of 128): workgroup
+// b works on column slice b % (D / 128), so with D = 1024 every XCD only ever gathers its
+// own 128-column slice of the table -- 1 MiB in bf16, resident in that XCD's 4 MiB L2 --
+// instead of all XCDs streaming the whole 8 MiB table from the Infinity Cache.  A row is
+// one 16-lane group (8 columns = one 16-B bf16 load per lane and table row); its FS0
+// (<= 32) indices are fetched by the group's lanes and broadcast with shuffles; each
+// group works on two rows at a time so that 2 x FS0 gathers are in flight.
+typedef unsigned short l1_u16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void l1_add8(const float* p, float (&a)[8]) {
+    const floatx4 x = *reinterpret_cast<const floatx4*>(p);
+    const floatx4 y = *reinterpret_cast<const floatx4*>(p + 4);
+    a[0] += x[0]; a[1] += x[1]; a[2] += x[2]; a[3] += x[3];
+    a[4] += y[0]; a[5] += y[1]; a[6] += y[2]; a[7] += y[3];
+}
+__device__ __forceinline__ void l1_add8(const bf16* p, float (&a)[8]) {
+    const l1_u16x8 x = *reinterpret_cast<const l1_u16x8*>(p);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[e] += __uint_as_float((unsigned)x[e] << 16);
+}
+__device__ __forceinline__ void l1_store8(float* p, const float (&a)[8]) {
+    *reinterpret_cast<floatx4*>(p) = floatx4{fmaxf(a[0], 0.f), fmaxf(a[1], 0.f), fmaxf(a[2], 0.f), fmaxf(a[3], 0.f)};
+    *reinterpret_cast<floatx4*>(p + 4) = floatx4{fmaxf(a[4], 0.f), fmaxf(a[5], 0.f), fmaxf(a[6], 0.f), fmaxf(a[7], 0.f)};
+}
+__device__ __forceinline__ void l1_store8(bf16* p, const float (&a)[8]) {
+    l1_u16x8 x;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = __bfloat16_as_ushort(__float2bfloat16(fmaxf(a[e], 0.f)));
+    *reinterpret_cast<l1_u16x8*>(p) = x;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void mlp_l1_xcd_kernel(const T* __restrict__ tab,
+                                                         const int64_t* __restrict__ x,
+                                                         int64_t ldx, int xoff, int Tlen, int64_t nrows,
+                                                         int rows_per_block, int nslices,
+                                                         const float* __restrict__ upper,
+                                                         int64_t ldu, T* __restrict__ out,
+                                                         int64_t ldo, int D, int FS0, int Q) {
+    const int slice = blockIdx.x % nslices;
+    const int64_t rb = blockIdx.x / nslices;
+    const int lane = threadIdx.x & 15, grp = threadIdx.x >> 4;
+    const int c0 = slice * 128 + lane * 8;
+    const int64_t rbeg = rb * rows_per_block;
+    const int64_t rend = min(nrows, rbeg + rows_per_block);
+    for (int64_t r = rbeg + grp; r < rend; r += 32) {
+        const int64_t r2 = r + 16;
+        const bool two = r2 < rend;
+        const int b = (int)(r / Tlen), t = (int)(r - (int64_t)b * Tlen);
+        const int64_t* xr = x + (int64_t)b * ldx + xoff + t;
+        const int64_t rr = two ? r2 : r;
+        const int b2 = (int)(rr / Tlen), t2 = (int)(rr - (int64_t)b2 * Tlen);
+        const int64_t* xr2 = x + (int64_t)b2 * ldx + xoff + t2;
+        const int qa0 = lane < FS0 ? (int)xr[lane] : 0;
+        const int qa1 = lane + 16 < FS0 ? (int)xr[lane + 16] : 0;
+        const int qb0 = lane < FS0 ? (int)xr2[lane] : 0;
+        const int qb1 = lane + 16 < FS0 ? (int)xr2[lane + 16] : 0;
+        float a[8], c[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[e] = c[e] = 0.f;
+        l1_add8(upper + r * ldu + c0, a);
+        l1_add8(upper + rr * ldu + c0, c);
+        for (int k = 0; k < FS0; ++k) {
+            const int qa = k < 16 ? __shfl(qa0, k, 16) : __shfl(qa1, k - 16, 16);
+            const int qb = k < 16 ? __shfl(qb0, k, 16) : __shfl(qb1, k - 16, 16);
+            l1_add8(tab + ((int64_t)k * Q + qa) * D + c0, a);
+            l1_add8(tab + ((int64_t)k * Q + qb) * D + c0, c);
+        }
+        l1_store8(out + r * ldo + c0, a);
+        if (two) l1_store8(out + r2 * ldo + c0, c);
+    }
+}
+
 int srnn_mlp_l1_impl(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff,
                      const int* base, int B, int Tlen, const float* upper, int64_t ldu, void* out,
                      int64_t ldo, int D, int FS0, int Q, hipStream_t s) {
     SRNN_REQUIRE(D % 4 == 0, "mlp_l1: D must be a multiple of 4");
     SRNN_REQUIRE(FS0 <= 32, "mlp_l1: frame_sizes[0] must be <= 32");
+    const int64_t nrows = (int64_t)B * Tlen;
+    if (!base && D % 128 == 0 && nrows >= 4096 && ldu % 4 == 0 && (uintptr_t)upper % 16 == 0 &&
+        ldo % 8 == 0 && (uintptr_t)out % 16 == 0 && (uintptr_t)tab % 16 == 0) {
+        const int nslices = D / 128;
+        const int rpb = 64;
+        const int64_t nblk = (nrows + rpb - 1) / rpb * nslices;
+        SRNN_REQUIRE(nblk < (1ll << 31), "mlp_l1: too many rows");
+        if (dtype == SRNN_F32)
+            hipLaunchKernelGGL((mlp_l1_xcd_kernel<float>), dim3((unsigned)nblk), dim3(256), 0, s,
+                               (const float*)tab, x, ldx, xoff, Tlen, nrows, rpb, nslices, upper,
+                               ldu, (float*)out, ldo, D, FS0, Q);
+        else
+            hipLaunchKernelGGL((mlp_l1_xcd_kernel<bf16>), dim3((unsigned)nblk), dim3(256), 0, s,
+                               (const bf16*)tab, x, ldx, xoff, Tlen, nrows, rpb, nslices, upper,
+                               ldu, (bf16*)out, ldo, D, FS0, Q);
+        SRNN_LAUNCH_CHECK();
+        return 0;
+    }
     dim3 grid(cdiv(D, 256 * 4), (int64_t)B * Tlen);
     if (dtype == SRNN_F32)
         hipLaunchKernelGGL((mlp_l1_kernel<float, 4>), grid, dim3(256), 0, s, (const float*)tab, x,
