@@ -68,10 +68,11 @@ int srnn_gru_cell_bwd(int dtype, int B, int D, const float* dy, int64_t lddy,
                       int64_t lddghl, float* dgi, int64_t lddgi, float* ddir, void* stream);
 
 /* ---- SampleLevelMLP (model.py:308-325) ----------------------------------------------
- * a1[b*Tlen+t] = relu(sum_k tab[k][x[b*ldx + xoff + t + k]] + upper[b*Tlen+t])          */
+ * a1[b*Tlen+t] = relu(sum_k tab[k][x[b*ldx + xoff + t + k]] + upper[b*Tlen+t])
+ * tab / out in `dtype`; upper in `upper_dtype` (SRNN_F32 or SRNN_BF16)                  */
 int srnn_mlp_l1(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff, int B,
-                int Tlen, const float* upper, int64_t ldu, void* out, int64_t ldo, int D,
-                int FS0, int Q, void* stream);
+                int Tlen, int upper_dtype, const void* upper, int64_t ldu, void* out,
+                int64_t ldo, int D, int FS0, int Q, void* stream);
 /* dtab[x_{t+k}][k][:] += da_t  (Q, FS0, D) fp32 accumulate; backward of the folded     *
  * embedding+conv                                                                        */
 int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x, int64_t ldx,

@@ -15,8 +15,8 @@
 #include "../../include/samplernn_hip.h"
 
 int srnn_mlp_l1_impl(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff,
-                     const int* base, int B, int Tlen, const float* upper, int64_t ldu, void* out,
-                     int64_t ldo, int D, int FS0, int Q, hipStream_t s);
+                     const int* base, int B, int Tlen, int upper_dtype, const void* upper,
+                     int64_t ldu, void* out, int64_t ldo, int D, int FS0, int Q, hipStream_t s);
 int srnn_sample_impl(const float* z, int64_t ldz, int B, const float* noise, uint64_t seed,
                      const int* base, int off, int L, int64_t* seq, int64_t ldseq,
                      float* logp_out, hipStream_t s);
@@ -174,7 +174,7 @@ int mlp_step(Ctx& c, int off) {
     const SrnnModel* m = c.m;
     const int D = m->dim, Q = m->q_levels, B = c.B, dt = m->dtype;
     const int FS0 = m->tier[0].frame_size;
-    RET(srnn_mlp_l1_impl(dt, m->tab, c.seq, c.ldseq, off - FS0, c.b.base, B, 1,
+    RET(srnn_mlp_l1_impl(dt, m->tab, c.seq, c.ldseq, off - FS0, c.b.base, B, 1, SRNN_F32,
                          c.b.up[0] + (size_t)(off % FS0) * D, (int64_t)FS0 * D, c.b.a1, D, D, FS0,
                          Q, c.s));
     RET(linear_fwd(dt, dt, B, D, D, c.b.a1, D, m->w_hid, D, m->b_hid, c.b.a2, D, 1, c.s));

@@ -18,11 +18,11 @@
 
 // ------------------------------------------------------------------ L1 gather
 // rows r = b * Tlen + t;  idx_k = x[b * ldx + xoff(+base) + t + k]
-template <typename T, int VPT>
+template <typename T, typename TU, int VPT>
 __global__ __launch_bounds__(256) void mlp_l1_kernel(const T* __restrict__ tab,
                                                      const int64_t* __restrict__ x, int64_t ldx,
                                                      int xoff, const int* __restrict__ base,
-                                                     int Tlen, const float* __restrict__ upper,
+                                                     int Tlen, const TU* __restrict__ upper,
                                                      int64_t ldu, T* __restrict__ out, int64_t ldo,
                                                      int D, int FS0, int Q) {
     const int64_t r = blockIdx.y;
@@ -32,9 +32,9 @@ __global__ __launch_bounds__(256) void mlp_l1_kernel(const T* __restrict__ tab,
     const int o0 = (blockIdx.x * 256 + threadIdx.x) * VPT;
     if (o0 >= D) return;
     float acc[VPT];
-    const float* ur = upper + r * ldu + o0;
+    const TU* ur = upper + r * ldu + o0;
 #pragma unroll
-    for (int j = 0; j < VPT; ++j) acc[j] = ur[j];
+    for (int j = 0; j < VPT; ++j) acc[j] = to_f(ur[j]);
     // all index loads first, then all table-row loads: one exposed latency, not FS0
     constexpr int KMAX = 32;
     int qs[KMAX];
@@ -84,12 +84,12 @@ __device__ __forceinline__ void l1_store8(bf16* p, const float (&a)[8]) {
     *reinterpret_cast<l1_u16x8*>(p) = x;
 }
 
-template <typename T>
+template <typename T, typename TU>
 __global__ __launch_bounds__(256) void mlp_l1_xcd_kernel(const T* __restrict__ tab,
                                                          const int64_t* __restrict__ x,
                                                          int64_t ldx, int xoff, int Tlen, int64_t nrows,
                                                          int rows_per_block, int nslices,
-                                                         const float* __restrict__ upper,
+                                                         const TU* __restrict__ upper,
                                                          int64_t ldu, T* __restrict__ out,
                                                          int64_t ldo, int D, int FS0, int Q) {
     const int slice = blockIdx.x % nslices;
@@ -126,45 +126,56 @@ __global__ __launch_bounds__(256) void mlp_l1_xcd_kernel(const T* __restrict__ t
     }
 }
 
-int srnn_mlp_l1_impl(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff,
-                     const int* base, int B, int Tlen, const float* upper, int64_t ldu, void* out,
-                     int64_t ldo, int D, int FS0, int Q, hipStream_t s) {
-    SRNN_REQUIRE(D % 4 == 0, "mlp_l1: D must be a multiple of 4");
-    SRNN_REQUIRE(FS0 <= 32, "mlp_l1: frame_sizes[0] must be <= 32");
+template <typename T, typename TU>
+static int mlp_l1_launch(const T* tab, const int64_t* x, int64_t ldx, int xoff, const int* base,
+                         int B, int Tlen, const TU* upper, int64_t ldu, T* out, int64_t ldo,
+                         int D, int FS0, int Q, hipStream_t s) {
     const int64_t nrows = (int64_t)B * Tlen;
-    if (!base && D % 128 == 0 && nrows >= 4096 && ldu % 4 == 0 && (uintptr_t)upper % 16 == 0 &&
-        ldo % 8 == 0 && (uintptr_t)out % 16 == 0 && (uintptr_t)tab % 16 == 0) {
+    const int ue = (int)sizeof(TU);
+    if (!base && D % 128 == 0 && nrows >= 4096 && (ldu * ue) % 16 == 0 &&
+        (uintptr_t)upper % 16 == 0 && (ldo * (int)sizeof(T)) % 16 == 0 &&
+        (uintptr_t)out % 16 == 0 && (uintptr_t)tab % 16 == 0) {
         const int nslices = D / 128;
         const int rpb = 64;
         const int64_t nblk = (nrows + rpb - 1) / rpb * nslices;
         SRNN_REQUIRE(nblk < (1ll << 31), "mlp_l1: too many rows");
-        if (dtype == SRNN_F32)
-            hipLaunchKernelGGL((mlp_l1_xcd_kernel<float>), dim3((unsigned)nblk), dim3(256), 0, s,
-                               (const float*)tab, x, ldx, xoff, Tlen, nrows, rpb, nslices, upper,
-                               ldu, (float*)out, ldo, D, FS0, Q);
-        else
-            hipLaunchKernelGGL((mlp_l1_xcd_kernel<bf16>), dim3((unsigned)nblk), dim3(256), 0, s,
-                               (const bf16*)tab, x, ldx, xoff, Tlen, nrows, rpb, nslices, upper,
-                               ldu, (bf16*)out, ldo, D, FS0, Q);
-        SRNN_LAUNCH_CHECK();
-        return 0;
+        hipLaunchKernelGGL((mlp_l1_xcd_kernel<T, TU>), dim3((unsigned)nblk), dim3(256), 0, s, tab,
+                           x, ldx, xoff, Tlen, nrows, rpb, nslices, upper, ldu, out, ldo, D, FS0, Q);
+    } else {
+        dim3 grid(cdiv(D, 256 * 4), nrows);
+        hipLaunchKernelGGL((mlp_l1_kernel<T, TU, 4>), grid, dim3(256), 0, s, tab, x, ldx, xoff,
+                           base, Tlen, upper, ldu, out, ldo, D, FS0, Q);
     }
-    dim3 grid(cdiv(D, 256 * 4), (int64_t)B * Tlen);
-    if (dtype == SRNN_F32)
-        hipLaunchKernelGGL((mlp_l1_kernel<float, 4>), grid, dim3(256), 0, s, (const float*)tab, x,
-                           ldx, xoff, base, Tlen, upper, ldu, (float*)out, ldo, D, FS0, Q);
-    else
-        hipLaunchKernelGGL((mlp_l1_kernel<bf16, 4>), grid, dim3(256), 0, s, (const bf16*)tab, x,
-                           ldx, xoff, base, Tlen, upper, ldu, (bf16*)out, ldo, D, FS0, Q);
     SRNN_LAUNCH_CHECK();
     return 0;
 }
 
+int srnn_mlp_l1_impl(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff,
+                     const int* base, int B, int Tlen, int upper_dtype, const void* upper,
+                     int64_t ldu, void* out, int64_t ldo, int D, int FS0, int Q, hipStream_t s) {
+    SRNN_REQUIRE(D % 4 == 0, "mlp_l1: D must be a multiple of 4");
+    SRNN_REQUIRE(FS0 <= 32, "mlp_l1: frame_sizes[0] must be <= 32");
+    SRNN_REQUIRE(upper_dtype == SRNN_F32 || upper_dtype == SRNN_BF16, "mlp_l1: bad upper dtype");
+    if ((int64_t)B * Tlen <= 0) return 0;
+    if (dtype == SRNN_F32) {
+        if (upper_dtype == SRNN_F32)
+            return mlp_l1_launch<float, float>((const float*)tab, x, ldx, xoff, base, B, Tlen,
+                                               (const float*)upper, ldu, (float*)out, ldo, D, FS0, Q, s);
+        return mlp_l1_launch<float, bf16>((const float*)tab, x, ldx, xoff, base, B, Tlen,
+                                          (const bf16*)upper, ldu, (float*)out, ldo, D, FS0, Q, s);
+    }
+    if (upper_dtype == SRNN_F32)
+        return mlp_l1_launch<bf16, float>((const bf16*)tab, x, ldx, xoff, base, B, Tlen,
+                                          (const float*)upper, ldu, (bf16*)out, ldo, D, FS0, Q, s);
+    return mlp_l1_launch<bf16, bf16>((const bf16*)tab, x, ldx, xoff, base, B, Tlen,
+                                     (const bf16*)upper, ldu, (bf16*)out, ldo, D, FS0, Q, s);
+}
+
 extern "C" int srnn_mlp_l1(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff,
-                           int B, int Tlen, const float* upper, int64_t ldu, void* out,
-                           int64_t ldo, int D, int FS0, int Q, void* stream) {
-    return srnn_mlp_l1_impl(dtype, tab, x, ldx, xoff, nullptr, B, Tlen, upper, ldu, out, ldo, D,
-                            FS0, Q, (hipStream_t)stream);
+                           int B, int Tlen, int upper_dtype, const void* upper, int64_t ldu,
+                           void* out, int64_t ldo, int D, int FS0, int Q, void* stream) {
+    return srnn_mlp_l1_impl(dtype, tab, x, ldx, xoff, nullptr, B, Tlen, upper_dtype, upper, ldu,
+                            out, ldo, D, FS0, Q, (hipStream_t)stream);
 }
 
 // ------------------------------------------------------------------ wave helpers

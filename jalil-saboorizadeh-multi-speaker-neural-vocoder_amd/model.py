@@ -83,6 +83,7 @@ class SampleRNN(torch.nn.Module):
             for (frame_size, n_frame_samples, c) in zip(frame_sizes, ns_frame_samples, is_cond)
         ])
         self.sample_level_mlp = SampleLevelMLP(frame_sizes[0], dim, q_levels, weight_norm)
+        self.frame_level_rnns[0].__dict__['_feeds_mlp'] = True
         for m in self.modules():
             if m is not self:
                 m.__dict__['_root'] = self
@@ -271,7 +272,11 @@ class _TierFn(torch.autograd.Function):
         k = mod.frame_size
         W_up = H.permute3(nn.weight_of(mod.upsampling.conv_t), (2, 1, 0), dtype=T)  # (k, D, D)
         b_up = H.permute3(up_b.reshape(1, D, k), (0, 2, 1)).reshape(k * D)
-        Y = H.linear(outsT[-1].reshape(B * Fr, D), W_up.reshape(k * D, D), bias=b_up)
+        # the bottom tier feeds the MLP's gather directly: its upsampled output (and so the
+        # gradient coming back) is in the compute dtype; upper tiers stay fp32 (Cin input)
+        y_dt = T if mod.__dict__.get('_feeds_mlp') else torch.float32
+        Y = H.linear(outsT[-1].reshape(B * Fr, D), W_up.reshape(k * D, D), bias=b_up,
+                     out_dtype=y_dt)
         h_new = torch.stack([o[:, -1] for o in outs], 0)
         ctx.mod = mod
         ctx.reset = reset
@@ -298,8 +303,11 @@ class _TierFn(torch.autograd.Function):
         st = H.stream
         M = B * Fr
         # --- upsampling (nn.py:33-43)
-        dY2 = dY.reshape(M, k * D).float().contiguous()
-        dYT = H.cast(dY2, T)
+        if dY.dtype == T:
+            dY2 = dYT = dY.reshape(M, k * D).contiguous()
+        else:
+            dY2 = dY.reshape(M, k * D).float().contiguous()
+            dYT = H.cast(dY2, T)
         dWup = H.gemm(dYT, outsT[-1].reshape(M, D), transA=True)          # (k*D, D)
         db_up = H.colsum(dY2, M, k * D)
         dX = H.gemm(dYT, W_up.reshape(k * D, D))                          # (M, D)
@@ -445,8 +453,9 @@ class _MlpFn(torch.autograd.Function):
         dev = upper.device
         tab, Wp, ET = _build_tab(mlp, T)
         a1 = torch.empty((B * Tl, D), device=dev, dtype=T)
+        upper = upper.contiguous()
         H.lib().call('srnn_mlp_l1', H.dcode(T), H.ptr(tab), H.ptr(x), x.shape[1], 0, B, Tl,
-                     H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
+                     H.dcode(upper), H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
         W_hid = H.cast(nn.weight_of(mlp.hidden).reshape(D, D), T)
         W_out = H.cast(nn.weight_of(mlp.output).reshape(Q, D), T)
         a2 = H.linear(a1, W_hid, bias=mlp.hidden.bias, relu=True, out_dtype=T)
@@ -456,6 +465,7 @@ class _MlpFn(torch.autograd.Function):
                      H.ptr(logp), Q, None, H.F32, 0, 0.0, H.stream())
         ctx.mlp = mlp
         ctx.T = T
+        ctx.udt = upper.dtype
         ctx.dims = (B, Tl, D, Q, FS0)
         ctx.save_for_backward(x, a1, a2, logp, Wp, ET, W_hid, W_out)
         return logp.reshape(B, Tl, Q)
@@ -478,11 +488,12 @@ class _MlpFn(torch.autograd.Function):
         da2 = H.gemm(dz, W_out, mask=a2, out_dtype=T)                    # (M, D)
         dW_hid = H.gemm(da2, a1, transA=True)                            # (D, D)
         db_hid = H.colsum(da2, M, D)
-        da1 = H.gemm(da2, W_hid, mask=a1)                                # (M, D) fp32
+        # d(upper) in upper's dtype: bf16 when the bottom tier hands the MLP a bf16 upper
+        da1 = H.gemm(da2, W_hid, mask=a1, out_dtype=ctx.udt)              # (M, D)
         # folded embedding . conv backward: dTab[q][k][:] += da1[t] for x_{t+k} = q
         dtabT = torch.empty((Q, FS0 * D), device=dev, dtype=T)
         work = torch.empty(Q * FS0 * D, device=dev, dtype=torch.int64)
-        H.lib().call('srnn_mlp_dtab', H.F32, H.ptr(da1), D, H.ptr(x), x.shape[1], 0, B, Tl,
+        H.lib().call('srnn_mlp_dtab', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.shape[1], 0, B, Tl,
                      H.ptr(dtabT), H.dcode(T), D, FS0, Q, H.ptr(work), work.numel() * 8, st())
         dE = H.gemm(dtabT, Wp.reshape(FS0 * D, Q))                       # (Q, Q)
         dWp = torch.empty((FS0, D, Q), device=dev, dtype=torch.float32)

@@ -40,7 +40,7 @@ _SIGS = {
                       _L, _P, _L, _P],
     'srnn_gru_cell_bwd': [_I, _I, _I, _P, _L, _P, _L, _P, _P, _P, _P, _L, _P, _L, _P, _L, _P, _L,
                           _P, _L, _P, _P],
-    'srnn_mlp_l1': [_I, _P, _P, _L, _I, _I, _I, _P, _L, _P, _L, _I, _I, _I, _P],
+    'srnn_mlp_l1': [_I, _P, _P, _L, _I, _I, _I, _I, _P, _L, _P, _L, _I, _I, _I, _P],
     'srnn_mlp_dtab': [_I, _P, _L, _P, _L, _I, _I, _I, _P, _I, _I, _I, _I, _P, _SZ, _P],
     'srnn_logsoftmax_nll': [_P, _L, _P, _L, _I, _L, _I, _P, _P, _L, _P, _I, _L, _F, _P],
     'srnn_logsoftmax_bwd': [_P, _L, _P, _L, _L, _I, _P, _I, _L, _P],

@@ -244,18 +244,20 @@ def test_logsoftmax_and_sampler(hip):
     torch.testing.assert_close(logp.cpu(), torch.log_softmax(z.cpu(), 1), atol=2e-6, rtol=0)
 
 
-@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('dtype,udtype', [(torch.float32, torch.float32),
+                                          (torch.bfloat16, torch.float32),
+                                          (torch.bfloat16, torch.bfloat16)])
 @pytest.mark.parametrize('B,Tl,D,FS0,Q', [(2, 40, 72, 16, 256), (8, 1024, 256, 16, 256),
                                           (5, 1000, 384, 20, 64), (4, 2048, 1024, 16, 256)])
-def test_mlp_l1_gather(hip, dtype, B, Tl, D, FS0, Q):
+def test_mlp_l1_gather(hip, dtype, udtype, B, Tl, D, FS0, Q):
     """a1 = relu(upper + sum_k Tab[k][x_{t+k}]) -- both the generic and the XCD-sliced
     (rows >= 4096, D % 128 == 0) kernels."""
     g = torch.Generator().manual_seed(Tl + D)
     tab = _rand(FS0, Q, D, seed=D).to(dtype)
     x = torch.randint(0, Q, (B, Tl + FS0 - 1), generator=g)
-    upper = _rand(B * Tl, D, seed=5)
+    upper = _rand(B * Tl, D, seed=5).to(udtype)
     idx = torch.stack([x[:, k:k + Tl] for k in range(FS0)], -1).reshape(B * Tl, FS0)
-    ref = upper.clone()
+    ref = upper.float().clone()
     tf = tab.float()
     for k in range(FS0):
         ref += tf[k][idx[:, k]]
@@ -263,7 +265,8 @@ def test_mlp_l1_gather(hip, dtype, B, Tl, D, FS0, Q):
     out = torch.empty(B * Tl, D, device=DEV, dtype=dtype)
     tab_d, x_d, up_d = tab.to(DEV), x.to(DEV), upper.to(DEV)     # keep alive over the call
     hip.lib().call('srnn_mlp_l1', hip.dcode(dtype), hip.ptr(tab_d), hip.ptr(x_d), x.shape[1], 0,
-                   B, Tl, hip.ptr(up_d), D, hip.ptr(out), D, D, FS0, Q, hip.stream())
+                   B, Tl, hip.dcode(udtype), hip.ptr(up_d), D, hip.ptr(out), D, D, FS0, Q,
+                   hip.stream())
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     torch.testing.assert_close(out.float().cpu(), ref, atol=tol, rtol=tol)
 
