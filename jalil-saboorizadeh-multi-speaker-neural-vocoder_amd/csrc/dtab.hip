@@ -36,14 +36,27 @@ __device__ __forceinline__ long long fx40(float g) {
 template <typename T, int CW, int FSC>
 __global__ __launch_bounds__(DTAB_NT) void dtab_fx_kernel(
     const T* __restrict__ da, int64_t ldda, const int64_t* __restrict__ x, int64_t ldx, int xoff,
-    int Tlen, int B, int nb, unsigned long long* __restrict__ fx, int D, int FS0, int Q) {
+    int Tlen, int B, int nb, int nrb, unsigned long long* __restrict__ fx, int D, int FS0, int Q) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int FS = FSC ? FSC : FS0;
     unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [Q][FS][CW]
     unsigned char* idx = reinterpret_cast<unsigned char*>(smem + (size_t)Q * FS * CW * 8);
     const int tid = threadIdx.x;
-    const int c0 = blockIdx.x * CW;
-    const int b0 = blockIdx.y * nb;
+    // XCD-aware order: when the slices split evenly over the 8 XCDs, XCD x (= block % 8
+    // under round-robin dispatch) walks slices [x * nsl / 8, (x + 1) * nsl / 8) of every
+    // row block, so the 16-32 slices sharing a cache line of da are fetched into ONE L2
+    const int nsl = gridDim.x / nrb;
+    int slice, rb;
+    if (nsl % 8 == 0) {
+        const int x = blockIdx.x % 8, local = blockIdx.x / 8, per = nsl / 8;
+        slice = x * per + local % per;
+        rb = local / per;
+    } else {
+        slice = blockIdx.x % nsl;
+        rb = blockIdx.x / nsl;
+    }
+    const int c0 = slice * CW;
+    const int b0 = rb * nb;
     const int nbb = min(nb, B - b0);
     const int W = Tlen + FS - 1;
     const int nacc = Q * FS * CW;
@@ -63,7 +76,7 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_fx_kernel(
         const T* dab = da + (int64_t)b0 * Tlen * ldda + min(c0 + c, D - 1);
         unsigned long long* ak = acc + k * CW + c;
         const unsigned char* ik = idx + k;
-        constexpr int U = 8;
+        constexpr int U = 16;
         int r0 = tid / per_row;
         if constexpr (FSC * CW == 64) r0 = __builtin_amdgcn_readfirstlane(r0);
         int b = r0 / Tlen, t = r0 - b * Tlen;
@@ -98,6 +111,121 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_fx_kernel(
     }
 }
 
+// Position-major form for FS0 = 16 (the shipped configs).  Write s = x[b, xoff:] and
+// note that position p of a batch row receives the 16 rows t = p - k:
+//     dTab[s[p]][k][:] += da[b, p - k, :]      k = 0..15
+// so ONE index s[p] (wave-uniform) addresses all 16 taps x CW columns of a step, which
+// are contiguous in the [q][c][k] accumulator: no bank conflicts and no same-address
+// collisions however repetitive the audio.  Lane (c, i) keeps the fixed-point value of
+// row t = i (mod 16) in (p - 16, p] and its tap k = (p - i) mod 16 rotates with p, so a
+// row is loaded and converted ONCE (not once per tap) and each step is one address add,
+// a conditional register swap and one ds_add_u64.  A wave walks whole batch rows in
+// 16-position batches; the next batch's values are loaded while the current one runs.
+// DIRECT (one row block: the workgroup sees every row of its columns): the accumulator is
+// final, so the flush converts and stores straight into the output (no zeroed int64
+// buffer, no global atomics, no conversion pass).
+template <typename T, typename TO, bool DIRECT>
+__global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
+    const T* __restrict__ da, int64_t ldda, const int64_t* __restrict__ x, int64_t ldx, int xoff,
+    int Tlen, int B, int nb, int nrb, unsigned long long* __restrict__ fx, TO* __restrict__ out,
+    int D, int Q) {
+    constexpr int CW = 4, FS = 16;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [Q][CW][FS]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nsl = gridDim.x / nrb;
+    int slice, rb;
+    if (nsl % 8 == 0) {
+        const int xc = blockIdx.x % 8, local = blockIdx.x / 8, per = nsl / 8;
+        slice = xc * per + local % per;
+        rb = local / per;
+    } else {
+        slice = blockIdx.x % nsl;
+        rb = blockIdx.x / nsl;
+    }
+    const int c0 = slice * CW;
+    const int b0 = rb * nb;
+    const int nbb = min(nb, B - b0);
+    const int W = Tlen + FS - 1;                   // positions per batch row
+    const int nacc = Q * FS * CW;
+    for (int i = tid; i < nacc; i += DTAB_NT) acc[i] = 0ull;
+    __syncthreads();
+    const int c = lane >> 4, li = lane & 15;       // column, row residue
+    const bool cok = c0 + c < D;
+    const T* dcol = da + (c0 + (cok ? c : 0));
+    const int coff = c * FS;
+    const int nbatch = (W + 15) / 16;
+    const unsigned acc_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)acc;
+    for (int b = wave; b < nbb; b += DTAB_NT / 64) {
+        const T* drow = dcol + (int64_t)(b0 + b) * Tlen * ldda;
+        const int64_t* srow = x + (int64_t)(b0 + b) * ldx + xoff;   // wave-uniform
+        auto load = [&](int pbase) -> long long {
+            const int t = pbase + li;
+            return (cok && t < Tlen) ? fx40(to_f(drow[(int64_t)t * ldda])) : 0ll;
+        };
+        // the 16 indices of a batch (scalar loads, clamped to the row), one batch ahead
+        auto load_q = [&](int pbase, int (&q)[16]) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) q[j] = (int)srow[min(pbase + j, W - 1)];
+        };
+        long long cur = 0;                         // row p_base + li - 16 (none yet)
+        long long nxt = load(0);
+        int qn[16];
+        load_q(0, qn);
+        for (int bt = 0; bt < nbatch; ++bt) {
+            const int pbase = bt * 16;
+            const long long nv = nxt;
+            int qc[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) qc[j] = qn[j];
+            if (bt + 1 < nbatch) {
+                nxt = load(pbase + 16);
+                load_q(pbase + 16, qn);
+            }
+            const int jmax = min(16, W - pbase);
+            // all 16 addresses and operands in their own registers first, then 16
+            // independent ds_add_u64 back to back (a register reused between two atomics
+            // would hold the second until the first had read its operands)
+            unsigned ad[16];
+            unsigned long long va[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                ad[j] = acc_base + (unsigned)((qc[j] * CW * FS + coff + ((j - li) & 15)) * 8);
+                va[j] = (unsigned long long)(li <= j ? nv : cur);   // row enters at tap 0
+            }
+            if (jmax == 16) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    asm volatile("ds_add_u64 %0, %1" ::"v"(ad[j]), "v"(va[j]) : "memory");
+                // keep every address register live up to here: no register is reused
+                // (and so waited on) between two atomics of the batch
+                asm volatile("" ::"v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]),
+                             "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8]), "v"(ad[9]),
+                             "v"(ad[10]), "v"(ad[11]), "v"(ad[12]), "v"(ad[13]), "v"(ad[14]),
+                             "v"(ad[15]));
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    if (j < jmax) asm volatile("ds_add_u64 %0, %1" ::"v"(ad[j]), "v"(va[j]) : "memory");
+            }
+            cur = nv;
+        }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // inline-asm atomics
+    __syncthreads();
+    for (int i = tid; i < nacc; i += DTAB_NT) {
+        // i walks the output order (q, k, c): 4 adjacent threads store 4 adjacent columns
+        const int cc = i % CW, qk = i / CW;
+        const int k = qk % FS, q = qk / FS;
+        const unsigned long long v = acc[(q * CW + cc) * FS + k];
+        if (c0 + cc >= D) continue;
+        const int64_t o = ((int64_t)q * FS + k) * D + c0 + cc;
+        if (DIRECT) out[o] = from_f<TO>((float)((double)(long long)v * (1.0 / DTAB_SCALE)));
+        else if (v != 0ull) atomicAdd(&fx[o], v);
+    }
+}
+
 template <typename TO>
 __global__ void dtab_fx_convert_kernel(const unsigned long long* __restrict__ fx,
                                        TO* __restrict__ out, int64_t n) {
@@ -124,11 +252,55 @@ static int launch_dtab(const void* da, int64_t ldda, const int64_t* x, int64_t l
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         attr = true;
     }
-    dim3 grid(nslices, cdiv(B, nb));
+    const int nrb = cdiv(B, nb);
+    dim3 grid(nslices * nrb);
     hipLaunchKernelGGL((dtab_fx_kernel<T, CW, FSC>), grid, dim3(DTAB_NT), lds, s, (const T*)da, ldda, x,
-                       ldx, xoff, Tlen, B, nb, fx, D, FS0, Q);
+                       ldx, xoff, Tlen, B, nb, nrb, fx, D, FS0, Q);
     SRNN_LAUNCH_CHECK();
     return 0;
+}
+
+static bool getenv_off(const char* name) {
+    const char* e = getenv(name);
+    return e && e[0] == '0';
+}
+
+template <typename T, typename TO, bool DIRECT>
+static int launch_pos(const void* da, int64_t ldda, const int64_t* x, int64_t ldx, int xoff, int B,
+                      int Tlen, unsigned long long* fx, void* out, int D, int Q, int nb, int nrb,
+                      hipStream_t s) {
+    const int lds = Q * 16 * 4 * 8;
+    const int nslices = cdiv(D, 4);
+    auto k = dtab_pos_kernel<T, TO, DIRECT>;
+    static bool attr = false;
+    if (!attr) {
+        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024));
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(nslices * nrb), dim3(DTAB_NT), lds, s, (const T*)da, ldda, x, ldx,
+                       xoff, Tlen, B, nb, nrb, fx, (TO*)out, D, Q);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// position-major path (FS0 == 16); returns 1 if it wrote dtab_out directly
+template <typename T>
+static int dtab_pos(const void* da, int64_t ldda, const int64_t* x, int64_t ldx, int xoff, int B,
+                    int Tlen, unsigned long long* fx, void* out, int out_dtype, int D, int Q,
+                    bool* direct, hipStream_t s) {
+    const int nslices = cdiv(D, 4);
+    if (nslices >= 192) {          // every workgroup takes all rows of its 4 columns
+        *direct = true;
+        return out_dtype == SRNN_F32
+                   ? launch_pos<T, float, true>(da, ldda, x, ldx, xoff, B, Tlen, fx, out, D, Q, B, 1, s)
+                   : launch_pos<T, bf16, true>(da, ldda, x, ldx, xoff, B, Tlen, fx, out, D, Q, B, 1, s);
+    }
+    *direct = false;
+    const int nblk = std::max(1, 1024 / nslices);
+    const int nb = std::max(1, cdiv(B, nblk));
+    return launch_pos<T, float, false>(da, ldda, x, ldx, xoff, B, Tlen, fx, out, D, Q, nb,
+                                       cdiv(B, nb), s);
 }
 
 // dtab_out (Q, FS0, D) in out_dtype; work: >= Q*FS0*D*8 bytes of device scratch
@@ -141,6 +313,16 @@ extern "C" int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int6
     SRNN_REQUIRE(work && work_bytes >= (size_t)n * 8, "dtab: workspace too small");
     hipStream_t s = (hipStream_t)stream;
     unsigned long long* fx = (unsigned long long*)work;
+    if (FS0 == 16 && Q * 16 * 4 * 8 <= 160 * 1024 && (int64_t)B * Tlen > 0 &&
+        !getenv_off("SRNN_DTAB_POS")) {
+        bool direct = false;
+        if (cdiv(D, 4) < 192) SRNN_CHECK_HIP(hipMemsetAsync(fx, 0, (size_t)n * 8, s));
+        const int rc = dtype == SRNN_F32
+            ? dtab_pos<float>(da, ldda, x, ldx, xoff, B, Tlen, fx, dtab_out, out_dtype, D, Q, &direct, s)
+            : dtab_pos<bf16>(da, ldda, x, ldx, xoff, B, Tlen, fx, dtab_out, out_dtype, D, Q, &direct, s);
+        if (rc || direct) return rc;
+        goto convert;
+    }
     SRNN_CHECK_HIP(hipMemsetAsync(fx, 0, (size_t)n * 8, s));
     if ((int64_t)B * Tlen > 0) {
         const int W = Tlen + FS0 - 1;
@@ -159,6 +341,7 @@ extern "C" int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int6
 #undef DTAB_GO
         if (rc) return rc;
     }
+convert:
     if (out_dtype == SRNN_F32)
         hipLaunchKernelGGL(dtab_fx_convert_kernel<float>, dim3(cdiv(n, 256)), dim3(256), 0, s, fx,
                            (float*)dtab_out, n);
