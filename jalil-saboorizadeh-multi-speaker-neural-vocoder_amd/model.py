@@ -428,8 +428,10 @@ class SampleLevelMLP(torch.nn.Module):
         """model.py:308-325: indices (B, T+FS0-1), conditioning (B, T, D) -> log-probs (B,T,Q)."""
         H.need_cuda(upper_tier_conditioning)
         x = prev_samples.to(upper_tier_conditioning.device).long().contiguous()
-        return _MlpFn.apply(self, x, upper_tier_conditioning.float().contiguous(),
-                            *self._param_list())
+        u = upper_tier_conditioning
+        if u.dtype not in (torch.float32, _dt(self)):
+            u = u.float()
+        return _MlpFn.apply(self, x, u.contiguous(), *self._param_list())
 
 
 def _build_tab(mlp, T):
