@@ -88,7 +88,9 @@ int srnn_logsoftmax_bwd(const float* dlogp, int64_t lddl, const float* logp, int
 int srnn_nll_fwd(const float* logp, int64_t ldl, const int64_t* target, int64_t ldt, int Tlen,
                  int64_t rows, float* loss_row, void* stream);
 int srnn_nll_bwd(const int64_t* target, int64_t ldt, int Tlen, int64_t rows, int Q,
-                 float* dlogp, int64_t ldd, float gscale, void* stream);
+                 float* dlogp, int64_t ldd, float gscale, const float* gmul, void* stream);
+/* (gmul: optional device scalar the scale is multiplied by -- the incoming loss gradient,
+ *  read on the device so the backward never synchronises with the host)                 */
 int srnn_logsoftmax_nll(const float* z, int64_t ldz, const int64_t* target, int64_t ldt,
                         int Tlen, int64_t rows, int Q, float* loss_row, float* logp,
                         int64_t ldl, void* dz, int dz_dtype, int64_t ldd, float gscale,
@@ -126,6 +128,12 @@ int srnn_colsum(int dtype, const void* src, int64_t lds, int64_t rows, int cols,
 int srnn_adam_clip(float* p, float* g, float* m, float* v, void* p_bf16, int64_t n,
                    float clip_lo, float clip_hi, double lr, double beta1, double beta2,
                    double eps, int64_t step, void* stream);
+/* The same for `ntensors` parameters in one launch (per 64 tensors): host arrays of device
+ * pointers and element counts; p_bf16 may be NULL (no copies) or hold NULL entries.      */
+int srnn_adam_clip_multi(int ntensors, float* const* p, float* const* g, float* const* m,
+                         float* const* v, void* const* p_bf16, const int64_t* n, float clip_lo,
+                         float clip_hi, double lr, double beta1, double beta2, double eps,
+                         int64_t step, void* stream);
 
 /* ---- autoregressive generation (Generator.__call__, model.py:445-520) --------------- */
 typedef struct SrnnTier {

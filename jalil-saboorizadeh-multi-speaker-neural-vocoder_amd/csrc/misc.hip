@@ -590,6 +590,81 @@ __global__ void adam_clip_kernel(float* __restrict__ p, float* __restrict__ g,
     if (p_lp) p_lp[i] = __float2bfloat16(pi);
 }
 
+// Multi-tensor form: every parameter of the optimizer in ONE launch (the per-tensor
+// descriptors travel in the kernel argument block).  A workgroup takes a 2048-element
+// chunk of the concatenated index space; the chunk's first tensor is found by a uniform
+// scan of the offsets, and a thread steps to the next tensor at a boundary.
+#define ADAM_MT 64
+struct AdamMulti {
+    int nt;
+    int64_t off[ADAM_MT + 1];
+    float* p[ADAM_MT];
+    float* g[ADAM_MT];
+    float* m[ADAM_MT];
+    float* v[ADAM_MT];
+    bf16* plp[ADAM_MT];
+};
+
+__global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float lo, float hi,
+                                                              float w1, float b2, float omb2,
+                                                              float step_size, float bc2s,
+                                                              float eps) {
+    constexpr int CH = 2048;
+    const int64_t cs = (int64_t)blockIdx.x * CH;
+    int t = 0;
+    while (t + 1 < a.nt && a.off[t + 1] <= cs) ++t;
+    for (int i = threadIdx.x; i < CH; i += 256) {
+        const int64_t e = cs + i;
+        if (e >= a.off[a.nt]) return;
+        while (e >= a.off[t + 1]) ++t;
+        const int64_t j = e - a.off[t];
+        float gi = fminf(fmaxf(a.g[t][j], lo), hi);
+        a.g[t][j] = gi;
+        float mi = a.m[t][j];
+        mi = mi + w1 * (gi - mi);
+        float vi = a.v[t][j] * b2;
+        vi = vi + omb2 * gi * gi;
+        const float denom = sqrtf(vi) / bc2s + eps;
+        const float pi = a.p[t][j] + (-step_size) * mi / denom;
+        a.m[t][j] = mi;
+        a.v[t][j] = vi;
+        a.p[t][j] = pi;
+        if (a.plp[t]) a.plp[t][j] = __float2bfloat16(pi);
+    }
+}
+
+extern "C" int srnn_adam_clip_multi(int ntensors, float* const* p, float* const* g,
+                                    float* const* m, float* const* v, void* const* p_bf16,
+                                    const int64_t* n, float clip_lo, float clip_hi, double lr,
+                                    double beta1, double beta2, double eps, int64_t step,
+                                    void* stream) {
+    SRNN_REQUIRE(ntensors >= 0, "adam_multi: bad tensor count");
+    SRNN_REQUIRE(step >= 1, "adam: step must be >= 1");
+    const double bc1 = 1.0 - pow(beta1, (double)step);
+    const double bc2 = 1.0 - pow(beta2, (double)step);
+    const float step_size = (float)(lr / bc1);
+    const float bc2s = (float)sqrt(bc2);
+    for (int t0 = 0; t0 < ntensors; t0 += ADAM_MT) {
+        AdamMulti a;
+        a.nt = 0;
+        a.off[0] = 0;
+        for (int t = t0; t < ntensors && a.nt < ADAM_MT; ++t) {
+            if (n[t] <= 0) continue;
+            const int k = a.nt++;
+            a.p[k] = p[t]; a.g[k] = g[t]; a.m[k] = m[t]; a.v[k] = v[t];
+            a.plp[k] = p_bf16 ? (bf16*)p_bf16[t] : nullptr;
+            a.off[k + 1] = a.off[k] + n[t];
+        }
+        if (a.nt == 0) continue;
+        const int64_t nblk = (a.off[a.nt] + 2047) / 2048;
+        hipLaunchKernelGGL(adam_clip_multi_kernel, dim3((unsigned)nblk), dim3(256), 0,
+                           (hipStream_t)stream, a, clip_lo, clip_hi, (float)(1.0 - beta1),
+                           (float)beta2, (float)(1.0 - beta2), step_size, bc2s, (float)eps);
+        SRNN_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
 extern "C" int srnn_adam_clip(float* p, float* g, float* m, float* v, void* p_bf16,
                               int64_t n, float clip_lo, float clip_hi, double lr, double beta1,
                               double beta2, double eps, int64_t step, void* stream) {

@@ -311,9 +311,10 @@ __global__ void nll_fwd_kernel(const float* __restrict__ lp, int64_t ldl,
 
 __global__ void nll_bwd_kernel(const int64_t* __restrict__ target, int64_t ldt, int Tlen,
                                int64_t rows, int Q, float* __restrict__ dl, int64_t ldd,
-                               float gscale) {
+                               float gscale, const float* __restrict__ gmul) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= rows * Q) return;
+    if (gmul) gscale *= *gmul;
     const int64_t r = e / Q;
     const int q = e % Q;
     const int64_t b = r / Tlen, t = r % Tlen;
@@ -330,10 +331,11 @@ extern "C" int srnn_nll_fwd(const float* logp, int64_t ldl, const int64_t* targe
 }
 
 extern "C" int srnn_nll_bwd(const int64_t* target, int64_t ldt, int Tlen, int64_t rows, int Q,
-                            float* dlogp, int64_t ldd, float gscale, void* stream) {
+                            float* dlogp, int64_t ldd, float gscale, const float* gmul,
+                            void* stream) {
     if (rows <= 0) return 0;
     hipLaunchKernelGGL(nll_bwd_kernel, dim3(cdiv(rows * Q, 256)), dim3(256), 0,
-                       (hipStream_t)stream, target, ldt, Tlen, rows, Q, dlogp, ldd, gscale);
+                       (hipStream_t)stream, target, ldt, Tlen, rows, Q, dlogp, ldd, gscale, gmul);
     SRNN_LAUNCH_CHECK();
     return 0;
 }

@@ -151,9 +151,11 @@ class _NllBitsFn(torch.autograd.Function):
         (tg,) = ctx.saved_tensors
         B, T, Q = ctx.shape
         d = torch.empty((B, T, Q), device=tg.device, dtype=torch.float32)
-        # gscale = g * log2(e) / N  (mean reduction); g is a 0-d device tensor
-        scale = float(g) * LOG2E / (B * T)
-        H.lib().call('srnn_nll_bwd', H.ptr(tg), T, T, B * T, Q, H.ptr(d), Q, scale, H.stream())
+        # gscale = g * log2(e) / N  (mean reduction); g (0-d device tensor) is read on the
+        # device: no host synchronisation inside backward
+        gd = g.detach().float().reshape(1).contiguous()
+        H.lib().call('srnn_nll_bwd', H.ptr(tg), T, T, B * T, Q, H.ptr(d), Q, LOG2E / (B * T),
+                     H.ptr(gd), H.stream())
         return d, None
 
 

@@ -16,11 +16,15 @@ import samplernn_hip as H
 
 
 def _fused_adam_step(optimizer, lo, hi):
+    """All parameters of a group that share a step count go through ONE multi-tensor
+    launch (srnn_adam_clip_multi) instead of one launch per tensor."""
+    import ctypes
     for group in optimizer.param_groups:
         if group.get('weight_decay', 0) != 0 or group.get('amsgrad', False) or \
                 group.get('maximize', False):
             raise NotImplementedError('fused clip+Adam: weight_decay/amsgrad/maximize')
         b1, b2 = group['betas']
+        by_step = {}
         for p in group['params']:
             if not p.requires_grad:
                 continue
@@ -31,11 +35,21 @@ def _fused_adam_step(optimizer, lo, hi):
                 st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
+            elif not p.grad.is_contiguous() or p.grad.dtype != torch.float32:
+                p.grad = p.grad.float().contiguous()
+            if not (p.is_contiguous() and p.dtype == torch.float32):
+                raise NotImplementedError('fused clip+Adam: contiguous fp32 parameters only')
             st['step'] += 1
-            H.lib().call('srnn_adam_clip', H.ptr(p), H.ptr(p.grad), H.ptr(st['exp_avg']),
-                         H.ptr(st['exp_avg_sq']), None, p.numel(), float(lo), float(hi),
-                         float(group['lr']), float(b1), float(b2), float(group['eps']),
-                         int(st['step'].item()), H.stream())
+            by_step.setdefault(int(st['step'].item()), []).append((p, st))
+        for step, items in sorted(by_step.items()):
+            n = len(items)
+            arr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])  # noqa: E731
+            H.lib().call('srnn_adam_clip_multi', n, arr([p for p, _ in items]),
+                         arr([p.grad for p, _ in items]), arr([s['exp_avg'] for _, s in items]),
+                         arr([s['exp_avg_sq'] for _, s in items]), None,
+                         (ctypes.c_int64 * n)(*[p.numel() for p, _ in items]), float(lo),
+                         float(hi), float(group['lr']), float(b1), float(b2),
+                         float(group['eps']), step, H.stream())
 
 
 def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):

@@ -45,7 +45,7 @@ _SIGS = {
     'srnn_logsoftmax_nll': [_P, _L, _P, _L, _I, _L, _I, _P, _P, _L, _P, _I, _L, _F, _P],
     'srnn_logsoftmax_bwd': [_P, _L, _P, _L, _L, _I, _P, _I, _L, _P],
     'srnn_nll_fwd': [_P, _L, _P, _L, _I, _L, _P, _P],
-    'srnn_nll_bwd': [_P, _L, _I, _L, _I, _P, _L, _F, _P],
+    'srnn_nll_bwd': [_P, _L, _I, _L, _I, _P, _L, _F, _P, _P],
     'srnn_weight_norm_fwd': [_P, _P, _P, _P, _I, _L, _P],
     'srnn_weight_norm_bwd': [_P, _P, _P, _P, _P, _I, _L, _I, _P],
     'srnn_permute3': [_P, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P],
@@ -56,6 +56,7 @@ _SIGS = {
     'srnn_add_bcast_rows': [_P, _P, _I, _I, _I, _L, _P],
     'srnn_colsum': [_I, _P, _L, _L, _I, _P, _F, _I, _P, _L, _P],
     'srnn_adam_clip': [_P, _P, _P, _P, _P, _L, _F, _F, _D, _D, _D, _D, _L, _P],
+    'srnn_adam_clip_multi': [_I, _P, _P, _P, _P, _P, _P, _F, _F, _D, _D, _D, _D, _L, _P],
     'srnn_gen_workspace_size': [_P, _I, ctypes.POINTER(_SZ)],
     'srnn_generate': [_P, _I, _I, _P, _P, _P, _U64, _P, _P, _P, _SZ, _I, _P],
 }

@@ -328,6 +328,32 @@ def test_colsum(hip, dtype, rows, cols):
                                rtol=1e-5)
 
 
+def test_adam_clip_multi_matches_torch(hip):
+    """Multi-tensor launch: 70 tensors (two launches of <= 64) of ragged sizes, 3 steps."""
+    import ctypes
+    sizes = [1, 3, 7, 64, 1000, 2049, 4096, 10007] * 9
+    sizes = sizes[:70]
+    ps = [_rand(n, seed=i).to(DEV) for i, n in enumerate(sizes)]
+    ms = [torch.zeros(n, device=DEV) for n in sizes]
+    vs = [torch.zeros(n, device=DEV) for n in sizes]
+    refs = [p.detach().cpu().clone().requires_grad_(True) for p in ps]
+    opt = torch.optim.Adam(refs, lr=1e-3)
+    arr = lambda ts: (ctypes.c_void_p * len(ts))(*[t.data_ptr() for t in ts])  # noqa: E731
+    for step in range(1, 4):
+        gs = [_rand(n, scale=3.0, seed=100 * step + i) for i, n in enumerate(sizes)]
+        gd = [g.to(DEV) for g in gs]
+        hip.lib().call('srnn_adam_clip_multi', len(sizes), arr(ps), arr(gd), arr(ms), arr(vs), None,
+                       (ctypes.c_int64 * len(sizes))(*sizes), -1.0, 1.0, 1e-3, 0.9, 0.999, 1e-8,
+                       step, hip.stream())
+        for r, g in zip(refs, gs):
+            r.grad = g.clamp(-1, 1)
+        opt.step()
+        for g, d in zip(gs, gd):
+            torch.testing.assert_close(d.cpu(), g.clamp(-1, 1))
+    for p, r in zip(ps, refs):
+        torch.testing.assert_close(p.cpu(), r.detach(), atol=1e-7, rtol=1e-6)
+
+
 def test_adam_clip_matches_torch(hip):
     n = 10007
     p0 = _rand(n, seed=1)
