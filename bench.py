@@ -102,10 +102,12 @@ def run_tbptt(args, dev, dist_mod):
     t0 = time.perf_counter()
     for n in range(args.warmup, n_chunks):
         losses.append(step(n))
+    t_host = time.perf_counter() - t0      # enqueue time: close to dt when launch-bound
     torch.cuda.synchronize()
     dist_mod.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    sys.stderr.write('tbptt host enqueue %.2f ms/step\n' % (t_host * 1e3 / max(args.steps, 1)))
     dt = dist_mod.max_over_ranks(dt, dev)
     loss_vals = [float(l) for l in losses]
     return dt, loss_vals, pred, m

@@ -119,6 +119,8 @@ int srnn_scatter_add_rows(float* table, int64_t ldt, const int64_t* idx, int64_t
 int srnn_axpby(float* out, const float* a, const float* b, float alpha, float beta, int64_t n,
                void* stream);
 int srnn_add_bcast_rows(float* x, const float* v, int B, int F, int D, int64_t ldv, void* stream);
+/* out[b][c] = sum_{f<F} src[(b*F + f)*lds + c]  (per-sequence frame sums, fp32)        */
+int srnn_segsum(const float* src, int64_t lds, int B, int F, int D, float* out, void* stream);
 int srnn_colsum(int dtype, const void* src, int64_t lds, int64_t rows, int cols, float* out,
                 float alpha, int accumulate, float* work, int64_t work_elems, void* stream);
 

@@ -176,6 +176,12 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
                    const float* bias, int bias_mode, int relu, const void* mask, int64_t ldmask,
                    int force, hipStream_t s);
 
+int srnn_gemm_small_try(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
+                        float alpha, const void* A, int64_t lda, const void* B, int64_t ldb,
+                        float beta, const float* Cin, int64_t ldcin, void* C, int64_t ldc,
+                        const float* bias, int bias_mode, int relu, const void* mask,
+                        hipStream_t s);
+
 static bool env_on(const char* name) {
     const char* e = getenv(name);
     return !(e && e[0] == '0');
@@ -226,6 +232,13 @@ int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int 
     };
     g.vecA = aligned(A, lda, strideA);
     g.vecB = aligned(B, ldb, strideB);
+    // thin problems (N <= 64 weight gradients, K <= 64 input projections); tile 6 forces
+    if ((tile < 0 || tile == 6) && batch == 1) {
+        int rc = srnn_gemm_small_try(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, B,
+                                     ldb, beta, Cin, ldcin, C, ldc, bias, bias_mode, relu, mask, s);
+        if (rc >= 0) return rc;
+        SRNN_REQUIRE(tile != 6, "gemm: shape not eligible for the thin path");
+    }
     // skinny NT problems (M = batch rows): small-tile deep-ring kernel; tile 4 forces it
     {
         const int KBr = 256 / es;

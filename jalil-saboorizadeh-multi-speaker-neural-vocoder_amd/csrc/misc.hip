@@ -559,6 +559,27 @@ int srnn_colsum_impl(int dtype, const void* src, int64_t lds, int64_t rows, int 
     return 0;
 }
 
+// out[b][c] = sum_{f < F} src[(b * F + f) * lds + c]   (per-sequence sum over frames)
+__global__ void segsum_kernel(const float* __restrict__ src, int64_t lds, int B, int F, int D,
+                              float* __restrict__ out) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = blockIdx.y;
+    if (c >= D) return;
+    const float* p = src + (int64_t)b * F * lds + c;
+    float s = 0.f;
+    for (int f = 0; f < F; ++f) s += p[(int64_t)f * lds];
+    out[(int64_t)b * D + c] = s;
+}
+
+extern "C" int srnn_segsum(const float* src, int64_t lds, int B, int F, int D, float* out,
+                           void* stream) {
+    if ((int64_t)B * D <= 0) return 0;
+    hipLaunchKernelGGL(segsum_kernel, dim3(cdiv(D, 256), B), dim3(256), 0, (hipStream_t)stream,
+                       src, lds, B, F, D, out);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
 extern "C" int srnn_colsum(int dtype, const void* src, int64_t lds, int64_t rows, int cols,
                            float* out, float alpha, int accumulate, float* work,
                            int64_t work_elems, void* stream) {
@@ -597,7 +618,8 @@ __global__ void adam_clip_kernel(float* __restrict__ p, float* __restrict__ g,
 #define ADAM_MT 64
 struct AdamMulti {
     int nt;
-    int64_t off[ADAM_MT + 1];
+    int64_t off[ADAM_MT + 1];     // element offsets
+    int boff[ADAM_MT + 1];        // first workgroup of each tensor
     float* p[ADAM_MT];
     float* g[ADAM_MT];
     float* m[ADAM_MT];
@@ -610,26 +632,33 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
                                                               float step_size, float bc2s,
                                                               float eps) {
     constexpr int CH = 2048;
-    const int64_t cs = (int64_t)blockIdx.x * CH;
+    // workgroups never straddle tensors, so the tensor index is uniform and its pointers
+    // come from the argument block with scalar loads
     int t = 0;
-    while (t + 1 < a.nt && a.off[t + 1] <= cs) ++t;
+    while (t + 1 < a.nt && a.boff[t + 1] <= (int)blockIdx.x) ++t;
+    t = __builtin_amdgcn_readfirstlane(t);
+    const int64_t n = a.off[t + 1] - a.off[t];
+    float* __restrict__ P = a.p[t];
+    float* __restrict__ G = a.g[t];
+    float* __restrict__ Mm = a.m[t];
+    float* __restrict__ V = a.v[t];
+    bf16* __restrict__ PL = a.plp[t];
+    const int64_t j0 = (int64_t)(blockIdx.x - a.boff[t]) * CH;
     for (int i = threadIdx.x; i < CH; i += 256) {
-        const int64_t e = cs + i;
-        if (e >= a.off[a.nt]) return;
-        while (e >= a.off[t + 1]) ++t;
-        const int64_t j = e - a.off[t];
-        float gi = fminf(fmaxf(a.g[t][j], lo), hi);
-        a.g[t][j] = gi;
-        float mi = a.m[t][j];
+        const int64_t j = j0 + i;
+        if (j >= n) return;
+        float gi = fminf(fmaxf(G[j], lo), hi);
+        G[j] = gi;
+        float mi = Mm[j];
         mi = mi + w1 * (gi - mi);
-        float vi = a.v[t][j] * b2;
+        float vi = V[j] * b2;
         vi = vi + omb2 * gi * gi;
         const float denom = sqrtf(vi) / bc2s + eps;
-        const float pi = a.p[t][j] + (-step_size) * mi / denom;
-        a.m[t][j] = mi;
-        a.v[t][j] = vi;
-        a.p[t][j] = pi;
-        if (a.plp[t]) a.plp[t][j] = __float2bfloat16(pi);
+        const float pi = P[j] + (-step_size) * mi / denom;
+        Mm[j] = mi;
+        V[j] = vi;
+        P[j] = pi;
+        if (PL) PL[j] = __float2bfloat16(pi);
     }
 }
 
@@ -648,15 +677,17 @@ extern "C" int srnn_adam_clip_multi(int ntensors, float* const* p, float* const*
         AdamMulti a;
         a.nt = 0;
         a.off[0] = 0;
+        a.boff[0] = 0;
         for (int t = t0; t < ntensors && a.nt < ADAM_MT; ++t) {
             if (n[t] <= 0) continue;
             const int k = a.nt++;
             a.p[k] = p[t]; a.g[k] = g[t]; a.m[k] = m[t]; a.v[k] = v[t];
             a.plp[k] = p_bf16 ? (bf16*)p_bf16[t] : nullptr;
             a.off[k + 1] = a.off[k] + n[t];
+            a.boff[k + 1] = a.boff[k] + (int)((n[t] + 2047) / 2048);
         }
         if (a.nt == 0) continue;
-        const int64_t nblk = (a.off[a.nt] + 2047) / 2048;
+        const int64_t nblk = a.boff[a.nt];
         hipLaunchKernelGGL(adam_clip_multi_kernel, dim3((unsigned)nblk), dim3(256), 0,
                            (hipStream_t)stream, a, clip_lo, clip_hi, (float)(1.0 - beta1),
                            (float)beta2, (float)(1.0 - beta2), step_size, bc2s, (float)eps);

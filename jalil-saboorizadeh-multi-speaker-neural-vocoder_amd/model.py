@@ -338,8 +338,9 @@ class _TierFn(torch.autograd.Function):
                              H.ptr(dGH[:, t]), Fr * 3 * D,
                              H.ptr(dGHT[:, t]) if lp else None, Fr * 3 * D,
                              H.ptr(dGI[:, t]), Fr * 3 * D, H.ptr(ddir[t % 2]), st())
-            dh_in[l] = H.gemm(dGHT[:, 0], Whh[l], M=B, N=D, K=3 * D, lda=Fr * 3 * D, ldb=D,
-                              cin=ddir[0], beta=1.0)
+            # dh_0 = dgh_0 . W_hh + dh_direct, as an NT product on W_hh^T (skinny ring path)
+            dh_in[l] = H.gemm(dGHT[:, 0], WhhT, transB=True, M=B, N=D, K=3 * D,
+                              lda=Fr * 3 * D, ldb=3 * D, cin=ddir[0], beta=1.0)
             # previous hidden states of every step: [h_in, out[:, :F-1]]
             hprevT = torch.empty((B, Fr, D), device=dev, dtype=T)
             H.lib().call('srnn_copy2d', H.F32, H.dcode(T), B, D, H.ptr(h_in[l]), D,
@@ -369,10 +370,8 @@ class _TierFn(torch.autograd.Function):
             dW_c = H.gemm(dx0T, condT, transA=True)                      # (D, C)
             grads += nn.weight_grad_to_params(mod.cond_expand, dW_c.reshape(D, C, 1))
             grads += [g_ie_b.clone()]                                    # cond bias grad
-            ones = torch.ones((1, Fr), device=dev, dtype=torch.float32)
             dspk = torch.empty((B, D), device=dev, dtype=torch.float32)
-            H.gemm(ones, dx0, M=1, N=D, K=Fr, lda=Fr, ldb=D, ldc=D, out=dspk, batch=B, sA=0,
-                   sB=Fr * D, sC=D)
+            H.lib().call('srnn_segsum', H.ptr(dx0), D, B, Fr, D, H.ptr(dspk), st())
             dspkT = H.cast(dspk, T)
             dW_s = H.gemm(dspkT, spk_embT, transA=True)                  # (D, S)
             db_s = H.colsum(dspk, B, D)

@@ -54,6 +54,7 @@ _SIGS = {
     'srnn_scatter_add_rows': [_P, _L, _P, _L, _I, _P, _L, _P],
     'srnn_axpby': [_P, _P, _P, _F, _F, _L, _P],
     'srnn_add_bcast_rows': [_P, _P, _I, _I, _I, _L, _P],
+    'srnn_segsum': [_P, _L, _I, _I, _I, _P, _P],
     'srnn_colsum': [_I, _P, _L, _L, _I, _P, _F, _I, _P, _L, _P],
     'srnn_adam_clip': [_P, _P, _P, _P, _P, _L, _F, _F, _D, _D, _D, _D, _L, _P],
     'srnn_adam_clip_multi': [_I, _P, _P, _P, _P, _P, _P, _F, _F, _D, _D, _D, _D, _L, _P],

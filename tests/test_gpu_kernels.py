@@ -93,6 +93,46 @@ def test_gemm3_256_kernel(hip, out_dtype, transA, transB, M, N, K, epi):
 
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('transA', [0, 1])
+@pytest.mark.parametrize('M,N,K', [(1024, 16, 8192), (1024, 43, 2048), (1000, 6, 128),
+                                   (128, 64, 1024), (300, 1, 5000)])
+def test_gemm_thin_small_n(hip, dtype, transA, M, N, K):
+    """Thin path (tile 6): N <= 64 weight gradients, split-K with atomics."""
+    A = _rand(K, M, seed=1) if transA else _rand(M, K, seed=1)
+    B = _rand(K, N, seed=2)
+    Ad, Bd = A.to(DEV, dtype), B.to(DEV, dtype)
+    out = hip.gemm(Ad, Bd, transA=bool(transA), tile=6, alpha=0.5)
+    Af, Bf = Ad.float().cpu(), Bd.float().cpu()
+    ref = 0.5 * ((Af.t() if transA else Af) @ Bf)
+    torch.testing.assert_close(out.cpu(), ref, atol=1e-4 * np.sqrt(K), rtol=1e-4)
+
+
+@pytest.mark.parametrize('dtype,odt', [(torch.float32, torch.float32),
+                                       (torch.bfloat16, torch.float32),
+                                       (torch.bfloat16, torch.bfloat16)])
+@pytest.mark.parametrize('M,N,K', [(8192, 1024, 16), (2048, 1024, 43), (300, 700, 64)])
+def test_gemm_thin_small_k(hip, dtype, odt, M, N, K):
+    """Thin path (tile 6): K <= 64 input projections with Cin + bias (+ relu)."""
+    A, W = _rand(M, K, seed=1), _rand(N, K, seed=2)
+    cin, bias = _rand(M, N, seed=3), _rand(N, seed=4)
+    Ad, Wd = A.to(DEV, dtype), W.to(DEV, dtype)
+    out = hip.gemm(Ad, Wd, transB=True, cin=cin.to(DEV), beta=1.0, bias=bias.to(DEV), relu=True,
+                   out_dtype=odt, tile=6)
+    ref = (Ad.float().cpu() @ Wd.float().cpu().t() + cin + bias).clamp_min(0)
+    tol = 1e-4 if odt == torch.float32 else 2e-2
+    torch.testing.assert_close(out.float().cpu(), ref, atol=tol, rtol=tol)
+
+
+def test_segsum(hip):
+    B, F, D = 7, 16, 1030
+    x = _rand(B * F, D + 3, seed=9).to(DEV)
+    out = torch.empty(B, D, device=DEV)
+    hip.lib().call('srnn_segsum', hip.ptr(x), D + 3, B, F, D, hip.ptr(out), hip.stream())
+    ref = x[:, :D].reshape(B, F, D).sum(1)
+    torch.testing.assert_close(out, ref, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('M,N,K', [(128, 1024, 1024), (67, 256, 512), (128, 40, 256),
                                    (256, 2048, 256)])
 def test_gemm_skinny_ring(hip, dtype, M, N, K):
