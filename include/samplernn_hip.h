@@ -67,6 +67,18 @@ int srnn_gru_cell_bwd(int dtype, int B, int D, const float* dy, int64_t lddy,
                       const float* hprev, int64_t ldhp, float* dgh, int64_t lddgh, void* dgh_lp,
                       int64_t lddghl, float* dgi, int64_t lddgi, float* ddir, void* stream);
 
+/* Whole-sequence forward of one GRU layer in a single persistent launch (bf16, D <= 1024,
+ * D % 128 == 0, (D/16) * ceil(B/32) workgroups co-resident): out[b][t] / out_lp /
+ * gates[b][t] exactly as Fr calls of srnn_gru_cell with gi[b][t] = gi + b*ldgi + t*sgi.
+ * work: >= (64 * ceil(B/32) + 1) ints (zeroed by the call; the last word is an error flag
+ * raised if a workgroup gave up waiting).  srnn_gru_seq_supported returns 1 / 0.       */
+int srnn_gru_seq_supported(int dtype, int B, int D);
+int srnn_gru_seq_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
+                     int64_t sgi, const float* h0, const void* h0_lp, const void* whh,
+                     const float* bhh, float* out, void* out_lp, int64_t ldo, int64_t so,
+                     float* gates, int64_t ldg, int64_t sg, int* work, size_t work_bytes,
+                     void* stream);
+
 /* ---- SampleLevelMLP (model.py:308-325) ----------------------------------------------
  * a1[b*Tlen+t] = relu(sum_k tab[k][x[b*ldx + xoff + t + k]] + upper[b*Tlen+t])
  * tab / out in `dtype`; upper in `upper_dtype` (SRNN_F32 or SRNN_BF16)                  */

@@ -58,6 +58,8 @@ _SIGS = {
     'srnn_colsum': [_I, _P, _L, _L, _I, _P, _F, _I, _P, _L, _P],
     'srnn_adam_clip': [_P, _P, _P, _P, _P, _L, _F, _F, _D, _D, _D, _D, _L, _P],
     'srnn_adam_clip_multi': [_I, _P, _P, _P, _P, _P, _P, _F, _F, _D, _D, _D, _D, _L, _P],
+    'srnn_gru_seq_fwd': [_I, _I, _I, _I, _P, _L, _L, _P, _P, _P, _P, _P, _P, _L, _L, _P, _L, _L,
+                         _P, _SZ, _P],
     'srnn_gen_workspace_size': [_P, _I, ctypes.POINTER(_SZ)],
     'srnn_generate': [_P, _I, _I, _P, _P, _P, _U64, _P, _P, _P, _SZ, _I, _P],
 }
@@ -109,7 +111,24 @@ def lib():
 
 
 def exported_symbols():
-    return sorted(_SIGS) + ['srnn_last_error', 'srnn_abi_version']
+    return sorted(_SIGS) + ['srnn_last_error', 'srnn_abi_version', 'srnn_gru_seq_supported']
+
+
+_GRU_SEQ = {}
+
+
+def gru_seq_supported(dtype, B, D):
+    """Whether the persistent whole-sequence GRU kernel can run (B, D) here (queried once;
+    SRNN_GRU_SEQ=0 disables it)."""
+    if os.environ.get('SRNN_GRU_SEQ', '1') == '0':
+        return False
+    key = (dtype, B, D)
+    if key not in _GRU_SEQ:
+        fn = lib().dll.srnn_gru_seq_supported
+        fn.argtypes = [_I, _I, _I]
+        fn.restype = _I
+        _GRU_SEQ[key] = bool(fn(dcode(dtype), B, D))
+    return _GRU_SEQ[key]
 
 
 # ------------------------------------------------------------------ helpers

@@ -123,6 +123,45 @@ def test_gemm_thin_small_k(hip, dtype, odt, M, N, K):
     torch.testing.assert_close(out.float().cpu(), ref, atol=tol, rtol=tol)
 
 
+@pytest.mark.parametrize('B,D,Fr', [(128, 1024, 16), (64, 1024, 5), (100, 256, 9)])
+def test_gru_seq_fwd_matches_steps(hip, B, D, Fr):
+    """Persistent whole-sequence GRU forward == Fr per-step cell launches, bit for bit."""
+    T = torch.bfloat16
+    if not hip.gru_seq_supported(T, B, D):
+        pytest.skip('persistent GRU not supported on this device')
+    g = torch.Generator().manual_seed(B + D)
+    whh = (torch.randn(3 * D, D, generator=g) * 0.03).to(DEV, T)
+    bhh = (torch.randn(3 * D, generator=g) * 0.1).to(DEV)
+    gi = (torch.randn(B * Fr, 3 * D, generator=g) * 0.5).to(DEV)
+    h0 = (torch.randn(B, D, generator=g) * 0.5).to(DEV)
+    h0T = h0.to(T)
+    outs = {}
+    for mode in ('seq', 'steps'):
+        out = torch.full((B, Fr, D), float('nan'), device=DEV)
+        outT = torch.zeros((B, Fr, D), device=DEV, dtype=T)
+        gt = torch.full((B, Fr, 4 * D), float('nan'), device=DEV)
+        if mode == 'seq':
+            nw = 64 * ((B + 31) // 32) + 1
+            work = torch.full((nw,), 7, device=DEV, dtype=torch.int32)
+            hip.lib().call('srnn_gru_seq_fwd', hip.BF16, B, D, Fr, hip.ptr(gi), Fr * 3 * D, 3 * D,
+                           hip.ptr(h0), hip.ptr(h0T), hip.ptr(whh), hip.ptr(bhh), hip.ptr(out),
+                           hip.ptr(outT), Fr * D, D, hip.ptr(gt), Fr * 4 * D, 4 * D,
+                           hip.ptr(work), work.numel() * 4, hip.stream())
+            torch.cuda.synchronize()
+            assert int(work[nw - 1]) == 0, 'persistent GRU gave up waiting'
+        else:
+            for t in range(Fr):
+                hp_t, hp_f, ldh = (h0T, h0, D) if t == 0 else (outT[:, t - 1], out[:, t - 1], Fr * D)
+                hip.lib().call('srnn_gru_cell', hip.BF16, B, D, D, None, 0, None, None,
+                               hip.ptr(gi[t:]), Fr * 3 * D, hip.ptr(hp_t), ldh, hip.ptr(hp_f), ldh,
+                               hip.ptr(whh), hip.ptr(bhh), hip.ptr(out[:, t]), Fr * D,
+                               hip.ptr(outT[:, t]), Fr * D, hip.ptr(gt[:, t]), Fr * 4 * D,
+                               hip.stream())
+        outs[mode] = (out.cpu(), outT.float().cpu(), gt.cpu())
+    for a, b in zip(outs['seq'], outs['steps']):
+        assert torch.equal(a, b)
+
+
 def test_segsum(hip):
     B, F, D = 7, 16, 1030
     x = _rand(B * F, D + 3, seed=9).to(DEV)
