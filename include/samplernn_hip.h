@@ -78,6 +78,14 @@ int srnn_gru_seq_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t l
                      const float* bhh, float* out, void* out_lp, int64_t ldo, int64_t so,
                      float* gates, int64_t ldg, int64_t sg, int* work, size_t work_bytes,
                      void* stream);
+/* Whole-sequence backward of one GRU layer (t = Fr-1 .. 0) in one persistent launch:
+ * the Fr calls of srnn_gru_cell_bwd, with dh_direct kept on chip; ddir0 receives the
+ * dh_direct of step 0.  dgh / dgh_lp / dgi share the row stride ldd and step stride sd.  */
+int srnn_gru_seq_bwd(int dtype, int B, int D, int Fr, const float* dy, int64_t lddy,
+                     int64_t sdy, const float* gates, int64_t ldg, int64_t sg, const float* hout,
+                     int64_t ldo, int64_t so, const float* h0, const void* whh_t, float* dgh,
+                     void* dgh_lp, float* dgi, int64_t ldd, int64_t sd, float* ddir0, int* work,
+                     size_t work_bytes, void* stream);
 
 /* ---- SampleLevelMLP (model.py:308-325) ----------------------------------------------
  * a1[b*Tlen+t] = relu(sum_k tab[k][x[b*ldx + xoff + t + k]] + upper[b*Tlen+t])

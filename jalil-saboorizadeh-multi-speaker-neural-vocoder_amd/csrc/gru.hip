@@ -11,6 +11,7 @@
 // backward in the epilogue.
 #include "gemm_core.hpp"
 #include "ring_core.hpp"
+#include "gru_point.hpp"
 #include "samplernn_hip_internal.hpp"
 
 // ring depth of the per-step GRU kernels: 8 slots (7 k-stages in flight) fit the 160 KiB
@@ -242,13 +243,8 @@ __device__ __forceinline__ void gru_bwd_epilogue(const GruBwdArgs& a, int row, i
     const float* g = a.gates + (int64_t)row * a.ldgt;
     const float r = g[u], z = g[D + u], n = g[2 * D + u], ghn = g[3 * D + u];
     const float hp = a.hprev[(int64_t)row * a.ldhp + u];
-    const float dn = dh * (1.0f - z);
-    const float dz = dh * (hp - n);
-    const float dan = dn * (1.0f - n * n);
-    const float dr = dan * ghn;
-    const float dar = dr * r * (1.0f - r);
-    const float daz = dz * z * (1.0f - z);
-    const float dghn = dan * r;
+    const GruBwdPoint o = gru_bwd_point(dh, r, z, n, ghn, hp);
+    const float dar = o.dar, daz = o.daz, dghn = o.dghn, dan = o.dan;
     float* dgh = a.dgh + (int64_t)row * a.lddgh;
     dgh[u] = dar; dgh[D + u] = daz; dgh[2 * D + u] = dghn;
     if (a.dgh_lp) {
@@ -257,7 +253,7 @@ __device__ __forceinline__ void gru_bwd_epilogue(const GruBwdArgs& a, int row, i
     }
     float* dgi = a.dgi + (int64_t)row * a.lddgi;
     dgi[u] = dar; dgi[D + u] = daz; dgi[2 * D + u] = dan;
-    a.ddir[(int64_t)row * D + u] = dh * z;
+    a.ddir[(int64_t)row * D + u] = o.ddir;
 }
 
 template <typename T, int BM>

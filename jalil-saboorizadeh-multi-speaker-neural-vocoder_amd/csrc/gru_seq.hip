@@ -13,6 +13,7 @@
 // The arithmetic (fragment order, k split over waves, reduction, gate epilogue) is the
 // per-step ring kernel's, so both paths give identical bits.
 #include "ring_core.hpp"
+#include "gru_point.hpp"
 #include "samplernn_hip_internal.hpp"
 
 namespace gseq {
@@ -201,6 +202,154 @@ __global__ __launch_bounds__(256, 1) void gru_seq_fwd_kernel(GruSeqArgs a) {
     }
 }
 
+// ------------------------------------------------------------------ backward
+// Reverse sweep of one layer (gru.hip's backward step, t = Fr-1 .. 0):
+//   dh_t = dy_t + ddir_{t+1} + dgh_{t+1} . W_hh,  then the gate backward.
+// Workgroup (unit tile, row tile) keeps W_hh^T[u0:u0+16, :] (16 x 3D bf16 = 96 KiB)
+// resident; per step the 32 rows x 3D of dgh_{t+1} of its row tile stream through an
+// 8-slot ring (64 KiB).  dh_direct (= dh z) stays in registers between steps.  The
+// hand-off is the forward's: write-through bf16 dgh, per-tile step flags.
+namespace gseqb {
+constexpr int BM = 32, BN = 16, WM = 2, WN = 1, WK = 2, NS = 8;
+typedef Ring<bf16, BM, BN, WM, WN, WK, NS> R;
+constexpr int MAXK = 3072;                         // 3D for D <= 1024
+constexpr int NSTAGE = MAXK / R::KB;               // 24
+constexpr int WIMG = BN * R::KSB * NSTAGE;         // 96 KiB
+constexpr int LDS = WIMG + NS * BM * R::KSB;       // + 64 KiB ring
+}  // namespace gseqb
+
+struct GruSeqBwdArgs {
+    const float* dy; int64_t lddy; int64_t sdy;          // dy[b][t] (D)
+    const float* gates; int64_t ldg; int64_t sg;         // forward gates r|z|n|ghn
+    const float* hout; int64_t ldo; int64_t so;          // forward h_t (fp32) for h_{t-1}
+    const float* h0;                                     // (B, D) initial state
+    const bf16* whh_t;                                   // (D, 3D)
+    float* dgh; bf16* dgh_lp; float* dgi; int64_t ldd; int64_t sd;   // (3D per row/step)
+    float* ddir0;                                        // (B, D): dh_direct of step 0
+    int* flags; int* err;
+    int B, D, Fr;
+};
+
+__global__ __launch_bounds__(256, 1) void gru_seq_bwd_kernel(GruSeqBwdArgs a) {
+    using namespace gseqb;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* wimg = smem;
+    char* ring = smem + WIMG;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wm = wave % WM, wk = wave / (WM * WN);
+    const int u0 = blockIdx.x * 16, m0 = blockIdx.y * BM;
+    const int D = a.D, K3 = 3 * D, nk = K3 / R::KB;
+    const int nunits = gridDim.x;
+    const RowClamp wmap{u0, D};
+    const RowClamp hmap{m0, a.B};
+    for (int s = 0; s < nk; ++s)
+        rc_issue<bf16, BN, R::IB>(a.whh_t, K3, wmap, s * R::KB, wimg + s * BN * R::KSB, wave,
+                                  lane);
+    const int lr = lane & 15, lh = lane >> 4;
+    const int u = u0 + lr;
+    const bool epi = wk == 0 && u < D;
+    float ddir[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int t = a.Fr - 1; t >= 0; --t) {
+        const bool has_next = t + 1 < a.Fr;
+        // epilogue operands first (older than the ring pieces in the vmcnt queue)
+        float dyv[4], gr[4], gz[4], gn[4], gg[4], hp[4];
+        if (epi) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = min(m0 + wm * 16 + lh * 4 + i, a.B - 1);
+                dyv[i] = a.dy[(int64_t)row * a.lddy + (int64_t)t * a.sdy + u];
+                const float* g = a.gates + (int64_t)row * a.ldg + (int64_t)t * a.sg;
+                gr[i] = g[u]; gz[i] = g[D + u]; gn[i] = g[2 * D + u]; gg[i] = g[3 * D + u];
+                hp[i] = t > 0 ? a.hout[(int64_t)row * a.ldo + (int64_t)(t - 1) * a.so + u]
+                              : a.h0[(int64_t)row * D + u];
+            }
+        }
+        floatx4 acc[1][1];
+        acc[0][0] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (has_next) {
+            if (!gseq_wait_flags(a.flags + blockIdx.y * 64, nunits, a.Fr - 1 - t, a.err, lane))
+                return;
+            const bf16* src = a.dgh_lp + (int64_t)(t + 1) * a.sd;
+            auto issue = [&](int kt) {
+                char* slot = ring + (kt % NS) * BM * R::KSB;
+                const int k0 = kt * R::KB;
+#pragma unroll
+                for (int i = 0; i < R::IA; ++i) {
+                    const int c = wave * R::IA + i;
+                    const int row = c * 4 + (lane >> 4);
+                    const int sl = (lane & 15) ^ (row & 15);
+                    const bf16* p = src + (int64_t)hmap(row) * a.ldd + k0 + sl * 8;
+                    __builtin_amdgcn_global_load_lds(RC_GLB(p), RC_LDS(slot + c * 1024), 16, 0,
+                                                     16 /*sc1*/);
+                }
+            };
+#pragma unroll
+            for (int st = 0; st < NS - 1; ++st)
+                if (st < nk) issue(st);
+            for (int kt = 0; kt < nk; ++kt) {
+                rc_wait_sel<R::IA, NS - 2>(nk - 1 - kt);
+                __builtin_amdgcn_s_barrier();
+                if (kt + NS - 1 < nk) issue(kt + NS - 1);
+                const char* ia = ring + (kt % NS) * BM * R::KSB;
+                const char* ib = wimg + kt * BN * R::KSB;
+#pragma unroll
+                for (int j = 0; j < R::UPW; ++j) {
+                    const int uu = wk + WK * j;
+                    const int ra = wm * 16 + lr;
+                    const bf16x8 av = *reinterpret_cast<const bf16x8*>(
+                        ia + ra * R::KSB + (((uu * 4 + lh) ^ (ra & 15)) * 16));
+                    const int rb = lr;
+                    const bf16x8 bv = *reinterpret_cast<const bf16x8*>(
+                        ib + rb * R::KSB + (((uu * 4 + lh) ^ (rb & 15)) * 16));
+                    Mma<bf16>::run(acc[0][0], av, bv);
+                }
+            }
+            __syncthreads();                   // ring free: reused by the reduction
+            ring_reduce<bf16, BM, BN, WM, WN, WK, NS>(ring, acc);
+        } else {
+            // first backward step: nothing to wait for, but the resident W_hh^T pieces must
+            // have landed before any later step reads them (the ring waits cover them then)
+        }
+        float o_dar[4], o_daz[4], o_dghn[4], o_dan[4];
+        if (epi) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float dh = acc[0][0][i] + dyv[i];
+                if (has_next) dh += ddir[i];
+                const float r = gr[i], z = gz[i], n = gn[i], ghn = gg[i];
+                const GruBwdPoint o = gru_bwd_point(dh, r, z, n, ghn, hp[i]);
+                const float dar = o.dar, daz = o.daz, dghn = o.dghn, dan = o.dan;
+                ddir[i] = o.ddir;
+                o_dar[i] = dar; o_daz[i] = daz; o_dghn[i] = dghn; o_dan[i] = dan;
+                const int row = m0 + wm * 16 + lh * 4 + i;
+                if (row < a.B) {      // the row tile's previous step reads these first
+                    bf16* dl = a.dgh_lp + (int64_t)row * a.ldd + (int64_t)t * a.sd;
+                    gseq_store_wt(dl + u, from_f<bf16>(dar));
+                    gseq_store_wt(dl + D + u, from_f<bf16>(daz));
+                    gseq_store_wt(dl + 2 * D + u, from_f<bf16>(dghn));
+                }
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0)
+            __hip_atomic_store(a.flags + blockIdx.y * 64 + blockIdx.x, a.Fr - t, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (epi) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int row = m0 + wm * 16 + lh * 4 + i;
+                if (row >= a.B) continue;
+                float* dg = a.dgh + (int64_t)row * a.ldd + (int64_t)t * a.sd;
+                dg[u] = o_dar[i]; dg[D + u] = o_daz[i]; dg[2 * D + u] = o_dghn[i];
+                float* di = a.dgi + (int64_t)row * a.ldd + (int64_t)t * a.sd;
+                di[u] = o_dar[i]; di[D + u] = o_daz[i]; di[2 * D + u] = o_dan[i];
+                if (t == 0) a.ddir0[(int64_t)row * D + u] = ddir[i];
+            }
+        }
+    }
+}
+
 static int g_ncu = 0;
 
 // 1 if the persistent path can run this shape on this device, else 0
@@ -214,6 +363,41 @@ extern "C" int srnn_gru_seq_supported(int dtype, int B, int D) {
     }
     // every workgroup must be co-resident (one per CU: 160 KiB LDS each); <= 64 unit tiles
     return D / 16 <= 64 && (int64_t)(D / 16) * cdiv(B, gseq::BM) <= g_ncu ? 1 : 0;
+}
+
+extern "C" int srnn_gru_seq_bwd(int dtype, int B, int D, int Fr, const float* dy, int64_t lddy,
+                                int64_t sdy, const float* gates, int64_t ldg, int64_t sg,
+                                const float* hout, int64_t ldo, int64_t so, const float* h0,
+                                const void* whh_t, float* dgh, void* dgh_lp, float* dgi,
+                                int64_t ldd, int64_t sd, float* ddir0, int* work,
+                                size_t work_bytes, void* stream) {
+    SRNN_REQUIRE(srnn_gru_seq_supported(dtype, B, D), "gru_seq: shape/device not supported");
+    SRNN_REQUIRE(3 * D <= gseqb::MAXK && (3 * D) % gseqb::R::KB == 0, "gru_seq_bwd: D");
+    const int nm = cdiv(B, gseqb::BM);
+    const size_t words = (size_t)nm * 64 + 1;
+    SRNN_REQUIRE(work && work_bytes >= words * sizeof(int), "gru_seq_bwd: workspace");
+    if (Fr <= 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    SRNN_CHECK_HIP(hipMemsetAsync(work, 0, words * sizeof(int), s));
+    static bool attr = false;
+    if (!attr) {
+        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)gru_seq_bwd_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           gseqb::LDS));
+        attr = true;
+    }
+    GruSeqBwdArgs a;
+    a.dy = dy; a.lddy = lddy; a.sdy = sdy;
+    a.gates = gates; a.ldg = ldg; a.sg = sg;
+    a.hout = hout; a.ldo = ldo; a.so = so; a.h0 = h0;
+    a.whh_t = (const bf16*)whh_t;
+    a.dgh = dgh; a.dgh_lp = (bf16*)dgh_lp; a.dgi = dgi; a.ldd = ldd; a.sd = sd;
+    a.ddir0 = ddir0;
+    a.flags = work; a.err = work + (size_t)nm * 64;
+    a.B = B; a.D = D; a.Fr = Fr;
+    hipLaunchKernelGGL(gru_seq_bwd_kernel, dim3(D / 16, nm), dim3(256), gseqb::LDS, s, a);
+    SRNN_LAUNCH_CHECK();
+    return 0;
 }
 
 extern "C" int srnn_gru_seq_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,

@@ -332,7 +332,17 @@ class _TierFn(torch.autograd.Function):
             ddir = [torch.empty((B, D), device=dev, dtype=torch.float32) for _ in range(2)]
             # W_hh^T (D, 3D): k-contiguous operand for the deep-ring backward kernel
             WhhT = H.permute3(Whh[l].float().reshape(1, 3 * D, D), (0, 2, 1), dtype=T)
-            for t in reversed(range(Fr)):
+            seq = lp and H.gru_seq_supported(T, B, D)
+            if seq:
+                # the whole reverse sweep in one persistent launch (W_hh^T resident in LDS)
+                work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
+                dOutc = dOut.contiguous()
+                H.lib().call('srnn_gru_seq_bwd', H.dcode(T), B, D, Fr, H.ptr(dOutc), Fr * D, D,
+                             H.ptr(gates[l]), Fr * 4 * D, 4 * D, H.ptr(outs[l]), Fr * D, D,
+                             H.ptr(h_in[l]), H.ptr(WhhT), H.ptr(dGH), H.ptr(dGHT), H.ptr(dGI),
+                             Fr * 3 * D, 3 * D, H.ptr(ddir[0]), H.ptr(work), work.numel() * 4,
+                             st())
+            for t in reversed(range(Fr)) if not seq else ():
                 nxt = t + 1 < Fr
                 if t > 0:
                     hp, ldhp = outs[l][:, t - 1], Fr * D

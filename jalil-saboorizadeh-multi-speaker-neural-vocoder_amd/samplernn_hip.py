@@ -60,6 +60,8 @@ _SIGS = {
     'srnn_adam_clip_multi': [_I, _P, _P, _P, _P, _P, _P, _F, _F, _D, _D, _D, _D, _L, _P],
     'srnn_gru_seq_fwd': [_I, _I, _I, _I, _P, _L, _L, _P, _P, _P, _P, _P, _P, _L, _L, _P, _L, _L,
                          _P, _SZ, _P],
+    'srnn_gru_seq_bwd': [_I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L, _P, _P, _P, _P, _P,
+                         _L, _L, _P, _P, _SZ, _P],
     'srnn_gen_workspace_size': [_P, _I, ctypes.POINTER(_SZ)],
     'srnn_generate': [_P, _I, _I, _P, _P, _P, _U64, _P, _P, _P, _SZ, _I, _P],
 }

@@ -162,6 +162,63 @@ def test_gru_seq_fwd_matches_steps(hip, B, D, Fr):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize('B,D,Fr', [(128, 1024, 16), (64, 1024, 5), (100, 256, 9)])
+def test_gru_seq_bwd_matches_steps(hip, B, D, Fr):
+    """Persistent whole-sequence GRU backward == Fr per-step backward launches, bit for bit."""
+    T = torch.bfloat16
+    if not hip.gru_seq_supported(T, B, D):
+        pytest.skip('persistent GRU not supported on this device')
+    g = torch.Generator().manual_seed(B * 7 + D)
+    whh = (torch.randn(3 * D, D, generator=g) * 0.03).to(DEV, T)
+    whhT = whh.t().contiguous()
+    # forward state from a real recurrence (per-step cells)
+    bhh = (torch.randn(3 * D, generator=g) * 0.1).to(DEV)
+    gi = (torch.randn(B * Fr, 3 * D, generator=g) * 0.5).to(DEV)
+    h0 = (torch.randn(B, D, generator=g) * 0.5).to(DEV)
+    h0T = h0.to(T)
+    out = torch.empty(B, Fr, D, device=DEV)
+    outT = torch.empty(B, Fr, D, device=DEV, dtype=T)
+    gt = torch.empty(B, Fr, 4 * D, device=DEV)
+    for t in range(Fr):
+        hp_t, hp_f, ldh = (h0T, h0, D) if t == 0 else (outT[:, t - 1], out[:, t - 1], Fr * D)
+        hip.lib().call('srnn_gru_cell', hip.BF16, B, D, D, None, 0, None, None, hip.ptr(gi[t:]),
+                       Fr * 3 * D, hip.ptr(hp_t), ldh, hip.ptr(hp_f), ldh, hip.ptr(whh),
+                       hip.ptr(bhh), hip.ptr(out[:, t]), Fr * D, hip.ptr(outT[:, t]), Fr * D,
+                       hip.ptr(gt[:, t]), Fr * 4 * D, hip.stream())
+    dy = (torch.randn(B, Fr, D, generator=g) * 0.1).to(DEV)
+    res = {}
+    for mode in ('seq', 'steps'):
+        dgh = torch.full((B, Fr, 3 * D), float('nan'), device=DEV)
+        dghT = torch.zeros((B, Fr, 3 * D), device=DEV, dtype=T)
+        dgi = torch.full((B, Fr, 3 * D), float('nan'), device=DEV)
+        ddir = [torch.zeros(B, D, device=DEV) for _ in range(2)]
+        if mode == 'seq':
+            nw = 64 * ((B + 31) // 32) + 1
+            work = torch.full((nw,), 7, device=DEV, dtype=torch.int32)
+            hip.lib().call('srnn_gru_seq_bwd', hip.BF16, B, D, Fr, hip.ptr(dy), Fr * D, D,
+                           hip.ptr(gt), Fr * 4 * D, 4 * D, hip.ptr(out), Fr * D, D, hip.ptr(h0),
+                           hip.ptr(whhT), hip.ptr(dgh), hip.ptr(dghT), hip.ptr(dgi), Fr * 3 * D,
+                           3 * D, hip.ptr(ddir[0]), hip.ptr(work), nw * 4, hip.stream())
+            torch.cuda.synchronize()
+            assert int(work[nw - 1]) == 0, 'persistent GRU backward gave up waiting'
+        else:
+            for t in reversed(range(Fr)):
+                nxt = t + 1 < Fr
+                hp, ldhp = (out[:, t - 1], Fr * D) if t > 0 else (h0, D)
+                hip.lib().call('srnn_gru_cell_bwd', hip.BF16, B, D, hip.ptr(dy[:, t]), Fr * D,
+                               hip.ptr(dghT[:, t + 1]) if nxt else None, Fr * 3 * D,
+                               hip.ptr(ddir[(t + 1) % 2]) if nxt else None, hip.ptr(whh),
+                               hip.ptr(whhT), hip.ptr(gt[:, t]), Fr * 4 * D, hip.ptr(hp), ldhp,
+                               hip.ptr(dgh[:, t]), Fr * 3 * D, hip.ptr(dghT[:, t]), Fr * 3 * D,
+                               hip.ptr(dgi[:, t]), Fr * 3 * D, hip.ptr(ddir[t % 2]),
+                               hip.stream())
+        res[mode] = (dgh.cpu(), dghT.float().cpu(), dgi.cpu(), ddir[0].cpu())
+    for name, a, b in zip(('dgh', 'dgh_lp', 'dgi', 'ddir0'), res['seq'], res['steps']):
+        bad = (a != b).nonzero()
+        assert bad.numel() == 0, (name, bad.shape[0], bad[:4].tolist(),
+                                  (a - b).abs().max().item())
+
+
 def test_segsum(hip):
     B, F, D = 7, 16, 1030
     x = _rand(B * F, D + 3, seed=9).to(DEV)
