@@ -9,8 +9,8 @@
 // opens each stage (counted s_waitcnt vmcnt, never a __syncthreads that would drain the
 // DMA queue).  LDS images (the global source addresses carry the swizzle, the DMA writes
 // lane-linear):
-//   k-contiguous operand   [256 rows][64 B]    16-B slot ^ ((row >> 2) & 3): the 16 lanes
-//                          of each ds_read_b128 pass hit 16 distinct bank quads;
+//   k-contiguous operand   [256 rows][64 B]    16-B slot ^ g3_kcswz(row): the 16 lanes
+//                          of each ds_read_b128 lane group hit 16 distinct bank quads;
 //   row-contiguous operand [32 k-rows][512 B]  16-B slot ^ (2*(k&3) + 8*((k>>3)&1)):
 //                          ds_read_b64_tr_b16 transposed reads, 32 distinct 8-B bank
 //                          slots per 32-lane pass.
@@ -37,6 +37,7 @@ struct Gemm3Args {
     int M, N, K, ksplit;
     float alpha, beta;
     int bias_mode, relu;
+    int diag;   // timing experiments (SRNN_G3DIAG): 1 no MFMA, 2 no DMA wait, 4 no DMA, 8 no epilogue
 };
 
 namespace g3 {
@@ -63,13 +64,19 @@ __device__ __forceinline__ void g3_wait_sel(int ahead) {
     }
 }
 
+// 16-B slot swizzle of a 64-B k-contiguous row: row block (r >> 2) -> 0, 2, 3, 1.  The
+// ds_read_b128 lane groups are {0-3,12-15,20-27}, {4-11,16-19,28-31} (+32): with this
+// permutation each group's 16 lanes hit 16 distinct 4-bank chunks (the plain
+// (r >> 2) & 3 puts two lanes on each chunk -- 8 LDS cycles per read instead of 4).
+__device__ __forceinline__ int g3_kcswz(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+
 // per-lane source of DMA piece c (1 KiB of the stage image) at k = k0
 template <bool KC>
 __device__ __forceinline__ const bf16* g3_src(const bf16* __restrict__ base, int64_t ld, int r0,
                                               int k0, int c, int lane) {
     if constexpr (KC) {
         const int row = c * 16 + (lane >> 2);
-        const int slot = (lane & 3) ^ ((row >> 2) & 3);
+        const int slot = (lane & 3) ^ g3_kcswz(row);
         return base + (int64_t)(r0 + row) * ld + k0 + slot * 8;
     } else {
         const int kr = c * 2 + (lane >> 5);
@@ -83,7 +90,7 @@ template <bool KC>
 __device__ __forceinline__ bf16x8 g3_frag(const char* img, int f0, int lane) {
     if constexpr (KC) {
         const int r = f0 + (lane & 15);
-        const int slot = (lane >> 4) ^ ((r >> 2) & 3);
+        const int slot = (lane >> 4) ^ g3_kcswz(r);
         return *reinterpret_cast<const bf16x8*>(img + r * 64 + slot * 16);
     } else {
         const int h = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
@@ -137,9 +144,9 @@ __device__ __forceinline__ void g3_store4(bf16* p, const float (&v)[4]) {
 // path, where a lane's 4 values are 4 rows of one column and each atomic instruction
 // covers 16 consecutive columns (64 B) of 4 rows instead of 16 rows x 4 B.
 // epilogue of one finished tile (registers -> C); zeroes the accumulators
-template <typename TO, bool SW>
-__device__ __forceinline__ void g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
-                                            int n0, int wm, int wn, int lane) {
+template <typename TO, bool SW, bool CIN>
+__device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
+                                              int n0, int wm, int wn, int lane) {
     if constexpr (!SW) {
         // plain fp32 partials: lane holds 4 rows x 1 column per fragment
         float* Cf = reinterpret_cast<float*>(g.C);
@@ -206,7 +213,7 @@ __device__ __forceinline__ void g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8
 #pragma unroll
                 for (int e = 0; e < 4; ++e) v[e] = g.alpha * acc[i][j][e];
                 acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-                if (g.beta != 0.f) {     // (no model GEMM on this path uses Cin)
+                if (CIN) {     // (no model GEMM on this path uses Cin)
                     float c[4];
                     g3_load4(g.Cin + (int64_t)row * g.ldcin + col, c);
 #pragma unroll
@@ -227,6 +234,16 @@ __device__ __forceinline__ void g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8
             }
         }
     }
+}
+
+// The Cin branch is resolved once per tile: a uniform branch inside the store loop makes
+// the compiler join its wait states with an s_waitcnt vmcnt(0) per fragment, which waits
+// for every store issued before it (32 serialised store round trips per tile).
+template <typename TO, bool SW>
+__device__ __forceinline__ void g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
+                                            int n0, int wm, int wn, int lane) {
+    if (SW && g.beta != 0.f) g3_epilogue_t<TO, SW, true>(g, acc, m0, n0, wm, wn, lane);
+    else g3_epilogue_t<TO, SW, false>(g, acc, m0, n0, wm, wn, lane);
 }
 
 // Persistent: workgroup w owns work units w, w + G, ... (unit = output tile x k-slice);
@@ -589,6 +606,311 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Ping-pong mode: the pair-mode LDS layout (64-deep stages, 2 x 64 KiB slots) with the
+// two waves of each SIMD working in opposite phases.  Waves 0-3 (X) and 4-7 (Y) each
+// alternate a LOAD segment (12 fragment reads of one 32-deep k-unit into registers) and
+// a COMPUTE segment (its 32 MFMAs of that unit), Y one segment behind X, so while one
+// wave of a SIMD keeps the matrix pipe busy its partner fetches its next operands:
+//      X:  L0 | C0 | L1 | C1 | L2 | ...
+//      Y:  -- | L0 | C0 | L1 | C1 | ...
+// with one raw s_barrier between segments.  X alone streams HBM -> LDS: in its LOAD
+// segment of a stage's first unit it issues all 16 DMA pieces (of 64) of the next stage
+// into the slot Y finished reading one segment earlier, and waits for them at the end of
+// its COMPUTE segment of the stage's second unit, three segments later.  A finished tile's
+// epilogue runs in the wave's next LOAD segment.
+template <typename TO, bool KCA, bool KCB, bool SW>
+__global__ __launch_bounds__(512, 1) void gemm3pp_kernel(Gemm3Args g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int grp = wave >> 2, wx = wave & 3;
+    const int ntm = g.M / g3::BM, ntn = g.N / g3::BN;
+    const int ntiles = ntm * ntn;
+    const int nunits = ntiles * g.ksplit;
+    const int G = gridDim.x;
+    const int nmine = (nunits - (int)blockIdx.x + G - 1) / G;
+    const int kslice = g.K / g.ksplit;
+    const int nk = kslice / g3p::BK;
+    const int S = nmine * nk;
+    const bf16* A = reinterpret_cast<const bf16*>(g.A);
+    const bf16* B = reinterpret_cast<const bf16*>(g.B);
+
+    auto unit = [&](int i, int& m0, int& n0, int& kbeg) {
+        const int v = (int)blockIdx.x + i * G;
+        const int z = v / ntiles;
+        const int t = g3_xcd_remap(v - z * ntiles, ntiles);
+        m0 = (t / ntn) * g3::BM;
+        n0 = (t % ntn) * g3::BN;
+        kbeg = z * kslice;
+    };
+
+    floatx4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    // X wave wx streams pieces c = 4 i + wx (i = 0..7) of each operand: pieces i and
+    // i + 2 share the source swizzle and sit 8 pieces (64 rows / 16 k-rows) apart
+    const int64_t stepA = KCA ? (int64_t)64 * g.lda : (int64_t)16 * g.lda;
+    const int64_t stepB = KCB ? (int64_t)64 * g.ldb : (int64_t)16 * g.ldb;
+    int iu = 0, kti = 0;
+    const bf16* srcA[2];
+    const bf16* srcB[2];
+    auto set_src = [&]() {
+        int m0, n0, kb;
+        unit(iu, m0, n0, kb);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int c = 4 * i + wx;
+            srcA[i] = g3p_src<KCA>(A, g.lda, m0, kb, c, lane);
+            srcB[i] = g3p_src<KCB>(B, g.ldb, n0, kb, c, lane);
+        }
+    };
+    auto koffA = [&](int kt) { return KCA ? (int64_t)kt * g3p::BK : (int64_t)kt * g3p::BK * g.lda; };
+    auto koffB = [&](int kt) { return KCB ? (int64_t)kt * g3p::BK : (int64_t)kt * g3p::BK * g.ldb; };
+    auto issue_stage = [&](char* img) {      // X waves only: 8 + 8 pieces of the next stage
+        const int64_t oa = koffA(kti), ob = koffB(kti);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            __builtin_amdgcn_global_load_lds(G3_GLB(srcA[i & 1] + oa + (i >> 1) * stepA),
+                                             G3_LDS(img + (4 * i + wx) * 1024), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            __builtin_amdgcn_global_load_lds(G3_GLB(srcB[i & 1] + ob + (i >> 1) * stepB),
+                                             G3_LDS(img + g3p::OPB + (4 * i + wx) * 1024), 16,
+                                             0, 0);
+        if (++kti == nk) {
+            kti = 0;
+            ++iu;
+            if (iu < nmine) set_src();
+        }
+    };
+    if (grp == 0) set_src();
+
+    bf16x8 a[8], b[4];
+    auto bar = []() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    // prologue: stage 0 resident before anyone reads
+    if (S > 0 && grp == 0) {
+        issue_stage(smem);
+        g3_wait_vm<0>();
+    }
+    bar();
+    if (grp == 1) bar();                     // Y runs one segment behind
+    int ic = 0, ktc = 0;
+    bool epi = false;
+    const int U = 2 * S;
+    for (int u = 0; u < U; ++u) {
+        const int st = u >> 1, h = u & 1;
+        const char* img = smem + (st & 1) * g3p::SLOT;
+        // ---- LOAD segment
+        if (epi) {
+            int m0, n0, kb;
+            unit(ic - 1, m0, n0, kb);
+            if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+            epi = false;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) b[j] = g3p_frag<KCB>(img + g3p::OPB, wn * 64 + j * 16, h, lane);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) a[i] = g3p_frag<KCA>(img, wm * 128 + i * 16, h, lane);
+        if (grp == 0 && h == 0 && st + 1 < S && !(g.diag & 4))
+            issue_stage(smem + ((st + 1) & 1) * g3p::SLOT);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        bar();
+        // ---- COMPUTE segment
+        __builtin_amdgcn_s_setprio(1);
+        if (!(g.diag & 1)) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0)
+                                   : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j][0] += (float)a[i][0] * (float)b[j][0];
+        }
+        __builtin_amdgcn_s_setprio(0);
+        if (h == 1) {
+            if (++ktc == nk) {
+                ktc = 0;
+                ++ic;
+                epi = true;
+            }
+            // X: the next stage's DMA (issued three segments ago) lands before Y and X read it
+            if (grp == 0 && !(g.diag & 2)) g3_wait_vm<0>();
+        }
+        bar();
+    }
+    if (grp == 0) bar();
+    if (epi) {
+        int m0, n0, kb;
+        unit(ic - 1, m0, n0, kb);
+        g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Ping-pong over the 32-deep ring (mode 4): the LOAD / COMPUTE alternation of the
+// ping-pong kernel on the 5-slot ring of 32-deep stages, so the DMA can be spread: every
+// wave issues its 4 pieces of stage u + NS - 1 in its LOAD segment of unit u (into the
+// slot Y finished reading one segment earlier), and waits, counted, for stage v at the end
+// of the segment before X reads it (X: its COMPUTE of v - 1; Y: its LOAD of v - 1).
+template <typename TO, bool KCA, bool KCB, bool SW>
+__global__ __launch_bounds__(512, 1) void gemm3q_kernel(Gemm3Args g) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int wm = wave & 1, wn = wave >> 1;
+    const int grp = wave >> 2;
+    const int ntm = g.M / g3::BM, ntn = g.N / g3::BN;
+    const int ntiles = ntm * ntn;
+    const int nunits = ntiles * g.ksplit;
+    const int G = gridDim.x;
+    const int nmine = (nunits - (int)blockIdx.x + G - 1) / G;
+    const int kslice = g.K / g.ksplit;
+    const int nk = kslice / g3::BK;
+    const int S = nmine * nk;
+    const bf16* A = reinterpret_cast<const bf16*>(g.A);
+    const bf16* B = reinterpret_cast<const bf16*>(g.B);
+    (void)ntm;
+
+    auto unit = [&](int i, int& m0, int& n0, int& kbeg) {
+        const int v = (int)blockIdx.x + i * G;
+        const int z = v / ntiles;
+        const int t = g3_xcd_remap(v - z * ntiles, ntiles);
+        m0 = (t / ntn) * g3::BM;
+        n0 = (t % ntn) * g3::BN;
+        kbeg = z * kslice;
+    };
+
+    floatx4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    int iu = 0, kti = 0, isl = 0;        // issue cursor: unit, stage in unit, ring slot
+    const bf16* srcA[g3::GLW];
+    const bf16* srcB[g3::GLW];
+    auto set_src = [&]() {
+        int m0, n0, kb;
+        unit(iu, m0, n0, kb);
+#pragma unroll
+        for (int i = 0; i < g3::GLW; ++i) {
+            const int c = wave * g3::GLW + i;
+            srcA[i] = g3_src<KCA>(A, g.lda, m0, kb, c, lane);
+            srcB[i] = g3_src<KCB>(B, g.ldb, n0, kb, c, lane);
+        }
+    };
+    set_src();
+    auto issue_stage = [&]() {
+        char* img = smem + isl * g3::SLOT;
+        const int64_t oa = KCA ? (int64_t)kti * g3::BK : (int64_t)kti * g3::BK * g.lda;
+        const int64_t ob = KCB ? (int64_t)kti * g3::BK : (int64_t)kti * g3::BK * g.ldb;
+#pragma unroll
+        for (int i = 0; i < g3::GLW; ++i)
+            __builtin_amdgcn_global_load_lds(G3_GLB(srcA[i] + oa),
+                                             G3_LDS(img + (wave * g3::GLW + i) * 1024), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < g3::GLW; ++i)
+            __builtin_amdgcn_global_load_lds(G3_GLB(srcB[i] + ob),
+                                             G3_LDS(img + g3::OPB + (wave * g3::GLW + i) * 1024),
+                                             16, 0, 0);
+        isl = isl == g3::NS - 1 ? 0 : isl + 1;
+        if (++kti == nk) {
+            kti = 0;
+            ++iu;
+            if (iu < nmine) set_src();
+        }
+    };
+    constexpr int PER = 2 * g3::GLW;
+    int issued = 0;                      // stages issued so far
+#pragma unroll
+    for (int st = 0; st < g3::NS - 1; ++st)
+        if (st < S) {
+            issue_stage();
+            ++issued;
+        }
+    // wait until stage v of this wave has landed (stages > v may stay in flight)
+    auto wait_stage = [&](int v) {
+        if (!(g.diag & 2)) g3_wait_sel<PER, g3::NS - 2>(issued - 1 - v);
+    };
+
+    bf16x8 a[8], b[4];
+    auto bar = []() {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    if (S > 0) wait_stage(0);
+    bar();                                 // stage 0 resident
+    if (grp == 1) bar();                   // Y runs one segment behind
+    int ic = 0, ktc = 0, rsl = 0;
+    bool epi = false;
+    for (int u = 0; u < S; ++u) {
+        // ---- LOAD segment of unit u
+        if (epi) {
+            int m0, n0, kb;
+            unit(ic - 1, m0, n0, kb);
+            if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+            epi = false;
+        }
+        {
+            const char* ia = smem + rsl * g3::SLOT;
+            const char* ib = ia + g3::OPB;
+            rsl = rsl == g3::NS - 1 ? 0 : rsl + 1;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[j] = g3_frag<KCB>(ib, wn * 64 + j * 16, lane);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) a[i] = g3_frag<KCA>(ia, wm * 128 + i * 16, lane);
+        }
+        if (issued < S && !(g.diag & 4)) {   // stage u + NS - 1 into the slot of u - 1
+            issue_stage();
+            ++issued;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (grp == 1 && u + 1 < S) wait_stage(u + 1);  // Y: before X's LOAD of u + 1
+        bar();
+        // ---- COMPUTE segment of unit u
+        __builtin_amdgcn_s_setprio(1);
+        if (!(g.diag & 1)) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0)
+                                   : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[i][j][0] += (float)a[i][0] * (float)b[j][0];
+        }
+        __builtin_amdgcn_s_setprio(0);
+        if (++ktc == nk) {
+            ktc = 0;
+            ++ic;
+            epi = true;
+        }
+        if (grp == 0 && u + 1 < S) wait_stage(u + 1);  // X: before its LOAD of u + 1
+        bar();
+    }
+    if (grp == 0) bar();
+    if (epi) {
+        int m0, n0, kb;
+        unit(ic - 1, m0, n0, kb);
+        if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+    }
+}
+
 static int g3_mode() {
     static int v = -1;
     if (v < 0) {
@@ -603,14 +925,20 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
     // mode 0: 32-deep 5-slot ring; 1: 64-deep pair mode; 2 (default): pair mode when an
     // operand is k-contiguous (full-line DMA pieces), the ring otherwise
     const int mode = g3_mode();
-    const bool pair = (mode == 1 || (mode == 2 && (KCA || KCB))) && (g.K / g.ksplit) % g3p::BK == 0;
-    auto k = pair ? gemm3p_kernel<TO, KCA, KCB, SW> : gemm3_kernel<TO, KCA, KCB, SW>;
-    const int lds = pair ? g3p::LDS : g3::LDS;
-    static bool attr[2] = {false, false};
-    if (!attr[pair]) {
+    const bool k64 = (g.K / g.ksplit) % g3p::BK == 0;
+    const bool pp = mode == 3 && k64;
+    const bool q = mode == 4;
+    const bool pair = !pp && !q && (mode == 1 || (mode == 2 && (KCA || KCB))) && k64;
+    auto k = q ? gemm3q_kernel<TO, KCA, KCB, SW>
+               : pp ? gemm3pp_kernel<TO, KCA, KCB, SW>
+                    : pair ? gemm3p_kernel<TO, KCA, KCB, SW> : gemm3_kernel<TO, KCA, KCB, SW>;
+    const int lds = (pp || pair) ? g3p::LDS : g3::LDS;
+    const int ki = q ? 3 : pp ? 2 : pair ? 1 : 0;
+    static bool attr[4] = {false, false, false, false};
+    if (!attr[ki]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-        attr[pair] = true;
+        attr[ki] = true;
     }
     static int ncu = 0;
     if (!ncu) {
@@ -673,6 +1001,7 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     g.lda = lda; g.ldb = ldb; g.ldc = ldc; g.ldcin = ldcin; g.ldmask = ldmask;
     g.M = M; g.N = N; g.K = K; g.alpha = alpha; g.beta = beta;
     g.bias_mode = bias ? bias_mode : 0; g.relu = relu;
+    g.diag = env_flag("SRNN_G3DIAG", 0);
     const int tiles = (M / g3::BM) * (N / g3::BN);
     const bool plain = beta == 0.f && !bias && !relu && !mask && out_dtype == SRNN_F32;
     const int ks = plain ? g3_pick_split(tiles, K) : 1;

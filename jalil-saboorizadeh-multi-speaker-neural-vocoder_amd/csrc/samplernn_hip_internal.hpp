@@ -17,3 +17,9 @@ static inline int linear_fwd(int dt, int odt, int M, int N, int K, const void* x
     return srnn_gemm_impl(dt, odt, 0, 1, M, N, K, 1.f, x, ldx, 0, W, ldw, 0, beta, yin, ldyin, 0,
                           y, ldy, 0, bias, 1, relu, 1, -1, s);
 }
+
+// integer value of an environment switch (dflt when unset or empty)
+static inline int env_flag(const char* name, int dflt) {
+    const char* e = getenv(name);
+    return (e && *e) ? atoi(e) : dflt;
+}

@@ -95,9 +95,9 @@ def test_gemm3_256_kernel(hip, out_dtype, transA, transB, M, N, K, epi):
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('transA', [0, 1])
 @pytest.mark.parametrize('M,N,K', [(1024, 16, 8192), (1024, 43, 2048), (1000, 6, 128),
-                                   (128, 64, 1024), (300, 1, 5000)])
+                                   (128, 64, 1024), (300, 1, 5000), (1002, 5, 300)])
 def test_gemm_thin_small_n(hip, dtype, transA, M, N, K):
-    """Thin path (tile 6): N <= 64 weight gradients, split-K with atomics."""
+    """Thin path (tile 6): N <= 64 weight gradients, split-K (scratch partials or atomics)."""
     A = _rand(K, M, seed=1) if transA else _rand(M, K, seed=1)
     B = _rand(K, N, seed=2)
     Ad, Bd = A.to(DEV, dtype), B.to(DEV, dtype)
@@ -110,7 +110,8 @@ def test_gemm_thin_small_n(hip, dtype, transA, M, N, K):
 @pytest.mark.parametrize('dtype,odt', [(torch.float32, torch.float32),
                                        (torch.bfloat16, torch.float32),
                                        (torch.bfloat16, torch.bfloat16)])
-@pytest.mark.parametrize('M,N,K', [(8192, 1024, 16), (2048, 1024, 43), (300, 700, 64)])
+@pytest.mark.parametrize('M,N,K', [(8192, 1024, 16), (2048, 1024, 43), (300, 700, 64),
+                                   (260, 702, 7)])
 def test_gemm_thin_small_k(hip, dtype, odt, M, N, K):
     """Thin path (tile 6): K <= 64 input projections with Cin + bias (+ relu)."""
     A, W = _rand(M, K, seed=1), _rand(N, K, seed=2)

@@ -38,6 +38,17 @@ def run(M, N, K, tA, tB, dtype, out_dtype, tile, tag):
     print('%-34s tile=%2d %7.3f ms %8.1f TFLOP/s' % (tag, tile, ms, tf), flush=True)
 
 
+def run_torch(M, N, K, tA, tB, dtype, tag):
+    """the vendor library (hipBLASLt / rocBLAS through torch.mm) on the same shape, for scale"""
+    A = torch.randn(K, M, device=DEV).to(dtype) if tA else torch.randn(M, K, device=DEV).to(dtype)
+    B = torch.randn(N, K, device=DEV).to(dtype) if tB else torch.randn(K, N, device=DEV).to(dtype)
+    a = A.t() if tA else A
+    b = B.t() if tB else B
+    out = torch.empty(M, N, device=DEV, dtype=dtype)
+    ms = timeit(lambda: torch.mm(a, b, out=out))
+    print('%-34s torch   %7.3f ms %8.1f TFLOP/s' % (tag, ms, 2.0 * M * N * K / ms / 1e9), flush=True)
+
+
 if __name__ == '__main__':
     bf, f32 = torch.bfloat16, torch.float32
     shapes = [
@@ -58,6 +69,12 @@ if __name__ == '__main__':
         (16384, 1024, 8192, False, True, bf, f32, 'mlp hidden NT K8192'),
         (131072, 1024, 1024, True, False, bf, bf, 'mlp hidden TN bf16out'),
         (256, 1024, 131072, True, False, bf, f32, 'mlp out wgrad TN'),
+        (2048, 3072, 1024, False, True, bf, f32, 'top gi fwd NT'),
+        (2048, 4096, 1024, False, True, bf, f32, 'top upsample fwd NT'),
+        (2048, 1024, 4096, False, False, bf, f32, 'top upsample dgrad NN'),
+        (4096, 1024, 2048, True, False, bf, f32, 'top upsample wgrad TN'),
+        (3072, 1024, 2048, True, False, bf, f32, 'top gru wgrad TN'),
+        (8192, 1024, 3072, False, False, bf, f32, 'gru dgrad NN'),
     ]
     tiles = [int(t) for t in os.environ.get('TILES', '5,3').split(',')]
     only = os.environ.get('ONLY')
@@ -66,3 +83,5 @@ if __name__ == '__main__':
             continue
         for tile in tiles:
             run(M, N, K, tA, tB, dt, odt, tile, tag)
+        if os.environ.get('TORCHREF') == '1':
+            run_torch(M, N, K, tA, tB, dt, tag)
