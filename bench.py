@@ -150,6 +150,21 @@ def kernel_roofline_gemm(dev, M, N, K, dtype, reps=20):
     return ms
 
 
+def pmc_traffic(kernel, path=os.path.join(ROOT, 'profiles', 'r01_pmc_gemm.txt')):
+    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
+    (tools/roofline_kernel.py under --pmc FETCH_SIZE, then --pmc WRITE_SIZE): FETCH_SIZE kB x 2
+    (gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md HBM section) + WRITE_SIZE kB."""
+    try:
+        vals = {}
+        for line in open(path):
+            m = line.split()
+            if len(m) >= 6 and m[0] == 'avg':
+                vals[m[1]] = float(m[-1])
+        return int(round((2 * vals['FETCH_SIZE'] + vals['WRITE_SIZE']) * 1024))
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(seconds_budget=20.0):
     """The oracle (torch-CPU restatement of the reference) on the host cores: a bounded
     TBPTT sample of the same workload (config B dims, T = 1024, B = 4 rows)."""
@@ -245,7 +260,9 @@ def main():
     ach = flops / (kms * 1e-3) / 1e12
     peak = MI355X_BF16_TFLOPS if args.dtype == 'bf16' else MI355X_FP32_TFLOPS
     roof = {'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
-            'frac': round(ach / peak, 4), 'traffic': None,
+            'frac': round(ach / peak, 4),
+            'traffic': pmc_traffic('gemm3p_kernel') if args.dtype == 'bf16' else None,
+            'traffic_algorithmic': 2 * (M_ * K_ + N_ * K_ + M_ * N_),
             'kernel': 'gemm_kernel (MLP hidden layer %dx%dx%d %s, relu epilogue), %.3f ms/launch'
                       % (M_, N_, K_, args.dtype, kms)}
 
