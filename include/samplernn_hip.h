@@ -183,6 +183,10 @@ typedef struct SrnnModel {
     const float* b_out;
 } SrnnModel;
 
+/* Rows per group R (8 or 16) of the persistent generation sample loop (gen_mlp.hip) for this
+ * shape on this device, or 0 when srnn_generate will use per-sample kernels instead.
+ * Replaces nothing in the reference: a capability query for the Generator wrapper. */
+int srnn_gen_persistent_rows(int dtype, int n_seqs, int dim, int fs0, int q_levels);
 /* Workspace bytes needed by srnn_generate for n_seqs rows. */
 int srnn_gen_workspace_size(const SrnnModel* m, int n_seqs, size_t* bytes);
 /* Generates n_cond * lookback samples for n_seqs rows.
@@ -192,7 +196,10 @@ int srnn_gen_workspace_size(const SrnnModel* m, int n_seqs, size_t* bytes);
  *            draw q in-kernel from Philox4x32-10(seed)
  *   seq      (n_seqs, L + n_cond*L) int64, columns [0, L) pre-filled (q_zero); output
  *   logp     optional (n_cond*L, n_seqs, Q) fp32 per-step log-probs (debug / parity)
- *   flags    bit 0: replay the generation block as a hipGraph                           */
+ *   flags    bit 0: replay the generation block as a hipGraph
+ *            bit 1: per-sample kernels instead of the persistent sample loop (gen_mlp.hip,
+ *                   used by default where the shape fits; env SRNN_GEN_PERSIST=0 also
+ *                   disables it)                                                        */
 int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const float* cond,
                   const float* row_bias, const float* noise, uint64_t seed, int64_t* seq,
                   float* logp, void* workspace, size_t workspace_bytes, int flags, void* stream);

@@ -1,0 +1,450 @@
+// Persistent sample loop of autoregressive generation (Generator.__call__, model.py:496-518):
+// the SampleLevelMLP chain of FS0 consecutive samples (everything between two bottom-tier
+// ticks) in ONE launch.
+//
+// Per sample i and row b the chain is strictly sequential:
+//   a1 = relu(sum_k Tab[k][x_{i-FS0+k}] + up0[b][i % FS0])        (folded embedding . conv)
+//   a2 = relu(W_hid a1 + b_hid)                                   (D x D)
+//   z  = W_out a2 + b_out                                         (Q x D)
+//   x_i = argmax(exp(log_softmax(z)) / q),  q ~ Exp(1)             (multinomial, model.py:514)
+// The per-step kernel path (generate.hip) pays four dependent launches per sample.  Here:
+//
+// * Rows are split into groups of R (8 or 16) rows; the P = D / CW workgroups of a group
+//   (CW = 64 columns each, 16 groups x 16 workgroups = 256 at B = 128, D = 1024: one per CU)
+//   cooperate on that group only.  Workgroup p owns columns [p*CW, (p+1)*CW) of a1 and a2 and
+//   Q/P logits.  Groups are blocks b with equal b % G, i.e. one XCD under round-robin dealing
+//   (speed only; correctness never depends on placement).
+// * Weights never move during the loop: each wave keeps its K-slice of the W_hid and W_out
+//   columns of its workgroup as MFMA B fragments in VGPRs (64 + 16 VGPRs in bf16 at D = 1024),
+//   and the newest-tap table slice Tab[FS0-1][:, cols] sits in LDS, so the sample -> a1 step
+//   is an LDS gather.  The FS0-1 older taps + up0 are summed off the critical path while the
+//   previous step's exchanges are in flight.
+// * The three hand-offs per sample (a1, a2, z: every workgroup of the group needs every
+//   column) are data-tagged 8-byte granules {value, tag = sample index} written by single
+//   sc1 (write-through) stores and polled by sc1 loads (MI355X guide, Guideline 16 R2): no
+//   flags, fences or barriers; a consumer spins on the data itself.  A buffer is only
+//   rewritten after every consumer of its previous contents has produced a later result,
+//   so a single buffer per hand-off suffices (see the note at gen_mlp_kernel).
+// * Every workgroup of a group samples all R rows itself (the same logits, the same code:
+//   identical indices), so the sampled index needs no hand-off; workgroup 0 writes seq/logp.
+// * Spins are bounded: a lost hand-off sets the error word and the loop runs out instead of
+//   hanging.
+#include "samplernn_hip_internal.hpp"
+#include "sampler.hpp"
+#include "gen_mlp.hpp"
+
+namespace gm {
+constexpr int NW = 8;                  // waves per workgroup (the K split of both GEMMs)
+constexpr int NTHR = NW * 64;
+constexpr int Q = 256;
+constexpr int HIST = 32;               // sample history ring per row (FS0 <= 32)
+constexpr int SPIN_LIMIT = 1 << 20;    // polls (each >= one L2 round trip): ~ a second
+}  // namespace gm
+
+typedef unsigned long long u64;
+
+template <typename T> struct GmT;
+template <> struct GmT<bf16> {
+    static constexpr int GV = 2;       // values per granule
+    static constexpr int UK = 32;      // k elements per MFMA unit (64 bytes)
+    typedef bf16x8 frag;
+};
+template <> struct GmT<float> {
+    static constexpr int GV = 1;
+    static constexpr int UK = 16;
+    typedef floatx4 frag;
+};
+
+__device__ __forceinline__ void gm_put(u64* p, uint32_t tag, uint32_t v) {
+    __hip_atomic_store(p, ((u64)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ u64 gm_get(const u64* p) {
+    return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <typename F>
+__device__ __forceinline__ F gm_frag(uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    const uint4 u = make_uint4(a, b, c, d);
+    F f;
+    __builtin_memcpy(&f, &u, 16);
+    return f;
+}
+
+template <typename F>
+__device__ __forceinline__ F gm_load16(const void* p) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    F f;
+    __builtin_memcpy(&f, &u, 16);
+    return f;
+}
+
+template <typename T> __device__ __forceinline__ float gm_ld(const T* p) { return to_f(*p); }
+
+__device__ __forceinline__ uint32_t gm_bits(float v) { return __float_as_uint(v); }
+__device__ __forceinline__ uint32_t gm_bf16_bits(float v) {
+    return (uint32_t)__bfloat16_as_ushort(__float2bfloat16(v));
+}
+
+// Wait for granule tags: returns true once all equal `tag`; on timeout raises the error word.
+// Once the error word is set every later wait returns at its first re-check.
+__device__ __forceinline__ bool gm_spin_fail(int& spins, int* err, int lane) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > gm::SPIN_LIMIT) {
+        if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return true;
+    }
+    if ((spins & 31) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        return true;
+    return false;
+}
+
+// A-operand fragments of one wave for one hand-off buffer (granules of row `row`):
+// for unit j (global unit u = wave + NW*j) the lane's 16 data bytes = 4 granules.
+template <typename T, int UPW>
+__device__ __forceinline__ void gm_fetch_a(const u64* src, bool rv, int wave, int lane, int NU,
+                                           int D, uint32_t tag, uint32_t (&w)[UPW][4], int* err) {
+    constexpr int GV = GmT<T>::GV, UK = GmT<T>::UK, EPL = UK / 4;
+    int spins = 0;
+    for (;;) {
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < UPW; ++j) {
+            const int u = wave + gm::NW * j;
+            const int ke = u * UK + (lane >> 4) * EPL;
+            if (rv && u < NU && ke < D) {
+                const u64* s = src + ke / GV;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const u64 x = gm_get(s + e);
+                    w[j][e] = (uint32_t)x;
+                    ok &= (uint32_t)(x >> 32) == tag;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e) w[j][e] = 0u;
+            }
+        }
+        if (__all(ok)) return;
+        if (gm_spin_fail(spins, err, lane)) return;
+    }
+}
+
+// Note on single buffering: a1(i+1) is written only after its writer sampled x_i, i.e. after
+// it read every z(i) granule of its group; each of those was written after its producer had
+// read all of a2(i), which in turn came after every producer had read all of a1(i).  So when
+// any a1(i+1) granule lands, a1(i) has been consumed by everyone; the same chain covers a2
+// and z.  A consumer therefore only ever sees tag i-1 (keep polling) or tag i (done).
+template <typename T, int UPW, int NT, int NZT>
+__global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
+    using F = typename GmT<T>::frag;
+    constexpr int GV = GmT<T>::GV, UK = GmT<T>::UK, EPL = UK / 4;
+    constexpr int Q = gm::Q;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int D = a.D, R = a.R, CW = a.CW, NZ = a.NZ, FS0 = a.FS0, B = a.B;
+    const int g = blockIdx.x % a.G, p = blockIdx.x / a.G;
+    const int c0 = p * CW, z0 = p * NZ;
+    const int NU = (D + UK - 1) / UK;
+    const int KW = min(gm::NW, NU);
+    const int nt = CW / 16, nzt = NZ / 16, ntm = max(nt, nzt);
+    const int DG = D / GV;
+    const T* __restrict__ tab = (const T*)a.tab;
+    // LDS: [tab15 Q x CW][red KW x ntm x 64 floatx4][hist R x HIST]
+    T* tab15 = (T*)smem;
+    size_t lo = ((size_t)Q * CW * sizeof(T) + 15) & ~(size_t)15;
+    floatx4* red = (floatx4*)(smem + lo);
+    lo += (size_t)KW * ntm * 64 * sizeof(floatx4);
+    int* hist = (int*)(smem + lo);
+
+    // ---- resident weights: B fragments of this wave's K units
+    F wh[UPW][NT], wo[UPW][NZT];
+#pragma unroll
+    for (int j = 0; j < UPW; ++j) {
+        const int u = wave + gm::NW * j;
+        const int ke = u * UK + (lane >> 4) * EPL;
+        const bool kv = u < NU && ke < D;
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int n = c0 + t * 16 + (lane & 15);
+            wh[j][t] = (kv && t < nt) ? gm_load16<F>((const T*)a.w_hid + (int64_t)n * D + ke)
+                                      : gm_frag<F>(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int t = 0; t < NZT; ++t) {
+            const int n = z0 + t * 16 + (lane & 15);
+            wo[j][t] = (kv && t < nzt) ? gm_load16<F>((const T*)a.w_out + (int64_t)n * D + ke)
+                                       : gm_frag<F>(0u, 0u, 0u, 0u);
+        }
+    }
+    // ---- newest-tap table slice and the sample history of this group's rows
+    const int i0 = *a.base + a.off;
+    for (int e = tid; e < Q * CW; e += gm::NTHR) {
+        const int q = e / CW, c = e % CW;
+        tab15[e] = tab[((int64_t)(FS0 - 1) * Q + q) * D + c0 + c];
+    }
+    for (int e = tid; e < R * FS0; e += gm::NTHR) {
+        const int r = e / FS0, k = e % FS0;
+        const int b = min(g * R + r, B - 1);
+        const int j = i0 - FS0 + k;
+        hist[r * gm::HIST + (j & (gm::HIST - 1))] = (int)a.seq[(int64_t)b * a.ldseq + j];
+    }
+    float bh[2];
+    {
+        for (int s = 0; s < 2; ++s) {
+            const int e = tid + s * gm::NTHR;
+            bh[s] = e < R * CW ? a.b_hid[c0 + e % CW] : 0.f;
+        }
+    }
+    const float bo = tid < R * NZ ? a.b_out[z0 + tid % NZ] : 0.f;
+    __syncthreads();
+
+    // a1 pieces owned by this thread: e = tid + s*NTHR < R*CW  (r = e / CW, c = e % CW)
+    float part[2];
+    auto make_part = [&](int i) {
+        const int jpos = i % FS0;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int e = tid + s * gm::NTHR;
+            if (e >= R * CW) { part[s] = 0.f; continue; }
+            const int r = e / CW, c = e % CW;
+            const int b = min(g * R + r, B - 1);
+            float v = a.up0[(int64_t)b * a.ldup + (int64_t)jpos * D + c0 + c];
+            for (int k = 0; k < FS0 - 1; ++k) {
+                const int x = hist[r * gm::HIST + ((i - FS0 + k) & (gm::HIST - 1))];
+                v += gm_ld(tab + ((int64_t)k * Q + x) * D + c0 + c);
+            }
+            part[s] = v;
+        }
+    };
+    // publish a1(i) = relu(part + Tab[FS0-1][x_{i-1}]) as granules tagged i
+    auto publish_a1 = [&](int i) {
+        u64* dst = a.xa1 + (size_t)g * R * DG;
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+            const int e = tid + s * gm::NTHR;
+            if (s * gm::NTHR >= R * CW) break;                 // uniform
+            const bool act = e < R * CW;
+            const int r = act ? e / CW : 0, c = act ? e % CW : 0;
+            float v = 0.f;
+            if (act) {
+                const int x = hist[r * gm::HIST + ((i - 1) & (gm::HIST - 1))];
+                v = fmaxf(part[s] + to_f(tab15[x * CW + c]), 0.f);
+            }
+            if (GV == 2) {
+                const uint32_t mine = gm_bf16_bits(v);
+                const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
+                if (act && (c & 1) == 0) gm_put(dst + (size_t)r * DG + (c0 + c) / 2, i, mine | (nb << 16));
+            } else if (act) {
+                gm_put(dst + (size_t)r * DG + c0 + c, i, gm_bits(v));
+            }
+        }
+    };
+
+    make_part(i0);
+    publish_a1(i0);
+    if (a.nsteps > 1) make_part(i0 + 1);
+
+    const int row = lane & 15;
+    const bool rv = row < R;
+    for (int s = 0; s < a.nsteps; ++s) {
+        const int i = i0 + s;
+        const uint32_t tag = (uint32_t)i;
+        // ---------------- a2 = relu(W_hid a1 + b_hid), this workgroup's CW columns
+        {
+            floatx4 acc[NT];
+#pragma unroll
+            for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            if (wave < KW) {
+                uint32_t w[UPW][4];
+                gm_fetch_a<T, UPW>(a.xa1 + ((size_t)g * R + row) * DG, rv, wave, lane, NU, D, tag, w,
+                                   a.err);
+#pragma unroll
+                for (int j = 0; j < UPW; ++j) {
+                    const F af = gm_frag<F>(w[j][0], w[j][1], w[j][2], w[j][3]);
+#pragma unroll
+                    for (int t = 0; t < NT; ++t) Mma<T>::run(acc[t], af, wh[j][t]);
+                }
+#pragma unroll
+                for (int t = 0; t < NT; ++t)
+                    if (t < nt) red[(wave * ntm + t) * 64 + lane] = acc[t];
+            }
+            __syncthreads();
+            u64* dst = a.xa2 + (size_t)g * R * DG;
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                const int e = tid + s2 * gm::NTHR;
+                if (s2 * gm::NTHR >= R * CW) break;
+                const bool act = e < R * CW;
+                const int r = act ? e / CW : 0, c = act ? e % CW : 0;
+                const int t = c >> 4, ln = (r >> 2) * 16 + (c & 15), ii = r & 3;
+                float v = 0.f;
+                if (act) {
+                    for (int kw = 0; kw < KW; ++kw) v += red[(kw * ntm + t) * 64 + ln][ii];
+                    v = fmaxf(v + bh[s2], 0.f);
+                }
+                if (GV == 2) {
+                    const uint32_t mine = gm_bf16_bits(v);
+                    const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
+                    if (act && (c & 1) == 0)
+                        gm_put(dst + (size_t)r * DG + (c0 + c) / 2, tag, mine | (nb << 16));
+                } else if (act) {
+                    gm_put(dst + (size_t)r * DG + c0 + c, tag, gm_bits(v));
+                }
+            }
+            __syncthreads();                   // red is reused by the next phase
+        }
+        // ---------------- z = W_out a2 + b_out, this workgroup's NZ logits
+        {
+            floatx4 acc[NZT];
+#pragma unroll
+            for (int t = 0; t < NZT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            if (wave < KW) {
+                uint32_t w[UPW][4];
+                gm_fetch_a<T, UPW>(a.xa2 + ((size_t)g * R + row) * DG, rv, wave, lane, NU, D, tag, w,
+                                   a.err);
+#pragma unroll
+                for (int j = 0; j < UPW; ++j) {
+                    const F af = gm_frag<F>(w[j][0], w[j][1], w[j][2], w[j][3]);
+#pragma unroll
+                    for (int t = 0; t < NZT; ++t)
+                        if (t < nzt) Mma<T>::run(acc[t], af, wo[j][t]);
+                }
+#pragma unroll
+                for (int t = 0; t < NZT; ++t)
+                    if (t < nzt) red[(wave * ntm + t) * 64 + lane] = acc[t];
+            }
+            __syncthreads();
+            for (int e = tid; e < R * NZ; e += gm::NTHR) {
+                const int r = e / NZ, c = e % NZ;
+                const int t = c >> 4, ln = (r >> 2) * 16 + (c & 15), ii = r & 3;
+                float v = 0.f;
+                for (int kw = 0; kw < KW; ++kw) v += red[(kw * ntm + t) * 64 + ln][ii];
+                gm_put(a.xz + ((size_t)g * R + r) * Q + z0 + c, tag,
+                       gm_bits(v + (e < gm::NTHR ? bo : a.b_out[z0 + c])));
+            }
+            __syncthreads();
+        }
+        // ---------------- sample x_i for every row of the group (one wave per row)
+        for (int r = wave; r < R; r += gm::NW) {
+            const int b = g * R + r;
+            const bool valid = b < B;
+            const floatx4 qn = valid ? sample_noise(a.noise, a.seed, B, b, i - a.L, lane)
+                                     : floatx4{1.f, 1.f, 1.f, 1.f};
+            const u64* src = a.xz + ((size_t)g * R + r) * Q + 4 * lane;
+            floatx4 v;
+            int spins = 0;
+            for (;;) {
+                bool ok = true;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const u64 x = gm_get(src + e);
+                    v[e] = __uint_as_float((uint32_t)x);
+                    ok &= (uint32_t)(x >> 32) == tag;
+                }
+                if (__all(ok)) break;
+                if (gm_spin_fail(spins, a.err, lane)) break;
+            }
+            float* lrow = (p == 0 && valid && a.logp)
+                              ? a.logp + ((int64_t)(i - a.L) * B + b) * Q : nullptr;
+            const int x = sample_row(v, qn, lrow, lane);
+            if (lane == 0) {
+                hist[r * gm::HIST + (i & (gm::HIST - 1))] = x;
+                if (p == 0 && valid) a.seq[(int64_t)b * a.ldseq + i] = x;
+            }
+        }
+        __syncthreads();
+        // ---------------- next sample's a1, then the one after's off-critical-path sum
+        if (s + 1 < a.nsteps) {
+            publish_a1(i + 1);
+            if (s + 2 < a.nsteps) make_part(i + 2);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ host side
+namespace {
+typedef void (*GmKernel)(GenMlpArgs);
+
+template <typename T>
+GmKernel pick(int upw, int nzt) {
+    if (upw <= 1 && nzt <= 16) return gen_mlp_kernel<T, 1, 4, 16>;
+    if (upw <= 2 && nzt <= 4) return gen_mlp_kernel<T, 2, 4, 4>;
+    if (upw <= 4 && nzt <= 2) return gen_mlp_kernel<T, 4, 4, 2>;
+    return nullptr;     // fp32 at D > 512 would spill its resident weights: per-step path
+}
+
+int device_cus() {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            ncu = 0;
+    }
+    return ncu;
+}
+}  // namespace
+
+int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
+    memset(pl, 0, sizeof(*pl));
+    if (Q != gm::Q || FS0 < 1 || FS0 > gm::HIST || D % 16 || D > 1024 || B < 1) return 0;
+    const int CW = D < 64 ? D : 64;
+    if (D % CW) return 0;
+    const int P = D / CW;
+    const int NZ = Q / P;
+    if (NZ % 16) return 0;
+    const int UK = dtype == SRNN_BF16 ? 32 : 16;
+    const int NU = (D + UK - 1) / UK;
+    const int upw = (NU + gm::NW - 1) / gm::NW;
+    const int ncu = device_cus();
+    if (ncu <= 0) return 0;
+    int R = 0;
+    for (int r : {8, 16})
+        if ((int64_t)cdiv(B, r) * P <= ncu) { R = r; break; }
+    if (!R) return 0;
+    const GmKernel k = dtype == SRNN_BF16 ? pick<bf16>(upw, NZ / 16) : pick<float>(upw, NZ / 16);
+    if (!k) return 0;
+    const int es = dtype == SRNN_BF16 ? 2 : 4;
+    const int KW = NU < gm::NW ? NU : gm::NW;
+    const int ntm = (CW / 16) > (NZ / 16) ? CW / 16 : NZ / 16;
+    size_t lds = ((size_t)gm::Q * CW * es + 15) & ~(size_t)15;
+    lds += (size_t)KW * ntm * 64 * 16;
+    lds += (size_t)R * gm::HIST * 4;
+    if (lds > 160 * 1024) return 0;
+    pl->ok = 1;
+    pl->dtype = dtype;
+    pl->R = R;
+    pl->G = cdiv(B, R);
+    pl->P = P;
+    pl->CW = CW;
+    pl->NZ = NZ;
+    pl->lds = lds;
+    pl->kernel = (const void*)k;
+    const int GV = dtype == SRNN_BF16 ? 2 : 1;
+    pl->xa_words = (size_t)pl->G * R * (D / GV);
+    pl->xz_words = (size_t)pl->G * R * Q;
+    return 1;
+}
+
+int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
+    SRNN_REQUIRE(pl && pl->ok, "gen_mlp: no plan");
+    a.R = pl->R;
+    a.G = pl->G;
+    a.P = pl->P;
+    a.CW = pl->CW;
+    a.NZ = pl->NZ;
+    const GmKernel k = (GmKernel)pl->kernel;
+    // raise the dynamic-LDS limit once per kernel (not inside a graph capture's launches)
+    static const void* done[16];
+    static size_t done_lds[16];
+    int slot = 0;
+    while (slot < 16 && done[slot] && done[slot] != (const void*)k) ++slot;
+    if (slot == 16 || !done[slot] || done_lds[slot] < pl->lds) {
+        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        if (slot < 16) { done[slot] = (const void*)k; done_lds[slot] = 160 * 1024; }
+    }
+    hipLaunchKernelGGL(k, dim3(pl->G * pl->P), dim3(gm::NTHR), pl->lds, s, a);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}

@@ -13,6 +13,7 @@
 #include "samplernn_hip_internal.hpp"
 #include "ulaw_tables.h"
 #include "../../include/samplernn_hip.h"
+#include "gen_mlp.hpp"
 
 int srnn_mlp_l1_impl(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff,
                      const int* base, int B, int Tlen, int upper_dtype, const void* upper,
@@ -75,10 +76,16 @@ struct Bufs {
     float* logits;
     float* lut2;
     int* base;
+    // persistent sample loop (gen_mlp.hip): hand-off granules + error word, one zeroed block
+    unsigned long long* xa1;
+    unsigned long long* xa2;
+    unsigned long long* xz;
+    int* gerr;
+    size_t gm_bytes;
 };
 
 // carve (or size, if ws == nullptr) the workspace
-size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b) {
+size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl) {
     const int D = m->dim, Q = m->q_levels;
     const size_t es = m->dtype == SRNN_F32 ? 4 : 2;
     const bool lp = m->dtype != SRNN_F32;
@@ -104,6 +111,17 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b) {
     b->logits = (float*)take((size_t)B * Q * 4);
     b->lut2 = (float*)take((size_t)Q * 4);
     b->base = (int*)take(64);
+    b->xa1 = b->xa2 = b->xz = nullptr;
+    b->gerr = nullptr;
+    b->gm_bytes = 0;
+    if (pl && pl->ok) {
+        const size_t start = off;
+        b->gerr = (int*)take(256);
+        b->xa1 = (unsigned long long*)take(pl->xa_words * 8);
+        b->xa2 = (unsigned long long*)take(pl->xa_words * 8);
+        b->xz = (unsigned long long*)take(pl->xz_words * 8);
+        b->gm_bytes = off - start;
+    }
     return off;
 }
 
@@ -119,6 +137,7 @@ struct Ctx {
     int64_t ldseq;
     float* logp;
     hipStream_t s;
+    const GenMlpPlan* pl;     // persistent sample loop, or null for per-sample kernels
 };
 
 #define RET(x) do { int _r = (x); if (_r) return _r; } while (0)
@@ -196,7 +215,22 @@ int run_block(Ctx& c, int periods) {
             RET(tier_tick(c, k, off, ticks[k] & 1));
             ticks[k]++;
         }
-        RET(mlp_step(c, off));
+        if (!c.pl) {
+            RET(mlp_step(c, off));
+        } else if (off % m->tier[0].frame_size == 0) {
+            // the FS0 samples up to the next bottom-tier tick in one persistent launch
+            GenMlpArgs a;
+            memset(&a, 0, sizeof(a));
+            a.tab = m->tab; a.w_hid = m->w_hid; a.b_hid = m->b_hid;
+            a.w_out = m->w_out; a.b_out = m->b_out;
+            a.up0 = c.b.up[0]; a.ldup = (int64_t)m->tier[0].frame_size * m->dim;
+            a.noise = c.noise; a.seed = c.seed;
+            a.seq = c.seq; a.ldseq = c.ldseq; a.logp = c.logp;
+            a.base = c.b.base; a.off = off; a.nsteps = m->tier[0].frame_size; a.L = c.L;
+            a.B = c.B; a.D = m->dim; a.FS0 = m->tier[0].frame_size;
+            a.xa1 = c.b.xa1; a.xa2 = c.b.xa2; a.xz = c.b.xz; a.err = c.b.gerr;
+            RET(gen_mlp_launch(c.pl, a, c.s));
+        }
     }
     hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(1), 0, c.s, c.b.base, periods * c.L);
     SRNN_LAUNCH_CHECK();
@@ -205,10 +239,26 @@ int run_block(Ctx& c, int periods) {
 
 }  // namespace
 
+// persistent sample loop plan for this model/batch (ok = 0: per-sample kernels)
+static void plan_for(const SrnnModel* m, int n_seqs, GenMlpPlan* pl) {
+    if (!gen_mlp_plan(m->dtype, n_seqs, m->dim, m->tier[0].frame_size, m->q_levels, pl) ||
+        !env_flag("SRNN_GEN_PERSIST", 1))
+        pl->ok = 0;
+}
+
+extern "C" int srnn_gen_persistent_rows(int dtype, int n_seqs, int dim, int fs0, int q_levels) {
+    GenMlpPlan pl;
+    if (!gen_mlp_plan(dtype, n_seqs, dim, fs0, q_levels, &pl) || !env_flag("SRNN_GEN_PERSIST", 1))
+        return 0;
+    return pl.R;
+}
+
 extern "C" int srnn_gen_workspace_size(const SrnnModel* m, int n_seqs, size_t* bytes) {
     SRNN_REQUIRE(m && bytes && n_seqs > 0, "gen_workspace_size: bad args");
     Bufs b;
-    *bytes = carve(m, n_seqs, nullptr, &b);
+    GenMlpPlan pl;
+    plan_for(m, n_seqs, &pl);
+    *bytes = carve(m, n_seqs, nullptr, &b, &pl);
     return 0;
 }
 
@@ -223,7 +273,10 @@ extern "C" int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const f
     SRNN_REQUIRE(m->dim % 16 == 0, "generate: dim must be a multiple of 16");
     Ctx c;
     c.m = m;
-    size_t need = carve(m, n_seqs, (char*)workspace, &c.b);
+    GenMlpPlan pl;
+    plan_for(m, n_seqs, &pl);
+    if (flags & 2) pl.ok = 0;          // caller asked for the per-sample kernel path
+    size_t need = carve(m, n_seqs, (char*)workspace, &c.b, &pl);
     SRNN_REQUIRE(workspace_bytes >= need, "generate: workspace %zu < %zu", workspace_bytes, need);
     c.B = n_seqs;
     c.n_cond = n_cond;
@@ -235,6 +288,7 @@ extern "C" int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const f
     c.seq = seq;
     c.ldseq = (int64_t)c.L * (n_cond + 1);
     c.logp = logp;
+    c.pl = pl.ok ? &pl : nullptr;
     hipStream_t user = (hipStream_t)stream;
     const int D = m->dim, B = n_seqs;
     // private stream so a hipGraph can be captured regardless of the caller's stream
@@ -261,6 +315,10 @@ extern "C" int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const f
             if (rc) { srnn_set_error("generate: lut upload"); break; }
             rc = hipMemsetAsync(c.b.base, 0, 64, s) ? 2 : 0;
             if (rc) break;
+            if (c.pl) {
+                rc = hipMemsetAsync(c.b.gerr, 0, c.b.gm_bytes, s) ? 2 : 0;
+                if (rc) break;
+            }
             int L = c.L;
             rc = hipMemcpyAsync(c.b.base, &L, sizeof(int), hipMemcpyHostToDevice, s) ? 2 : 0;
             if (rc) break;
@@ -322,6 +380,13 @@ extern "C" int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const f
     if (hipStreamSynchronize(s) != hipSuccess && !rc) {
         srnn_set_error("generate: %s", hipGetErrorString(hipGetLastError()));
         rc = 2;
+    }
+    if (!rc && c.pl) {
+        int e = 0;
+        if (hipMemcpy(&e, c.b.gerr, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || e) {
+            srnn_set_error("generate: persistent sample loop lost a hand-off (spin limit)");
+            rc = 2;
+        }
     }
     if (exec) (void)hipGraphExecDestroy(exec);
     if (graph) (void)hipGraphDestroy(graph);

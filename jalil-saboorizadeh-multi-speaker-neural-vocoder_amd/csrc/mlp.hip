@@ -15,6 +15,7 @@
 #include <algorithm>
 
 #include "samplernn_hip_internal.hpp"
+#include "sampler.hpp"
 
 // ------------------------------------------------------------------ L1 gather
 // rows r = b * Tlen + t;  idx_k = x[b * ldx + xoff(+base) + t + k]
@@ -178,18 +179,6 @@ extern "C" int srnn_mlp_l1(int dtype, const void* tab, const int64_t* x, int64_t
                             out, ldo, D, FS0, Q, (hipStream_t)stream);
 }
 
-// ------------------------------------------------------------------ wave helpers
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
-}
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
 // ------------------------------------------------------------------ log-softmax + NLL
 // One wave per row (Q = 256: lane holds q = lane + 64 j).  Writes
 //   loss_row[r] = lse - z[target]     (if loss_row)
@@ -341,26 +330,8 @@ extern "C" int srnn_nll_bwd(const int64_t* target, int64_t ldt, int Tlen, int64_
 }
 
 // ------------------------------------------------------------------ sampler
-// Philox4x32-10 (Salmon et al. 2011): counter = (q/4, row, step, 0), key = seed.
-__device__ __forceinline__ uint4 philox4x32(uint4 c, uint2 k) {
-#pragma unroll
-    for (int i = 0; i < 10; ++i) {
-        const uint32_t lo0 = c.x * 0xD2511F53u, hi0 = __umulhi(c.x, 0xD2511F53u);
-        const uint32_t lo1 = c.z * 0xCD9E8D57u, hi1 = __umulhi(c.z, 0xCD9E8D57u);
-        c = make_uint4(hi1 ^ c.y ^ k.x, lo1, hi0 ^ c.w ^ k.y, lo0);
-        k.x += 0x9E3779B9u;
-        k.y += 0xBB67AE85u;
-    }
-    return c;
-}
-
-// Exp(1) from a 32-bit draw: u in (0, 1], q = -log(u)
-__device__ __forceinline__ float exp1_from_u32(uint32_t x) {
-    const float u = ((float)(x >> 8) + 1.0f) * (1.0f / 16777216.0f);
-    return -logf(u);
-}
-
-// One wave per row; lane holds q = 4 * lane + j (16-B loads of logits and noise).
+// One wave per row; lane holds q = 4 * lane + j (16-B loads of logits and noise).  The
+// per-row math lives in sampler.hpp, shared with the persistent generation loop.
 __global__ __launch_bounds__(256) void sample_kernel(
     const float* __restrict__ z, int64_t ldz, int B, const float* __restrict__ noise,
     uint64_t seed, const int* __restrict__ base, int off, int L, int64_t* __restrict__ seq,
@@ -371,38 +342,9 @@ __global__ __launch_bounds__(256) void sample_kernel(
     const int i = *base + off;        // absolute sample index being generated
     const int step = i - L;
     const floatx4 v = *reinterpret_cast<const floatx4*>(z + (int64_t)b * ldz + 4 * lane);
-    float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-    m = wave_max(m);
-    float s = 0.f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) s += expf(v[j] - m);
-    s = wave_sum(s);
-    const float ls = logf(s);
-    floatx4 q;
-    if (noise) {
-        q = *reinterpret_cast<const floatx4*>(noise + ((int64_t)step * B + b) * 256 + 4 * lane);
-    } else {
-        const uint4 rnd = philox4x32(make_uint4((uint32_t)lane, (uint32_t)b, (uint32_t)step, 0u),
-                                     make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
-        q = floatx4{exp1_from_u32(rnd.x), exp1_from_u32(rnd.y), exp1_from_u32(rnd.z),
-                    exp1_from_u32(rnd.w)};
-    }
-    float best = -1.0f;
-    int bi = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const float lp = (v[j] - m) - ls;
-        if (logp_out) logp_out[((int64_t)step * B + b) * 256 + 4 * lane + j] = lp;
-        const float r = expf(lp) / q[j];
-        if (r > best) { best = r; bi = 4 * lane + j; }
-    }
-    // wave argmax, first index on ties (torch argmax)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const float ob = __shfl_xor(best, o);
-        const int oi = __shfl_xor(bi, o);
-        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
-    }
+    const floatx4 q = sample_noise(noise, seed, B, b, step, lane);
+    const int bi = sample_row(v, q, logp_out ? logp_out + ((int64_t)step * B + b) * 256 : nullptr,
+                              lane);
     if (lane == 0) seq[(int64_t)b * ldseq + i] = bi;
 }
 

@@ -671,7 +671,9 @@ class Generator(Runner):
     CPU `multinomial(1)` computes: sampler='torch' draws q from torch's CPU generator in
     the reference's order (bit-replay of the reference stream); sampler='philox' draws q
     on the device (counter-based Philox4x32-10, seed) for long runs.  `cuda` is accepted
-    for API compatibility; the product path always runs on the GPU.
+    for API compatibility; the product path always runs on the GPU.  persistent=True (the
+    default) runs the sample chain between bottom-tier ticks as one persistent launch
+    (gen_mlp.hip) where the shape fits, else per-sample kernels.
     """
 
     def __init__(self, model, cuda=False):
@@ -680,7 +682,7 @@ class Generator(Runner):
         self.last_sequences = None
 
     def __call__(self, n_seqs, seq_len, cond, spk, sampler='torch', seed=0, noise=None,
-                 return_logp=False, use_graph=True, dtype=None):
+                 return_logp=False, use_graph=True, dtype=None, persistent=True):
         model = self.model
         self.reset_hidden_states()
         dev = next(model.parameters()).device
@@ -711,7 +713,8 @@ class Generator(Runner):
         ws = torch.empty(sz.value, device=dev, dtype=torch.uint8)
         H.lib().call('srnn_generate', ctypes.byref(m), n_seqs, num_cond, H.ptr(cond),
                      H.ptr(row_bias), H.ptr(noise), int(seed) & ((1 << 64) - 1), H.ptr(seq),
-                     H.ptr(logp), H.ptr(ws), sz.value, 1 if use_graph else 0, H.stream())
+                     H.ptr(logp), H.ptr(ws), sz.value,
+                     (1 if use_graph else 0) | (0 if persistent else 2), H.stream())
         del keep
         self.last_sequences = seq
         out = model.dequantize(seq[:, L:], Q).cpu()

@@ -113,7 +113,17 @@ def lib():
 
 
 def exported_symbols():
-    return sorted(_SIGS) + ['srnn_last_error', 'srnn_abi_version', 'srnn_gru_seq_supported']
+    return sorted(_SIGS) + ['srnn_last_error', 'srnn_abi_version', 'srnn_gru_seq_supported',
+                            'srnn_gen_persistent_rows']
+
+
+def gen_persistent_rows(dtype, n_seqs, dim, fs0, q_levels=256):
+    """Rows per group of the persistent generation loop for this shape (0: per-sample
+    kernels)."""
+    fn = lib().dll.srnn_gen_persistent_rows
+    fn.argtypes = [_I, _I, _I, _I, _I]
+    fn.restype = _I
+    return int(fn(dcode(dtype), n_seqs, dim, fs0, q_levels))
 
 
 _GRU_SEQ = {}

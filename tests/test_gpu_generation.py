@@ -1,0 +1,89 @@
+"""Persistent generation sample loop (csrc/gen_mlp.hip) against the per-sample kernel path,
+the teacher-forced Predictor and the sampler definition (Generator.__call__,
+model.py:445-520).
+
+* fp32: the persistent loop and the per-sample kernels must draw the SAME index stream from
+  the same Exp(1) noise, and their per-step log-probs agree within 1e-4 (north star);
+* bf16 (the production dtype) at configs[2] size (D = 1024, B = 128): every drawn index is
+  exactly argmax(exp(logp) / q) of the log-probs the loop reports, and those log-probs are
+  the teacher-forced fp32 Predictor's on the generated stream within a bf16 tolerance;
+* shapes with a ragged last row group (B not a multiple of R).
+"""
+import numpy as np
+import pytest
+import torch
+
+import recipe
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def build(cfg, seed, dtype):
+    import model as M
+    m = M.SampleRNN(cfg['frame_sizes'], cfg['n_rnn'], cfg['dim'], cfg['learn_h0'],
+                    cfg['q_levels'], True, cfg['weight_norm'], cfg['cond_dim'], cfg['spk_dim'])
+    m.compute_dtype = dtype
+    pred = M.Predictor(m)
+    pred.load_state_dict({k: torch.from_numpy(v.copy())
+                          for k, v in recipe.make_weights(cfg, seed).items()})
+    return m.to(DEV), pred.to(DEV)
+
+
+def generate(m, n_seqs, cond, spk, persistent, **kw):
+    import model as M
+    gen = M.Generator(m, True)
+    _, lp = gen(n_seqs, 0, cond, spk, return_logp=True, persistent=persistent, **kw)
+    return gen.last_sequences.cpu(), lp.cpu()
+
+
+@pytest.mark.parametrize('D,B,n_cond,n_rnn', [(64, 5, 3, 1), (32, 3, 2, 2), (256, 24, 2, 1),
+                                              (512, 40, 2, 1)])
+def test_persistent_matches_per_sample_fp32(hip, D, B, n_cond, n_rnn):
+    cfg = dict(recipe.CONFIGS['t3'], dim=D, n_rnn=n_rnn)
+    m, _ = build(cfg, 7, torch.float32)
+    assert hip.gen_persistent_rows(torch.float32, B, D, 16) > 0
+    cond = recipe.synth_cond((B, n_cond, cfg['cond_dim']), 4)
+    spk = np.arange(B) % cfg['spk_dim']
+    noise = torch.from_numpy(recipe.synth_noise((n_cond * 64, B, 256), 9))
+    s1, l1 = generate(m, B, cond, spk, True, noise=noise)
+    s0, l0 = generate(m, B, cond, spk, False, noise=noise)
+    assert torch.equal(s1, s0)
+    torch.testing.assert_close(l1, l0, atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize('B', [128, 130, 9])
+def test_persistent_bf16_d1024(hip, B):
+    cfg = recipe.CONFIGS['big']
+    m, pred = build(cfg, 11, torch.bfloat16)
+    assert hip.gen_persistent_rows(torch.bfloat16, B, 1024, 16) > 0
+    n_cond = 2
+    cond = recipe.synth_cond((B, n_cond, cfg['cond_dim']), 5)
+    spk = np.arange(B) % cfg['spk_dim']
+    noise = torch.from_numpy(recipe.synth_noise((n_cond * 64, B, 256), 3))
+    seq, lp = generate(m, B, cond, spk, True, noise=noise)
+    L = m.lookback
+    # sampler definition, exactly: x_t = argmax(exp(logp_t) / q_t) (first index on ties)
+    drawn = torch.argmax(torch.exp(lp) / noise.permute(1, 0, 2), dim=-1)
+    assert torch.equal(drawn, seq[:, L:])
+    # teacher-forced fp32 Predictor on the generated stream: bf16 tolerance on log-probs
+    m.compute_dtype = torch.float32
+    with torch.no_grad():
+        tf = pred(seq[:, :-1], True, torch.from_numpy(cond),
+                  torch.from_numpy(spk).reshape(-1, 1)).cpu()
+    err = (tf - lp).abs()
+    assert err.max().item() < 0.25, err.max().item()
+    assert err.mean().item() < 0.02, err.mean().item()
+
+
+def test_persistent_philox_matches_per_sample_fp32(hip):
+    """Device RNG: both paths draw Philox4x32-10(seed) noise with the same counters."""
+    cfg = dict(recipe.CONFIGS['t3'], dim=128)
+    m, _ = build(cfg, 3, torch.float32)
+    B, n_cond = 16, 3
+    cond = recipe.synth_cond((B, n_cond, cfg['cond_dim']), 6)
+    spk = np.arange(B) % cfg['spk_dim']
+    s1, l1 = generate(m, B, cond, spk, True, sampler='philox', seed=99)
+    s0, l0 = generate(m, B, cond, spk, False, sampler='philox', seed=99)
+    assert torch.equal(s1, s0)
+    torch.testing.assert_close(l1, l0, atol=1e-4, rtol=0)

@@ -49,15 +49,16 @@ def test_forward_golden(hip, name):
 
 
 @pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn'])
-@pytest.mark.parametrize('graph', [True, False])
-def test_generation_golden(hip, name, graph):
+@pytest.mark.parametrize('graph,persistent', [(True, True), (False, True), (True, False),
+                                              (False, False)])
+def test_generation_golden(hip, name, graph, persistent):
     import model as M
     g = golden('gen_' + name)
     cfg = recipe.CONFIGS[name]
     m, _ = build(cfg, recipe.make_weights(cfg, int(g['weight_seed'])))
     gen = M.Generator(m, True)
     out, lp = gen(int(g['n_seqs']), 0, g['cond'], int(g['spk']), noise=g['noise'],
-                  return_logp=True, use_graph=graph)
+                  return_logp=True, use_graph=graph, persistent=persistent)
     L = m.lookback
     idx = gen.last_sequences[:, L:].cpu().numpy()
     assert np.array_equal(idx, g['idx'])
