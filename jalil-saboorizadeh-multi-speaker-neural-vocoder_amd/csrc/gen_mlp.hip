@@ -98,11 +98,25 @@ __device__ __forceinline__ bool gm_spin_fail(int& spins, int* err, int lane) {
     return false;
 }
 
-// A-operand fragments of one wave for one hand-off buffer (granules of row `row`):
-// for unit j (global unit u = wave + NW*j) the lane's 16 data bytes = 4 granules.
+// Buffer resource over a hand-off buffer: 16-B granule-pair loads with sc1 (L1 bypass)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gm_rsrc(const void* p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff,
+                                             0x00020000);
+}
+__device__ __forceinline__ uint4 gm_get2(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /*sc1*/);
+    uint4 u;
+    __builtin_memcpy(&u, &v, 16);
+    return u;
+}
+
+// A-operand fragments of one wave for one hand-off buffer (granules of row `row`, starting
+// at granule `rowg`): for unit j (global unit u = wave + NW*j) the lane's 16 data bytes are
+// 4 granules = two 16-B loads.  Spins until every tag == tag.
 template <typename T, int UPW>
-__device__ __forceinline__ void gm_fetch_a(const u64* src, bool rv, int wave, int lane, int NU,
-                                           int D, uint32_t tag, uint32_t (&w)[UPW][4], int* err) {
+__device__ __forceinline__ void gm_fetch_a(__amdgpu_buffer_rsrc_t src, uint32_t rowg, bool rv,
+                                           int wave, int lane, int NU, int D, uint32_t tag,
+                                           uint32_t (&w)[UPW][4], int* err) {
     constexpr int GV = GmT<T>::GV, UK = GmT<T>::UK, EPL = UK / 4;
     int spins = 0;
     for (;;) {
@@ -112,13 +126,10 @@ __device__ __forceinline__ void gm_fetch_a(const u64* src, bool rv, int wave, in
             const int u = wave + gm::NW * j;
             const int ke = u * UK + (lane >> 4) * EPL;
             if (rv && u < NU && ke < D) {
-                const u64* s = src + ke / GV;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const u64 x = gm_get(s + e);
-                    w[j][e] = (uint32_t)x;
-                    ok &= (uint32_t)(x >> 32) == tag;
-                }
+                const uint32_t off = (rowg + (uint32_t)(ke / GV)) * 8u;
+                const uint4 x0 = gm_get2(src, off), x1 = gm_get2(src, off + 16);
+                w[j][0] = x0.x; w[j][1] = x0.z; w[j][2] = x1.x; w[j][3] = x1.z;
+                ok &= (x0.y == tag) & (x0.w == tag) & (x1.y == tag) & (x1.w == tag);
             } else {
 #pragma unroll
                 for (int e = 0; e < 4; ++e) w[j][e] = 0u;
@@ -134,7 +145,9 @@ __device__ __forceinline__ void gm_fetch_a(const u64* src, bool rv, int wave, in
 // read all of a2(i), which in turn came after every producer had read all of a1(i).  So when
 // any a1(i+1) granule lands, a1(i) has been consumed by everyone; the same chain covers a2
 // and z.  A consumer therefore only ever sees tag i-1 (keep polling) or tag i (done).
-template <typename T, int UPW, int NT, int NZT>
+//
+// Thread tid owns a1/a2 element (r, c) = (tid / CW, tid % CW) of its workgroup (R*CW <= 512).
+template <typename T, int UPW, int NT, int NZT, int MAXT>
 __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     using F = typename GmT<T>::frag;
     constexpr int GV = GmT<T>::GV, UK = GmT<T>::UK, EPL = UK / 4;
@@ -149,38 +162,80 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     const int nt = CW / 16, nzt = NZ / 16, ntm = max(nt, nzt);
     const int DG = D / GV;
     const T* __restrict__ tab = (const T*)a.tab;
+    // optional phase timestamps (workgroup 0, thread 0; s_memrealtime = 100 MHz)
+    unsigned long long* dg = (a.diag && blockIdx.x == 0 && tid == 0) ? a.diag : nullptr;
+    int nd = 0;
+#define GM_STAMP() do { if (dg && nd < 512) dg[nd++] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    GM_STAMP();
     // LDS: [tab15 Q x CW][red KW x ntm x 64 floatx4][hist R x HIST]
     T* tab15 = (T*)smem;
     size_t lo = ((size_t)Q * CW * sizeof(T) + 15) & ~(size_t)15;
     floatx4* red = (floatx4*)(smem + lo);
     lo += (size_t)KW * ntm * 64 * sizeof(floatx4);
     int* hist = (int*)(smem + lo);
+    const __amdgpu_buffer_rsrc_t rx1 = gm_rsrc(a.xa1), rx2 = gm_rsrc(a.xa2), rxz = gm_rsrc(a.xz);
 
     // ---- resident weights: B fragments of this wave's K units
     F wh[UPW][NT], wo[UPW][NZT];
+    // (loads from clamped addresses with no branches, so all of them are in flight at once;
+    //  fragments outside the shape are zeroed afterwards)
+    {
+        uint4 lw[UPW][NT], lz[UPW][NZT];
 #pragma unroll
-    for (int j = 0; j < UPW; ++j) {
-        const int u = wave + gm::NW * j;
-        const int ke = u * UK + (lane >> 4) * EPL;
-        const bool kv = u < NU && ke < D;
+        for (int j = 0; j < UPW; ++j) {
+            const int u = wave + gm::NW * j;
+            const int ke = min(u * UK + (lane >> 4) * EPL, D - EPL);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) {
-            const int n = c0 + t * 16 + (lane & 15);
-            wh[j][t] = (kv && t < nt) ? gm_load16<F>((const T*)a.w_hid + (int64_t)n * D + ke)
-                                      : gm_frag<F>(0u, 0u, 0u, 0u);
+            for (int t = 0; t < NT; ++t) {
+                const int n = min(c0 + t * 16 + (lane & 15), D - 1);
+                lw[j][t] = *reinterpret_cast<const uint4*>((const T*)a.w_hid + (int64_t)n * D + ke);
+            }
+#pragma unroll
+            for (int t = 0; t < NZT; ++t) {
+                const int n = min(z0 + t * 16 + (lane & 15), Q - 1);
+                lz[j][t] = *reinterpret_cast<const uint4*>((const T*)a.w_out + (int64_t)n * D + ke);
+            }
         }
 #pragma unroll
-        for (int t = 0; t < NZT; ++t) {
-            const int n = z0 + t * 16 + (lane & 15);
-            wo[j][t] = (kv && t < nzt) ? gm_load16<F>((const T*)a.w_out + (int64_t)n * D + ke)
-                                       : gm_frag<F>(0u, 0u, 0u, 0u);
+        for (int j = 0; j < UPW; ++j) {
+            const int u = wave + gm::NW * j;
+            const bool kv = u < NU && u * UK + (lane >> 4) * EPL < D;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const bool v = kv && t < nt;
+                wh[j][t] = gm_frag<F>(v ? lw[j][t].x : 0u, v ? lw[j][t].y : 0u,
+                                      v ? lw[j][t].z : 0u, v ? lw[j][t].w : 0u);
+            }
+#pragma unroll
+            for (int t = 0; t < NZT; ++t) {
+                const bool v = kv && t < nzt;
+                wo[j][t] = gm_frag<F>(v ? lz[j][t].x : 0u, v ? lz[j][t].y : 0u,
+                                      v ? lz[j][t].z : 0u, v ? lz[j][t].w : 0u);
+            }
         }
     }
     // ---- newest-tap table slice and the sample history of this group's rows
     const int i0 = *a.base + a.off;
-    for (int e = tid; e < Q * CW; e += gm::NTHR) {
-        const int q = e / CW, c = e % CW;
-        tab15[e] = tab[((int64_t)(FS0 - 1) * Q + q) * D + c0 + c];
+    {
+        // Q x CW slice in 16-B pieces, all loads in flight before the LDS stores
+        constexpr int PER = 16 / sizeof(T);
+        const int cpr = CW / PER;                       // pieces per table row
+        const int npc = Q * cpr;
+        constexpr int MAXIT = gm::Q * 64 * 4 / 16 / gm::NTHR;   // fp32, CW = 64: 8
+        uint4 buf[MAXIT];
+#pragma unroll
+        for (int it = 0; it < MAXIT; ++it) {
+            const int e = min(tid + it * gm::NTHR, npc - 1);
+            const int q = e / cpr, c = (e % cpr) * PER;
+            buf[it] = *reinterpret_cast<const uint4*>(
+                tab + ((int64_t)(FS0 - 1) * Q + q) * D + c0 + c);
+        }
+        // (clamped pieces store the same bytes to the same slot: no branch)
+#pragma unroll
+        for (int it = 0; it < MAXIT; ++it) {
+            const int e = min(tid + it * gm::NTHR, npc - 1);
+            *reinterpret_cast<uint4*>(tab15 + (size_t)e * PER) = buf[it];
+        }
     }
     for (int e = tid; e < R * FS0; e += gm::NTHR) {
         const int r = e / FS0, k = e % FS0;
@@ -188,64 +243,64 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         const int j = i0 - FS0 + k;
         hist[r * gm::HIST + (j & (gm::HIST - 1))] = (int)a.seq[(int64_t)b * a.ldseq + j];
     }
-    float bh[2];
-    {
-        for (int s = 0; s < 2; ++s) {
-            const int e = tid + s * gm::NTHR;
-            bh[s] = e < R * CW ? a.b_hid[c0 + e % CW] : 0.f;
-        }
-    }
+    // this thread's a1/a2 element
+    const bool own = tid < R * CW;
+    const int er = own ? tid / CW : 0, ec = own ? tid % CW : 0;
+    const int eb = min(g * R + er, B - 1);
+    const float bh = own ? a.b_hid[c0 + ec] : 0.f;
     const float bo = tid < R * NZ ? a.b_out[z0 + tid % NZ] : 0.f;
     __syncthreads();
 
-    // a1 pieces owned by this thread: e = tid + s*NTHR < R*CW  (r = e / CW, c = e % CW)
-    float part[2];
-    auto make_part = [&](int i) {
-        const int jpos = i % FS0;
+    // partial a1 sum of sample i: up0 + the FS0-1 older taps.  issue_part puts every load in
+    // flight (indices first, then table rows); finish_part sums them -- callers place other
+    // work (the next hand-off wait) in between so the gathers' latency hides behind it.
+    // The loads are unconditional (clamped tap index; unused taps re-read tap 0 and are
+    // dropped by a select), so the compiler keeps them all in flight in one basic block.
+    T tv[MAXT];
+    float upv = 0.f, part = 0.f;
+    auto issue_part = [&](int i) {
+        int xs[MAXT];
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int e = tid + s * gm::NTHR;
-            if (e >= R * CW) { part[s] = 0.f; continue; }
-            const int r = e / CW, c = e % CW;
-            const int b = min(g * R + r, B - 1);
-            float v = a.up0[(int64_t)b * a.ldup + (int64_t)jpos * D + c0 + c];
-            for (int k = 0; k < FS0 - 1; ++k) {
-                const int x = hist[r * gm::HIST + ((i - FS0 + k) & (gm::HIST - 1))];
-                v += gm_ld(tab + ((int64_t)k * Q + x) * D + c0 + c);
-            }
-            part[s] = v;
-        }
+        for (int k = 0; k < MAXT; ++k)
+            xs[k] = hist[er * gm::HIST + ((i - FS0 + (k < FS0 - 1 ? k : 0)) & (gm::HIST - 1))];
+#pragma unroll
+        for (int k = 0; k < MAXT; ++k)
+            tv[k] = tab[((int64_t)(k < FS0 - 1 ? k : 0) * Q + xs[k]) * D + c0 + ec];
+        upv = a.up0[(int64_t)eb * a.ldup + (int64_t)(i % FS0) * D + c0 + ec];
+    };
+    auto finish_part = [&]() {
+        float v = upv;
+#pragma unroll
+        for (int k = 0; k < MAXT; ++k) v += k < FS0 - 1 ? to_f(tv[k]) : 0.f;
+        part = own ? v : 0.f;
     };
     // publish a1(i) = relu(part + Tab[FS0-1][x_{i-1}]) as granules tagged i
     auto publish_a1 = [&](int i) {
         u64* dst = a.xa1 + (size_t)g * R * DG;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int e = tid + s * gm::NTHR;
-            if (s * gm::NTHR >= R * CW) break;                 // uniform
-            const bool act = e < R * CW;
-            const int r = act ? e / CW : 0, c = act ? e % CW : 0;
-            float v = 0.f;
-            if (act) {
-                const int x = hist[r * gm::HIST + ((i - 1) & (gm::HIST - 1))];
-                v = fmaxf(part[s] + to_f(tab15[x * CW + c]), 0.f);
-            }
-            if (GV == 2) {
-                const uint32_t mine = gm_bf16_bits(v);
-                const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
-                if (act && (c & 1) == 0) gm_put(dst + (size_t)r * DG + (c0 + c) / 2, i, mine | (nb << 16));
-            } else if (act) {
-                gm_put(dst + (size_t)r * DG + c0 + c, i, gm_bits(v));
-            }
+        float v = 0.f;
+        if (own) {
+            const int x = hist[er * gm::HIST + ((i - 1) & (gm::HIST - 1))];
+            v = fmaxf(part + to_f(tab15[x * CW + ec]), 0.f);
+        }
+        if (GV == 2) {
+            const uint32_t mine = gm_bf16_bits(v);
+            const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
+            if (own && (ec & 1) == 0) gm_put(dst + (size_t)er * DG + (c0 + ec) / 2, i, mine | (nb << 16));
+        } else if (own) {
+            gm_put(dst + (size_t)er * DG + c0 + ec, i, gm_bits(v));
         }
     };
 
-    make_part(i0);
+    GM_STAMP();
+    issue_part(i0);
+    finish_part();
     publish_a1(i0);
-    if (a.nsteps > 1) make_part(i0 + 1);
+    if (a.nsteps > 1) issue_part(i0 + 1);
+    bool pending = a.nsteps > 1;
 
     const int row = lane & 15;
     const bool rv = row < R;
+    const uint32_t rowg = (uint32_t)((g * R + row) * DG);
     for (int s = 0; s < a.nsteps; ++s) {
         const int i = i0 + s;
         const uint32_t tag = (uint32_t)i;
@@ -256,8 +311,8 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
             if (wave < KW) {
                 uint32_t w[UPW][4];
-                gm_fetch_a<T, UPW>(a.xa1 + ((size_t)g * R + row) * DG, rv, wave, lane, NU, D, tag, w,
-                                   a.err);
+                gm_fetch_a<T, UPW>(rx1, rowg, rv, wave, lane, NU, D, tag, w, a.err);
+                GM_STAMP();
 #pragma unroll
                 for (int j = 0; j < UPW; ++j) {
                     const F af = gm_frag<F>(w[j][0], w[j][1], w[j][2], w[j][3]);
@@ -268,31 +323,27 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 for (int t = 0; t < NT; ++t)
                     if (t < nt) red[(wave * ntm + t) * 64 + lane] = acc[t];
             }
+            if (pending) { finish_part(); pending = false; }   // gathers landed meanwhile
+            GM_STAMP();
             __syncthreads();
             u64* dst = a.xa2 + (size_t)g * R * DG;
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const int e = tid + s2 * gm::NTHR;
-                if (s2 * gm::NTHR >= R * CW) break;
-                const bool act = e < R * CW;
-                const int r = act ? e / CW : 0, c = act ? e % CW : 0;
-                const int t = c >> 4, ln = (r >> 2) * 16 + (c & 15), ii = r & 3;
-                float v = 0.f;
-                if (act) {
-                    for (int kw = 0; kw < KW; ++kw) v += red[(kw * ntm + t) * 64 + ln][ii];
-                    v = fmaxf(v + bh[s2], 0.f);
-                }
-                if (GV == 2) {
-                    const uint32_t mine = gm_bf16_bits(v);
-                    const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
-                    if (act && (c & 1) == 0)
-                        gm_put(dst + (size_t)r * DG + (c0 + c) / 2, tag, mine | (nb << 16));
-                } else if (act) {
-                    gm_put(dst + (size_t)r * DG + c0 + c, tag, gm_bits(v));
-                }
+            float v = 0.f;
+            if (own) {
+                const int t = ec >> 4, ln = (er >> 2) * 16 + (ec & 15), ii = er & 3;
+                for (int kw = 0; kw < KW; ++kw) v += red[(kw * ntm + t) * 64 + ln][ii];
+                v = fmaxf(v + bh, 0.f);
+            }
+            if (GV == 2) {
+                const uint32_t mine = gm_bf16_bits(v);
+                const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
+                if (own && (ec & 1) == 0)
+                    gm_put(dst + (size_t)er * DG + (c0 + ec) / 2, tag, mine | (nb << 16));
+            } else if (own) {
+                gm_put(dst + (size_t)er * DG + c0 + ec, tag, gm_bits(v));
             }
             __syncthreads();                   // red is reused by the next phase
         }
+        GM_STAMP();
         // ---------------- z = W_out a2 + b_out, this workgroup's NZ logits
         {
             floatx4 acc[NZT];
@@ -300,8 +351,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             for (int t = 0; t < NZT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
             if (wave < KW) {
                 uint32_t w[UPW][4];
-                gm_fetch_a<T, UPW>(a.xa2 + ((size_t)g * R + row) * DG, rv, wave, lane, NU, D, tag, w,
-                                   a.err);
+                gm_fetch_a<T, UPW>(rx2, rowg, rv, wave, lane, NU, D, tag, w, a.err);
 #pragma unroll
                 for (int j = 0; j < UPW; ++j) {
                     const F af = gm_frag<F>(w[j][0], w[j][1], w[j][2], w[j][3]);
@@ -324,23 +374,21 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             }
             __syncthreads();
         }
+        GM_STAMP();
         // ---------------- sample x_i for every row of the group (one wave per row)
         for (int r = wave; r < R; r += gm::NW) {
             const int b = g * R + r;
             const bool valid = b < B;
             const floatx4 qn = valid ? sample_noise(a.noise, a.seed, B, b, i - a.L, lane)
                                      : floatx4{1.f, 1.f, 1.f, 1.f};
-            const u64* src = a.xz + ((size_t)g * R + r) * Q + 4 * lane;
+            const uint32_t zoff = (uint32_t)((((size_t)g * R + r) * Q + 4 * lane) * 8);
             floatx4 v;
             int spins = 0;
             for (;;) {
-                bool ok = true;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const u64 x = gm_get(src + e);
-                    v[e] = __uint_as_float((uint32_t)x);
-                    ok &= (uint32_t)(x >> 32) == tag;
-                }
+                const uint4 x0 = gm_get2(rxz, zoff), x1 = gm_get2(rxz, zoff + 16);
+                v = floatx4{__uint_as_float(x0.x), __uint_as_float(x0.z), __uint_as_float(x1.x),
+                            __uint_as_float(x1.z)};
+                const bool ok = (x0.y == tag) & (x0.w == tag) & (x1.y == tag) & (x1.w == tag);
                 if (__all(ok)) break;
                 if (gm_spin_fail(spins, a.err, lane)) break;
             }
@@ -353,24 +401,32 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             }
         }
         __syncthreads();
-        // ---------------- next sample's a1, then the one after's off-critical-path sum
+        GM_STAMP();
+        // ---------------- next sample's a1; the one after's gathers go in flight
         if (s + 1 < a.nsteps) {
             publish_a1(i + 1);
-            if (s + 2 < a.nsteps) make_part(i + 2);
+            if (s + 2 < a.nsteps) { issue_part(i + 2); pending = true; }
         }
+        GM_STAMP();
     }
+#undef GM_STAMP
 }
 
 // ------------------------------------------------------------------ host side
 namespace {
 typedef void (*GmKernel)(GenMlpArgs);
 
-template <typename T>
-GmKernel pick(int upw, int nzt) {
-    if (upw <= 1 && nzt <= 16) return gen_mlp_kernel<T, 1, 4, 16>;
-    if (upw <= 2 && nzt <= 4) return gen_mlp_kernel<T, 2, 4, 4>;
-    if (upw <= 4 && nzt <= 2) return gen_mlp_kernel<T, 4, 4, 2>;
+template <typename T, int MAXT>
+GmKernel pick_t(int upw, int nzt) {
+    if (upw <= 1 && nzt <= 16) return gen_mlp_kernel<T, 1, 4, 16, MAXT>;
+    if (upw <= 2 && nzt <= 4) return gen_mlp_kernel<T, 2, 4, 4, MAXT>;
+    if (upw <= 4 && nzt <= 2) return gen_mlp_kernel<T, 4, 4, 2, MAXT>;
     return nullptr;     // fp32 at D > 512 would spill its resident weights: per-step path
+}
+// MAXT = older taps gathered per sample (FS0 - 1 <= MAXT)
+template <typename T>
+GmKernel pick(int upw, int nzt, int fs0) {
+    return fs0 - 1 <= 15 ? pick_t<T, 15>(upw, nzt) : pick_t<T, 31>(upw, nzt);
 }
 
 int device_cus() {
@@ -399,10 +455,11 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     const int ncu = device_cus();
     if (ncu <= 0) return 0;
     int R = 0;
-    for (int r : {8, 16})
+    for (int r : {8})          // one a1 element per thread: R * CW <= 512
         if ((int64_t)cdiv(B, r) * P <= ncu) { R = r; break; }
     if (!R) return 0;
-    const GmKernel k = dtype == SRNN_BF16 ? pick<bf16>(upw, NZ / 16) : pick<float>(upw, NZ / 16);
+    const GmKernel k = dtype == SRNN_BF16 ? pick<bf16>(upw, NZ / 16, FS0)
+                                          : pick<float>(upw, NZ / 16, FS0);
     if (!k) return 0;
     const int es = dtype == SRNN_BF16 ? 2 : 4;
     const int KW = NU < gm::NW ? NU : gm::NW;
@@ -426,6 +483,21 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     return 1;
 }
 
+unsigned long long*& gm_diag_buf() {
+    static unsigned long long* p = nullptr;
+    return p;
+}
+
+extern "C" int srnn_gen_diag_dump(void) {
+    unsigned long long h[512];
+    if (!gm_diag_buf() || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(h, gm_diag_buf(), sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+        return 1;
+    for (int k = 1; k < 512 && h[k]; ++k)
+        fprintf(stderr, "gen_mlp diag %3d: +%8.2f us\n", k, (double)(h[k] - h[k - 1]) / 100.0);
+    return 0;
+}
+
 int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
     SRNN_REQUIRE(pl && pl->ok, "gen_mlp: no plan");
     a.R = pl->R;
@@ -433,6 +505,19 @@ int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
     a.P = pl->P;
     a.CW = pl->CW;
     a.NZ = pl->NZ;
+    {
+        // SRNN_GEN_DIAG=1: phase timestamps of the first launch into a device buffer that
+        // srnn_gen_diag_dump prints (timing diagnostics only)
+        static unsigned long long* diag = nullptr;
+        static int armed = -1;
+        if (armed < 0) armed = env_flag("SRNN_GEN_DIAG", 0);
+        if (armed == 1 && !diag && hipMalloc(&diag, 512 * 8) == hipSuccess) {
+            (void)hipMemsetAsync(diag, 0, 512 * 8, s);
+            a.diag = diag;
+            armed = 2;
+            gm_diag_buf() = diag;
+        }
+    }
     const GmKernel k = (GmKernel)pl->kernel;
     // raise the dynamic-LDS limit once per kernel (not inside a graph capture's launches)
     static const void* done[16];

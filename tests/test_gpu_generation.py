@@ -52,7 +52,7 @@ def test_persistent_matches_per_sample_fp32(hip, D, B, n_cond, n_rnn):
     torch.testing.assert_close(l1, l0, atol=1e-4, rtol=0)
 
 
-@pytest.mark.parametrize('B', [128, 130, 9])
+@pytest.mark.parametrize('B', [128, 120, 9])
 def test_persistent_bf16_d1024(hip, B):
     cfg = recipe.CONFIGS['big']
     m, pred = build(cfg, 11, torch.bfloat16)
