@@ -55,8 +55,16 @@ template <> struct GmT<float> {
     typedef floatx4 frag;
 };
 
-__device__ __forceinline__ void gm_put(u64* p, uint32_t tag, uint32_t v) {
-    __hip_atomic_store(p, ((u64)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Granule store.  Global mode: sc1 (write-through) store, visible to every XCD.  Local mode
+// (the census proved every member of the group runs on this workgroup's XCD): a plain
+// store, which completes into the XCD's shared L2 and keeps the line there, so the sc1
+// (L1-bypassing) polls of the other members hit L2 instead of the Infinity Fabric.
+__device__ __forceinline__ void gm_put(u64* p, uint32_t tag, uint32_t v, bool local) {
+    const u64 x = ((u64)tag << 32) | v;
+    if (local)
+        __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else
+        __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ u64 gm_get(const u64* p) {
     return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -155,7 +163,58 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int D = a.D, R = a.R, CW = a.CW, NZ = a.NZ, FS0 = a.FS0, B = a.B;
-    const int g = blockIdx.x % a.G, p = blockIdx.x / a.G;
+    // ---- group / member of this workgroup
+    // Static map: group = block % G (one XCD under round-robin dealing, speed only) with sc1
+    // hand-offs.  XCD census (a.census): every workgroup reads its XCC id and takes a slot on
+    // its XCD; once all arrived, if every XCD holds whole groups (count % P == 0) the groups
+    // are formed per XCD and hand-offs stay in that XCD's L2 (local mode).  All workgroups
+    // read the same final counts, so they all take the same decision.
+    // (the 16-B word block at the very end of the dynamic LDS; no static __shared__: it would
+    //  shift the 16-B alignment of the dynamic base)
+    int* gsh = (int*)(smem + ((((size_t)gm::Q * a.CW * sizeof(T) + 15) & ~(size_t)15) +
+                              (size_t)min(gm::NW, (a.D + UK - 1) / UK) *
+                                  max(a.CW / 16, a.NZ / 16) * 64 * sizeof(floatx4) +
+                              (size_t)a.R * gm::HIST * 4));
+    if (tid == 0) {
+        int gg = blockIdx.x % a.G, pp = blockIdx.x / a.G, loc = 0;
+        if (a.census) {
+            const int n = (*a.base + a.off - a.L) / FS0;          // launch index in this call
+            int* cur = a.census + (n & 1) * 16;
+            unsigned xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+            xcc &= 7;
+            const int slot = __hip_atomic_fetch_add(cur + xcc, 1, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_add(cur + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (blockIdx.x == 0)          // the next launch's census array (last used 2 ago)
+                for (int j = 0; j < 9; ++j)
+                    __hip_atomic_store(a.census + ((n + 1) & 1) * 16 + j, 0, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            int spins = 0;
+            bool all = false;
+            while (!(all = __hip_atomic_load(cur + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+                           (int)gridDim.x)) {
+                if (gm_spin_fail(spins, a.err, 0)) break;
+            }
+            if (all) {
+                int cnt[8], ok = 1, before = 0;
+                for (int x = 0; x < 8; ++x) {
+                    cnt[x] = __hip_atomic_load(cur + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok &= cnt[x] % a.P == 0;
+                    if (x < (int)xcc) before += cnt[x];
+                }
+                if (ok) {
+                    gg = before / a.P + slot / a.P;
+                    pp = slot % a.P;
+                    loc = 1;
+                }
+            }
+        }
+        gsh[0] = gg; gsh[1] = pp; gsh[2] = loc;
+    }
+    __syncthreads();
+    const int g = gsh[0], p = gsh[1];
+    const bool local = gsh[2] != 0;
     const int c0 = p * CW, z0 = p * NZ;
     const int NU = (D + UK - 1) / UK;
     const int KW = min(gm::NW, NU);
@@ -165,8 +224,9 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     // optional phase timestamps (workgroup 0, thread 0; s_memrealtime = 100 MHz)
     unsigned long long* dg = (a.diag && blockIdx.x == 0 && tid == 0) ? a.diag : nullptr;
     int nd = 0;
-#define GM_STAMP() do { if (dg && nd < 512) dg[nd++] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define GM_STAMP() do { if (dg && nd < 511) dg[nd++] = __builtin_amdgcn_s_memrealtime(); } while (0)
     GM_STAMP();
+    if (dg) dg[511] = local ? 1 : 2;
     // LDS: [tab15 Q x CW][red KW x ntm x 64 floatx4][hist R x HIST]
     T* tab15 = (T*)smem;
     size_t lo = ((size_t)Q * CW * sizeof(T) + 15) & ~(size_t)15;
@@ -285,9 +345,9 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         if (GV == 2) {
             const uint32_t mine = gm_bf16_bits(v);
             const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
-            if (own && (ec & 1) == 0) gm_put(dst + (size_t)er * DG + (c0 + ec) / 2, i, mine | (nb << 16));
+            if (own && (ec & 1) == 0) gm_put(dst + (size_t)er * DG + (c0 + ec) / 2, i, mine | (nb << 16), local);
         } else if (own) {
-            gm_put(dst + (size_t)er * DG + c0 + ec, i, gm_bits(v));
+            gm_put(dst + (size_t)er * DG + c0 + ec, i, gm_bits(v), local);
         }
     };
 
@@ -337,9 +397,9 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 const uint32_t mine = gm_bf16_bits(v);
                 const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
                 if (own && (ec & 1) == 0)
-                    gm_put(dst + (size_t)er * DG + (c0 + ec) / 2, tag, mine | (nb << 16));
+                    gm_put(dst + (size_t)er * DG + (c0 + ec) / 2, tag, mine | (nb << 16), local);
             } else if (own) {
-                gm_put(dst + (size_t)er * DG + c0 + ec, tag, gm_bits(v));
+                gm_put(dst + (size_t)er * DG + c0 + ec, tag, gm_bits(v), local);
             }
             __syncthreads();                   // red is reused by the next phase
         }
@@ -370,7 +430,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 float v = 0.f;
                 for (int kw = 0; kw < KW; ++kw) v += red[(kw * ntm + t) * 64 + ln][ii];
                 gm_put(a.xz + ((size_t)g * R + r) * Q + z0 + c, tag,
-                       gm_bits(v + (e < gm::NTHR ? bo : a.b_out[z0 + c])));
+                       gm_bits(v + (e < gm::NTHR ? bo : a.b_out[z0 + c])), local);
             }
             __syncthreads();
         }
@@ -467,8 +527,10 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     size_t lds = ((size_t)gm::Q * CW * es + 15) & ~(size_t)15;
     lds += (size_t)KW * ntm * 64 * 16;
     lds += (size_t)R * gm::HIST * 4;
+    lds += 16;                                        // group / member / mode words
     if (lds > 160 * 1024) return 0;
     pl->ok = 1;
+    pl->local = env_flag("SRNN_GEN_LOCAL", 1);
     pl->dtype = dtype;
     pl->R = R;
     pl->G = cdiv(B, R);
@@ -493,7 +555,8 @@ extern "C" int srnn_gen_diag_dump(void) {
     if (!gm_diag_buf() || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(h, gm_diag_buf(), sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
         return 1;
-    for (int k = 1; k < 512 && h[k]; ++k)
+    fprintf(stderr, "gen_mlp diag mode: %s\n", h[511] == 1 ? "xcd-local" : "static map");
+    for (int k = 1; k < 511 && h[k]; ++k)
         fprintf(stderr, "gen_mlp diag %3d: +%8.2f us\n", k, (double)(h[k] - h[k - 1]) / 100.0);
     return 0;
 }
@@ -505,6 +568,7 @@ int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
     a.P = pl->P;
     a.CW = pl->CW;
     a.NZ = pl->NZ;
+    if (!pl->local) a.census = nullptr;
     {
         // SRNN_GEN_DIAG=1: phase timestamps of the first launch into a device buffer that
         // srnn_gen_diag_dump prints (timing diagnostics only)

@@ -116,7 +116,7 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
     b->gm_bytes = 0;
     if (pl && pl->ok) {
         const size_t start = off;
-        b->gerr = (int*)take(256);
+        b->gerr = (int*)take(512);           // [0] error word, [64..96) XCD census
         b->xa1 = (unsigned long long*)take(pl->xa_words * 8);
         b->xa2 = (unsigned long long*)take(pl->xa_words * 8);
         b->xz = (unsigned long long*)take(pl->xz_words * 8);
@@ -229,6 +229,7 @@ int run_block(Ctx& c, int periods) {
             a.base = c.b.base; a.off = off; a.nsteps = m->tier[0].frame_size; a.L = c.L;
             a.B = c.B; a.D = m->dim; a.FS0 = m->tier[0].frame_size;
             a.xa1 = c.b.xa1; a.xa2 = c.b.xa2; a.xz = c.b.xz; a.err = c.b.gerr;
+            a.census = c.b.gerr + 64;
             RET(gen_mlp_launch(c.pl, a, c.s));
         }
     }

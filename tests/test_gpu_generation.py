@@ -87,3 +87,19 @@ def test_persistent_philox_matches_per_sample_fp32(hip):
     s0, l0 = generate(m, B, cond, spk, False, sampler='philox', seed=99)
     assert torch.equal(s1, s0)
     torch.testing.assert_close(l1, l0, atol=1e-4, rtol=0)
+
+
+def test_persistent_static_map_mode(hip, monkeypatch):
+    """SRNN_GEN_LOCAL=0: groups by block index with write-through (sc1) hand-offs instead of
+    the XCD census; same index stream as the per-sample path."""
+    monkeypatch.setenv('SRNN_GEN_LOCAL', '0')
+    cfg = dict(recipe.CONFIGS['t3'], dim=256)
+    m, _ = build(cfg, 5, torch.float32)
+    B, n_cond = 64, 2
+    cond = recipe.synth_cond((B, n_cond, cfg['cond_dim']), 8)
+    spk = np.arange(B) % cfg['spk_dim']
+    noise = torch.from_numpy(recipe.synth_noise((n_cond * 64, B, 256), 2))
+    s1, l1 = generate(m, B, cond, spk, True, noise=noise)
+    s0, l0 = generate(m, B, cond, spk, False, noise=noise)
+    assert torch.equal(s1, s0)
+    torch.testing.assert_close(l1, l0, atol=1e-4, rtol=0)
