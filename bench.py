@@ -6,7 +6,8 @@ frame_sizes [16, 4], 6-speaker + 43-d Ahocoder conditioning, T = 1024, B = 128 r
 GPU, bf16 MFMA (fp32 master weights / recurrences), one step = forward + backward +
 (all-reduce) + clipped Adam.  Weak scaling: every rank owns its own 128 stream rows.
 The line also carries `tbptt_steps_per_s`, the generation throughput of configs[2]
-(128 utterances x 3 s per GPU, replicas only), the roofline of the dominant kernel
+(128 utterances x 3 s per GPU, replicas only; `gen` = bf16 through the persistent sample
+loop, `gen_fp32` = the parity-grade fp32 path), the roofline of the dominant kernel
 (measured with HIP events on the launching stream) and a bounded CPU baseline.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--no-gen] [--no-cpu]
@@ -203,7 +204,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--batch', type=int, default=128)
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
-    ap.add_argument('--gen-dtype', default='fp32', choices=['bf16', 'fp32'])
+    ap.add_argument('--gen-dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--no-gen-fp32', action='store_true')
     ap.add_argument('--gen-seqs', type=int, default=128)
     ap.add_argument('--gen-cond', type=int, default=750)
     ap.add_argument('--no-gen', action='store_true')
@@ -227,30 +229,41 @@ def main():
     del pred, m
     torch.cuda.empty_cache()
 
-    gen = None
-    if not args.no_gen:
-        gdt = torch.bfloat16 if args.gen_dtype == 'bf16' else torch.float32
+    def gen_line(dname):
+        gdt = torch.bfloat16 if dname == 'bf16' else torch.float32
         t = run_gen(args, dev, args.gen_seqs, args.gen_cond, gdt)
         t = D.max_over_ranks(t, dev)
         gs = N * args.gen_seqs * args.gen_cond * 64 / t
         steps_per_s = args.gen_cond * 64 / t
         # algorithmic bytes per generation step: weights read once per step,
         # tiers amortised by their clocks, + per-row activations
-        es = 2 if args.gen_dtype == 'bf16' else 4
+        es = 2 if dname == 'bf16' else 4
         W_step = 5571840 + 23110656 / 16 + 10616868 / 64
         bytes_step = es * W_step + args.gen_seqs * (4 * (1024 + 256) + 8 * 16 + 8)
-        gen = {'value': round(gs, 1), 'unit': 'samples/s', 'x_realtime': round(gs / 16000, 1),
-               'x_realtime_per_gpu': round(gs / 16000 / N, 1), 'dtype': args.gen_dtype,
-               'seconds': round(t, 3), 'steps_per_s': round(steps_per_s, 1),
-               'config': {'workload': 'generate 3-tier dim1024 FS=[16,4], %d utt x %d cond '
-                                      'rows (%d samples) per GPU, Philox sampler'
-                                      % (args.gen_seqs, args.gen_cond, args.gen_cond * 64)},
-               'roofline': {'bound': 'hbm', 'achieved': round(bytes_step * steps_per_s / 1e9, 1),
-                            'peak': MI355X_HBM_TBS * 1000, 'unit': 'GB/s',
-                            'frac': round(bytes_step * steps_per_s / 1e9 / (MI355X_HBM_TBS * 1000),
-                                          4),
-                            'traffic': None}}
-        log('gen: %.3f s, %.0f samples/s (%.1fx realtime)' % (t, gs, gs / 16000))
+        import samplernn_hip as H
+        rows_pg = H.gen_persistent_rows(gdt, args.gen_seqs, 1024, 16)
+        log('gen %s: %.3f s, %.0f samples/s (%.1fx realtime)' % (dname, t, gs, gs / 16000))
+        return {'value': round(gs, 1), 'unit': 'samples/s', 'x_realtime': round(gs / 16000, 1),
+                'x_realtime_per_gpu': round(gs / 16000 / N, 1), 'dtype': dname,
+                'seconds': round(t, 3), 'steps_per_s': round(steps_per_s, 1),
+                'us_per_step': round(1e6 / steps_per_s, 2),
+                'sample_loop': ('persistent (gen_mlp.hip, %d rows/group)' % rows_pg) if rows_pg
+                               else 'per-sample kernels (hipGraph)',
+                'config': {'workload': 'generate 3-tier dim1024 FS=[16,4], %d utt x %d cond '
+                                       'rows (%d samples) per GPU, Philox sampler'
+                                       % (args.gen_seqs, args.gen_cond, args.gen_cond * 64)},
+                'roofline': {'bound': 'hbm',
+                             'achieved': round(bytes_step * steps_per_s / 1e9, 1),
+                             'peak': MI355X_HBM_TBS * 1000, 'unit': 'GB/s',
+                             'frac': round(bytes_step * steps_per_s / 1e9 /
+                                           (MI355X_HBM_TBS * 1000), 4),
+                             'traffic': None}}
+
+    gen = gen_fp32 = None
+    if not args.no_gen:
+        gen = gen_line(args.gen_dtype)
+        if args.gen_dtype != 'fp32' and not args.no_gen_fp32:
+            gen_fp32 = gen_line('fp32')       # parity-grade numerics (bit-replay tests)
 
     # dominant kernel of the TBPTT step: the MLP hidden layer GEMM (B*T x D x D, bf16)
     tdt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
@@ -281,7 +294,7 @@ def main():
                            'global_batch': N * rows, 'seq_len': 1024,
                            'parallelism': 'dp%d' % N},
                 'tbptt_steps_per_s': round(args.steps / dt, 3),
-                'roofline': roof, 'cpu_baseline': cpu, 'gen': gen,
+                'roofline': roof, 'cpu_baseline': cpu, 'gen': gen, 'gen_fp32': gen_fp32,
                 'final_loss': round(losses[-1], 4)}
         print(json.dumps(line), flush=True)
     D.barrier()
