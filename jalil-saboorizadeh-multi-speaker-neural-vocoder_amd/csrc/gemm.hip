@@ -72,9 +72,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 // Skinny NT path (M = batch rows, e.g. the generation loop's y = x W^T with M = 128):
 // small tiles so >= 256 workgroups exist, and the deep glds ring of ring_core.hpp so a
 // workgroup's K chain is not one exposed memory latency per stage.
-template <typename T, typename TO, int BM, int BN, int WM, int WN, int WK>
+template <typename T, typename TO, int BM, int BN, int WM, int WN, int WK, int NS = 4>
 __global__ __launch_bounds__(256) void skinny_kernel(GemmArgs g) {
-    typedef Ring<T, BM, BN, WM, WN, WK, 4> R;
+    typedef Ring<T, BM, BN, WM, WN, WK, NS> R;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
     floatx4 acc[R::FM][R::FN];
@@ -82,9 +82,9 @@ __global__ __launch_bounds__(256) void skinny_kernel(GemmArgs g) {
     for (int i = 0; i < R::FM; ++i)
 #pragma unroll
         for (int j = 0; j < R::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-    ring_core<T, BM, BN, WM, WN, WK, 4>((const T*)g.A, g.lda, RowClamp{m0, g.M}, (const T*)g.B,
-                                        g.ldb, RowClamp{n0, g.N}, g.K, smem, acc);
-    ring_reduce<T, BM, BN, WM, WN, WK, 4>(smem, acc);
+    ring_core<T, BM, BN, WM, WN, WK, NS>((const T*)g.A, g.lda, RowClamp{m0, g.M}, (const T*)g.B,
+                                         g.ldb, RowClamp{n0, g.N}, g.K, smem, acc);
+    ring_reduce<T, BM, BN, WM, WN, WK, NS>(smem, acc);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
     if (wk != 0) return;
@@ -111,8 +111,30 @@ __global__ __launch_bounds__(256) void skinny_kernel(GemmArgs g) {
         }
 }
 
+// all M (<= 128) rows in one tile, so every weight row streams through the chip ONCE (the
+// generation loop's upsampling, 128 x 16384 x 1024): 128 x 64 tiles with a 3-stage ring
+// (144 KiB) when that still gives >= 256 tiles, else 128 x 32 with 4 stages (160 KiB)
+template <typename T, typename TO, int BN, int WM, int WN, int NS>
+static int launch_skinny_rows(const GemmArgs& g, hipStream_t s) {
+    typedef Ring<T, 128, BN, WM, WN, 1, NS> R;
+    auto k = skinny_kernel<T, TO, 128, BN, WM, WN, 1, NS>;
+    static bool attr = false;
+    if (!attr) {
+        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, R::LDS));
+        attr = true;
+    }
+    hipLaunchKernelGGL(k, dim3(cdiv(g.N, BN), 1), dim3(256), R::LDS, s, g);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
 template <typename T, typename TO>
 static int launch_skinny(const GemmArgs& g, hipStream_t s) {
+    if (g.M > 64 && g.M <= 128 && g.N >= 64 * 64 && env_flag("SRNN_SKINNY_ROWS", 1)) {
+        if (g.N >= 64 * 256) return launch_skinny_rows<T, TO, 64, 2, 2, 3>(g, s);
+        return launch_skinny_rows<T, TO, 32, 4, 1, 4>(g, s);
+    }
     // 32 x 16 tiles (waves: 2 along M, 2 along K) unless 32 x 32 already gives 512 tiles
     const int64_t t32 = (int64_t)cdiv(g.M, 32) * cdiv(g.N, 32);
     if (t32 >= 512) {

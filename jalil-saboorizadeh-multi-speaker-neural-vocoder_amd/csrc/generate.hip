@@ -27,25 +27,37 @@ int srnn_gru_cell_impl(int dtype, int B, int D, int Din, const void* x, int64_t 
                        const float* bhh, float* hout, int64_t ldho, void* hout_lp, int64_t ldhl,
                        float* gates, int64_t ldgt, hipStream_t s);
 
-// A_in[b, s] = 2*deq(seq[b, i - nfs + s]) (s < nfs);  A_in[b, nfs + c] = cond[b, j, c]
+// Fused tier input (build_input + input projection of one tier tick), one row per block:
+//   a[s] = 2*deq(seq[b, i - nfs + s]) (s < nfs) | cond[b, i/L - 1, s - nfs]   (rounded to T,
+//          as the GEMM path's T operand)
+//   x[b, o] = sum_s a[s] W_in[o, s] + bias[o] + add[b][o]
+// add = the top tier's per-row bias (speaker + cond/input biases) or the upper tier's
+// upsampled conditioning row (model.py:196-220).  in_dim <= 16 + cond_dim is small, so a
+// thread per output with the row's inputs in LDS beats a GEMM launch plus an input kernel.
 template <typename T>
-__global__ void build_input_kernel(const int64_t* __restrict__ seq, int64_t ldseq,
-                                   const int* __restrict__ base, int off, int nfs,
-                                   const float* __restrict__ lut2, const float* __restrict__ cond,
-                                   int n_cond, int C, int L, int B, T* __restrict__ A,
-                                   int in_dim) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= B * in_dim) return;
-    const int b = e / in_dim, s = e % in_dim;
+__global__ __launch_bounds__(256) void tier_input_kernel(
+    const int64_t* __restrict__ seq, int64_t ldseq, const int* __restrict__ base, int off,
+    int nfs, const float* __restrict__ lut2, const float* __restrict__ cond, int n_cond, int C,
+    int L, const T* __restrict__ w_in, int in_dim, const float* __restrict__ bias,
+    const float* __restrict__ add, int64_t ldadd, T* __restrict__ x, int D) {
+    extern __shared__ float av[];
+    const int b = blockIdx.x;
     const int i = *base + off;
-    float v;
-    if (s < nfs) {
-        v = lut2[seq[(int64_t)b * ldseq + i - nfs + s]];
-    } else {
-        const int j = i / L - 1;   // model.py:483
-        v = cond[((int64_t)b * n_cond + j) * C + (s - nfs)];
+    for (int s = threadIdx.x; s < in_dim; s += blockDim.x) {
+        float v;
+        if (s < nfs) v = lut2[seq[(int64_t)b * ldseq + i - nfs + s]];
+        else v = cond[((int64_t)b * n_cond + (i / L - 1)) * C + (s - nfs)];
+        av[s] = to_f(from_f<T>(v));
     }
-    A[(int64_t)b * in_dim + s] = from_f<T>(v);
+    __syncthreads();
+    for (int o = threadIdx.x; o < D; o += blockDim.x) {
+        const T* w = w_in + (int64_t)o * in_dim;
+        float acc = 0.f;
+        for (int s = 0; s < in_dim; ++s) acc += av[s] * to_f(w[s]);
+        if (bias) acc += bias[o];
+        acc += add[(int64_t)b * ldadd + o];
+        x[(int64_t)b * D + o] = from_f<T>(acc);
+    }
 }
 
 template <typename T>
@@ -66,7 +78,6 @@ constexpr size_t ALIGN = 256;
 inline size_t al(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
 
 struct Bufs {
-    void* A_in[SRNN_MAX_TIERS];
     void* x[SRNN_MAX_TIERS];
     float* h[SRNN_MAX_TIERS][SRNN_MAX_RNN][2];
     void* hlp[SRNN_MAX_TIERS][SRNN_MAX_RNN][2];
@@ -97,7 +108,6 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
     };
     for (int k = 0; k < m->n_tiers; ++k) {
         const SrnnTier& t = m->tier[k];
-        b->A_in[k] = take((size_t)B * t.in_dim * es);
         b->x[k] = take((size_t)B * D * es);
         for (int l = 0; l < m->n_rnn; ++l)
             for (int p = 0; p < 2; ++p) {
@@ -149,30 +159,32 @@ int tier_tick(Ctx& c, int k, int off, int par) {
     const int D = m->dim, B = c.B, dt = m->dtype;
     const bool top = (k == m->n_tiers - 1);
     const bool lp = dt != SRNN_F32;
-    // 1. input rows
+    // 1. x = A_in . W_in^T + (top: row_bias ; lower: b_in + upper-tier conditioning row)
     {
-        const int n = B * t.in_dim;
+        const float* add;
+        int64_t ldadd;
+        const float* bias;
+        if (top) {
+            add = c.row_bias; ldadd = D; bias = nullptr;
+        } else {
+            const SrnnTier& u = m->tier[k + 1];
+            // frame_index = (i // nfs_k) % FS_{k+1}  (model.py:491-492); base is a multiple of L
+            const int fi = (off / t.n_frame_samples) % u.frame_size;
+            add = c.b.up[k + 1] + (size_t)fi * D; ldadd = (int64_t)u.frame_size * D;
+            bias = t.b_in;
+        }
+        const size_t lds = (size_t)t.in_dim * sizeof(float);
         if (dt == SRNN_F32)
-            hipLaunchKernelGGL((build_input_kernel<float>), dim3(cdiv(n, 256)), dim3(256), 0, c.s,
-                               c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.cond,
-                               c.n_cond, m->cond_dim, c.L, B, (float*)c.b.A_in[k], t.in_dim);
+            hipLaunchKernelGGL((tier_input_kernel<float>), dim3(B), dim3(256), lds, c.s, c.seq,
+                               c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.cond,
+                               c.n_cond, m->cond_dim, c.L, (const float*)t.w_in, t.in_dim, bias,
+                               add, ldadd, (float*)c.b.x[k], D);
         else
-            hipLaunchKernelGGL((build_input_kernel<bf16>), dim3(cdiv(n, 256)), dim3(256), 0, c.s,
-                               c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.cond,
-                               c.n_cond, m->cond_dim, c.L, B, (bf16*)c.b.A_in[k], t.in_dim);
+            hipLaunchKernelGGL((tier_input_kernel<bf16>), dim3(B), dim3(256), lds, c.s, c.seq,
+                               c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.cond,
+                               c.n_cond, m->cond_dim, c.L, (const bf16*)t.w_in, t.in_dim, bias,
+                               add, ldadd, (bf16*)c.b.x[k], D);
         SRNN_LAUNCH_CHECK();
-    }
-    // 2. x = A_in . W_in^T + (top: row_bias ; lower: b_in + upper-tier conditioning row)
-    if (top) {
-        RET(linear_fwd(dt, dt, B, D, t.in_dim, c.b.A_in[k], t.in_dim, t.w_in, t.in_dim, nullptr,
-                       c.b.x[k], D, 0, c.s, 1.f, c.row_bias, D));
-    } else {
-        const SrnnTier& u = m->tier[k + 1];
-        // frame_index = (i // nfs_k) % FS_{k+1}  (model.py:491-492); base is a multiple of L
-        const int fi = (off / t.n_frame_samples) % u.frame_size;
-        RET(linear_fwd(dt, dt, B, D, t.in_dim, c.b.A_in[k], t.in_dim, t.w_in, t.in_dim, t.b_in,
-                       c.b.x[k], D, 0, c.s, 1.f, c.b.up[k + 1] + (size_t)fi * D,
-                       (int64_t)u.frame_size * D));
     }
     // 3. GRU layers
     const int cur = par, nxt = par ^ 1;

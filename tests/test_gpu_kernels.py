@@ -231,7 +231,8 @@ def test_segsum(hip):
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('M,N,K', [(128, 1024, 1024), (67, 256, 512), (128, 40, 256),
-                                   (256, 2048, 256)])
+                                   (256, 2048, 256), (128, 16384, 1024), (100, 4096, 1024),
+                                   (65, 16448, 256)])
 def test_gemm_skinny_ring(hip, dtype, M, N, K):
     """Skinny NT deep-ring kernel (tile 4 forces it), with the full epilogue."""
     A, W = _rand(M, K, seed=1), _rand(N, K, seed=2)
