@@ -77,7 +77,8 @@ def run_tbptt(args, dev, dist_mod):
     dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
     m, pred = make_model(dtype)
     pred = pred.to(dev)
-    sync = dist_mod.GradAllReduce() if dist_mod.world() > 1 else None
+    sync = dist_mod.GradAllReduce(overlap_groups=dist_mod.readiness_groups(pred)) \
+        if dist_mod.world() > 1 else None
     opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3), grad_sync=sync)
     rows = slice(0, B)
     n_chunks = args.warmup + args.steps
@@ -110,7 +111,7 @@ def run_tbptt(args, dev, dist_mod):
     dt = time.perf_counter() - t0
     sys.stderr.write('tbptt host enqueue %.2f ms/step\n' % (t_host * 1e3 / max(args.steps, 1)))
     dt = dist_mod.max_over_ranks(dt, dev)
-    loss_vals = [float(l) for l in losses]
+    loss_vals = [float(l.detach()) if torch.is_tensor(l) else float(l) for l in losses]
     return dt, loss_vals, pred, m
 
 
@@ -274,7 +275,8 @@ def main():
     peak = MI355X_BF16_TFLOPS if args.dtype == 'bf16' else MI355X_FP32_TFLOPS
     roof = {'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
             'frac': round(ach / peak, 4),
-            'traffic': pmc_traffic('gemm3p_kernel') if args.dtype == 'bf16' else None,
+            'traffic': pmc_traffic('gemm3p_kernel') if (args.dtype == 'bf16' and rows == 128)
+            else None,
             'traffic_algorithmic': 2 * (M_ * K_ + N_ * K_ + M_ * N_),
             'kernel': 'gemm_kernel (MLP hidden layer %dx%dx%d %s, relu epilogue), %.3f ms/launch'
                       % (M_, N_, K_, args.dtype, kms)}

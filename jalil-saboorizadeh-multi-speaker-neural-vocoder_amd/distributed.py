@@ -66,30 +66,56 @@ def shard_rows(total_rows, r=None, n=None):
     return slice(r * per, (r + 1) * per)
 
 
+def readiness_groups(model):
+    """Parameters of a SampleRNN (or Predictor) in the order backward produces their grads:
+    the sample-level MLP first, then the tiers bottom -> top; the learned h0 rows last (they
+    only get a gradient on reset chunks, so they must not hold a bucket back)."""
+    m = getattr(model, 'model', model)
+    groups = [[p for p in m.sample_level_mlp.parameters() if p.requires_grad]]
+    h0 = []
+    for rnn in m.frame_level_rnns:
+        ps = []
+        for name, p in rnn.named_parameters():
+            if not p.requires_grad:
+                continue
+            (h0 if name == 'h0' else ps).append(p)
+        groups.append(ps)
+    groups.append(h0)
+    return [g for g in groups if g]
+
+
 class GradAllReduce:
     """Average gradients across ranks in flat buckets of ~bucket_mb, in place.
 
     Used as `gradient_clipping(..., grad_sync=GradAllReduce())`: runs after the closure's
     backward and before the clamp + Adam.  Parameters without a grad contribute zeros
     (torch-0.4 zero_grad semantics), so every rank reduces identical bucket layouts.
+
+    overlap_groups (e.g. readiness_groups(model)): parameter groups in the order backward
+    completes them.  A post-accumulate-grad hook packs a group's bucket and starts its
+    all-reduce asynchronously (RCCL on its own stream, ordered after the producing kernels)
+    as soon as the group's last gradient lands, so the MLP's and the bottom tier's
+    reductions run under the rest of the backward; __call__ then only waits.  Groups whose
+    grads never arrive this step (h0 on non-reset chunks) are reduced at the sync point.
+    The reduced values are identical to the non-overlapped path (same buckets, same sums).
     """
 
-    def __init__(self, bucket_mb=64, group=None):
+    def __init__(self, bucket_mb=64, group=None, overlap_groups=None):
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.group = group
         self._bufs = {}
+        self._groups = None
+        self._hooks = []
+        self._pending = {}
+        if overlap_groups is not None and dist.is_available() and dist.is_initialized() and \
+                dist.get_world_size(group) > 1:
+            self._install(overlap_groups)
 
-    def __call__(self, optimizer):
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
-            return
-        n = dist.get_world_size(self.group)
-        params = [p for g in optimizer.param_groups for p in g['params'] if p.requires_grad]
-        for p in params:
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
+    # ---- bucketing
+    def _split(self, params):
         buckets, cur, size = [], [], 0
         for p in params:
-            nb = p.numel() * p.grad.element_size()
+            nb = p.numel() * p.element_size()
             if cur and size + nb > self.bucket_bytes:
                 buckets.append(cur)
                 cur, size = [], 0
@@ -97,25 +123,81 @@ class GradAllReduce:
             size += nb
         if cur:
             buckets.append(cur)
-        for bi, bucket in enumerate(buckets):
-            total = sum(p.numel() for p in bucket)
-            key = (bi, total, bucket[0].grad.dtype, bucket[0].grad.device)
-            flat = self._bufs.get(key)
-            if flat is None:
-                flat = torch.empty(total, dtype=bucket[0].grad.dtype, device=bucket[0].grad.device)
-                self._bufs[key] = flat
-            off = 0
-            for p in bucket:
-                k = p.numel()
+        return buckets
+
+    def _flat(self, key, bucket):
+        total = sum(p.numel() for p in bucket)
+        k = (key, total, bucket[0].dtype, bucket[0].device)
+        flat = self._bufs.get(k)
+        if flat is None:
+            flat = torch.empty(total, dtype=bucket[0].dtype, device=bucket[0].device)
+            self._bufs[k] = flat
+        return flat
+
+    def _launch(self, key, bucket, async_op):
+        flat = self._flat(key, bucket)
+        off = 0
+        for p in bucket:
+            k = p.numel()
+            if p.grad is None:
+                flat[off:off + k].zero_()
+            else:
                 flat[off:off + k].copy_(p.grad.reshape(-1))
-                off += k
-            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
-            flat.mul_(1.0 / n)
-            off = 0
+            off += k
+        work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+        return flat, work
+
+    def _unpack(self, bucket, flat, n):
+        flat.mul_(1.0 / n)
+        off = 0
+        for p in bucket:
+            k = p.numel()
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            p.grad.copy_(flat[off:off + k].view_as(p.grad))
+            off += k
+
+    # ---- overlapped mode
+    def _install(self, groups):
+        self._groups = []
+        for gi, params in enumerate(groups):
+            for bi, bucket in enumerate(self._split(params)):
+                self._groups.append(((gi, bi), bucket))
+        self._owner = {}
+        for idx, (_, bucket) in enumerate(self._groups):
             for p in bucket:
-                k = p.numel()
-                p.grad.copy_(flat[off:off + k].view_as(p.grad))
-                off += k
+                self._owner[id(p)] = idx
+        self._ready = [0] * len(self._groups)
+        for idx, (_, bucket) in enumerate(self._groups):
+            for p in bucket:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    def _on_grad(self, p):
+        idx = self._owner[id(p)]
+        self._ready[idx] += 1
+        key, bucket = self._groups[idx]
+        if self._ready[idx] == len(bucket) and idx not in self._pending:
+            self._pending[idx] = self._launch(key, bucket, True)
+
+    def __call__(self, optimizer):
+        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+            return
+        n = dist.get_world_size(self.group)
+        if self._groups is not None:
+            for idx, (key, bucket) in enumerate(self._groups):
+                if idx not in self._pending:          # grads that never arrived this step
+                    self._pending[idx] = self._launch(key, bucket, True)
+            for idx, (key, bucket) in enumerate(self._groups):
+                flat, work = self._pending[idx]
+                work.wait()
+                self._unpack(bucket, flat, n)
+            self._pending = {}
+            self._ready = [0] * len(self._groups)
+            return
+        params = [p for g in optimizer.param_groups for p in g['params'] if p.requires_grad]
+        for bi, bucket in enumerate(self._split(params)):
+            flat, _ = self._launch(bi, bucket, False)
+            self._unpack(bucket, flat, n)
 
 
 def barrier():

@@ -216,7 +216,8 @@ def main(exp, frame_sizes, dataset, **params):
     if params['scheduler']:
         from torch.optim.lr_scheduler import MultiStepLR
         scheduler = MultiStepLR(optimizer, milestones=[15, 35], gamma=0.1)
-    sync = dist_mod.GradAllReduce() if dist_mod.world() > 1 else None
+    sync = dist_mod.GradAllReduce(overlap_groups=dist_mod.readiness_groups(predictor)) \
+        if dist_mod.world() > 1 else None
     optimizer = gradient_clipping(optimizer, grad_sync=sync)
     rows = dist_mod.shard_rows(params['batch_size']) if dist_mod.world() > 1 else None
     data_loader = make_data_loader(model.lookback, params, rows)

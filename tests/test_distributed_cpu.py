@@ -69,14 +69,19 @@ def _train(model, data, rows, grad_sync):
     return losses, [p.detach().clone() for p in model.parameters()]
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, overlap=False):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import distributed as D
     D.init(backend='gloo')
     data = _data()
     rows = D.shard_rows(data.shape[1])
-    losses, params = _train(_Toy(), data, rows, D.GradAllReduce(bucket_mb=0.0001))
+    model = _Toy()
+    # overlapped mode: hooks start each group's all-reduce when its last grad lands; h0 in
+    # its own group (it has no grad on non-reset chunks in the real model)
+    groups = [[model.U], [model.W], [model.h0]] if overlap else None
+    losses, params = _train(model, data, rows,
+                            D.GradAllReduce(bucket_mb=0.0001, overlap_groups=groups))
     loss_t = torch.tensor(losses)
     dist.all_reduce(loss_t)
     if rank == 0:
@@ -84,11 +89,12 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_dp_two_ranks_equals_full_batch():
+@pytest.mark.parametrize('overlap', [False, True])
+def test_dp_two_ranks_equals_full_batch(overlap):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
     for p in procs:
         p.start()
     losses_dp, params_dp = q.get(timeout=120)
