@@ -73,6 +73,18 @@ int srnn_gru_cell_bwd(int dtype, int B, int D, const float* dy, int64_t lddy,
  * work: >= (64 * ceil(B/32) + 1) ints (zeroed by the call; the last word is an error flag
  * raised if a workgroup gave up waiting).  srnn_gru_seq_supported returns 1 / 0.       */
 int srnn_gru_seq_supported(int dtype, int B, int D);
+/* Whole-sequence GRU forward of one layer as ONE persistent launch with row groups of 16
+ * placed per XCD (gru_xcd.hip): W_hh resident in VGPRs, h hand-offs as data-tagged granules
+ * in the XCD's L2.  Same operands and outputs as srnn_gru_seq_fwd (torch.nn.GRU recurrence,
+ * model.py:148-165 / 244), gi includes b_ih; work = srnn_gru_xcd_work_bytes(dtype, B, D) bytes
+ * (0 = shape or device not supported; zeroed by the call).  srnn_gru_xcd_error(work)
+ * synchronises and returns nonzero if a hand-off was given up (bounded spin). */
+size_t srnn_gru_xcd_work_bytes(int dtype, int B, int D);
+int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi, int64_t sgi,
+                     const float* h0, const void* whh, const float* bhh, float* out,
+                     void* out_lp, int64_t ldo, int64_t so, float* gates, int64_t ldg,
+                     int64_t sg, void* work, size_t work_bytes, void* stream);
+int srnn_gru_xcd_error(const void* work);
 int srnn_gru_seq_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
                      int64_t sgi, const float* h0, const void* h0_lp, const void* whh,
                      const float* bhh, float* out, void* out_lp, int64_t ldo, int64_t so,

@@ -32,16 +32,15 @@
 #include "samplernn_hip_internal.hpp"
 #include "sampler.hpp"
 #include "gen_mlp.hpp"
+#include "handoff.hpp"
 
 namespace gm {
 constexpr int NW = 8;                  // waves per workgroup (the K split of both GEMMs)
 constexpr int NTHR = NW * 64;
 constexpr int Q = 256;
 constexpr int HIST = 32;               // sample history ring per row (FS0 <= 32)
-constexpr int SPIN_LIMIT = 1 << 20;    // polls (each >= one L2 round trip): ~ a second
 }  // namespace gm
 
-typedef unsigned long long u64;
 
 template <typename T> struct GmT;
 template <> struct GmT<bf16> {
@@ -55,17 +54,6 @@ template <> struct GmT<float> {
     typedef floatx4 frag;
 };
 
-// Granule store.  Global mode: sc1 (write-through) store, visible to every XCD.  Local mode
-// (the census proved every member of the group runs on this workgroup's XCD): a plain
-// store, which completes into the XCD's shared L2 and keeps the line there, so the sc1
-// (L1-bypassing) polls of the other members hit L2 instead of the Infinity Fabric.
-__device__ __forceinline__ void gm_put(u64* p, uint32_t tag, uint32_t v, bool local) {
-    const u64 x = ((u64)tag << 32) | v;
-    if (local)
-        __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    else
-        __hip_atomic_store(p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 __device__ __forceinline__ u64 gm_get(const u64* p) {
     return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -93,31 +81,6 @@ __device__ __forceinline__ uint32_t gm_bf16_bits(float v) {
     return (uint32_t)__bfloat16_as_ushort(__float2bfloat16(v));
 }
 
-// Wait for granule tags: returns true once all equal `tag`; on timeout raises the error word.
-// Once the error word is set every later wait returns at its first re-check.
-__device__ __forceinline__ bool gm_spin_fail(int& spins, int* err, int lane) {
-    __builtin_amdgcn_s_sleep(1);
-    if (++spins > gm::SPIN_LIMIT) {
-        if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return true;
-    }
-    if ((spins & 31) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        return true;
-    return false;
-}
-
-// Buffer resource over a hand-off buffer: 16-B granule-pair loads with sc1 (L1 bypass)
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t gm_rsrc(const void* p) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff,
-                                             0x00020000);
-}
-__device__ __forceinline__ uint4 gm_get2(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 16 /*sc1*/);
-    uint4 u;
-    __builtin_memcpy(&u, &v, 16);
-    return u;
-}
-
 // A-operand fragments of one wave for one hand-off buffer (granules of row `row`, starting
 // at granule `rowg`): for unit j (global unit u = wave + NW*j) the lane's 16 data bytes are
 // 4 granules = two 16-B loads.  Spins until every tag == tag.
@@ -128,23 +91,29 @@ __device__ __forceinline__ void gm_fetch_a(__amdgpu_buffer_rsrc_t src, uint32_t 
     constexpr int GV = GmT<T>::GV, UK = GmT<T>::UK, EPL = UK / 4;
     int spins = 0;
     for (;;) {
+        // every load unconditional (clamped k), so all 2 x UPW are in flight at once; a
+        // branch per unit would put a vmcnt(0) between them
+        uint4 x[UPW][2];
+#pragma unroll
+        for (int j = 0; j < UPW; ++j) {
+            const int u = wave + gm::NW * j;
+            const int ke = min(u * UK + (lane >> 4) * EPL, D - EPL);
+            const uint32_t off = (rowg + (uint32_t)(ke / GV)) * 8u;
+            x[j][0] = hx_get2(src, off);
+            x[j][1] = hx_get2(src, off + 16);
+        }
         bool ok = true;
 #pragma unroll
         for (int j = 0; j < UPW; ++j) {
             const int u = wave + gm::NW * j;
-            const int ke = u * UK + (lane >> 4) * EPL;
-            if (rv && u < NU && ke < D) {
-                const uint32_t off = (rowg + (uint32_t)(ke / GV)) * 8u;
-                const uint4 x0 = gm_get2(src, off), x1 = gm_get2(src, off + 16);
-                w[j][0] = x0.x; w[j][1] = x0.z; w[j][2] = x1.x; w[j][3] = x1.z;
-                ok &= (x0.y == tag) & (x0.w == tag) & (x1.y == tag) & (x1.w == tag);
-            } else {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) w[j][e] = 0u;
-            }
+            const bool v = rv && u < NU && u * UK + (lane >> 4) * EPL < D;
+            w[j][0] = v ? x[j][0].x : 0u; w[j][1] = v ? x[j][0].z : 0u;
+            w[j][2] = v ? x[j][1].x : 0u; w[j][3] = v ? x[j][1].z : 0u;
+            ok &= !v || ((x[j][0].y == tag) & (x[j][0].w == tag) & (x[j][1].y == tag) &
+                         (x[j][1].w == tag));
         }
         if (__all(ok)) return;
-        if (gm_spin_fail(spins, err, lane)) return;
+        if (hx_spin_fail(spins, err, lane)) return;
     }
 }
 
@@ -180,35 +149,11 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         if (a.census) {
             const int n = (*a.base + a.off - a.L) / FS0;          // launch index in this call
             int* cur = a.census + (n & 1) * 16;
-            unsigned xcc;
-            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
-            xcc &= 7;
-            const int slot = __hip_atomic_fetch_add(cur + xcc, 1, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_fetch_add(cur + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (blockIdx.x == 0)          // the next launch's census array (last used 2 ago)
                 for (int j = 0; j < 9; ++j)
                     __hip_atomic_store(a.census + ((n + 1) & 1) * 16 + j, 0, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-            int spins = 0;
-            bool all = false;
-            while (!(all = __hip_atomic_load(cur + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
-                           (int)gridDim.x)) {
-                if (gm_spin_fail(spins, a.err, 0)) break;
-            }
-            if (all) {
-                int cnt[8], ok = 1, before = 0;
-                for (int x = 0; x < 8; ++x) {
-                    cnt[x] = __hip_atomic_load(cur + x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok &= cnt[x] % a.P == 0;
-                    if (x < (int)xcc) before += cnt[x];
-                }
-                if (ok) {
-                    gg = before / a.P + slot / a.P;
-                    pp = slot % a.P;
-                    loc = 1;
-                }
-            }
+            loc = hx_census(cur, a.P, a.err, gg, pp) ? 1 : 0;
         }
         gsh[0] = gg; gsh[1] = pp; gsh[2] = loc;
     }
@@ -233,7 +178,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     floatx4* red = (floatx4*)(smem + lo);
     lo += (size_t)KW * ntm * 64 * sizeof(floatx4);
     int* hist = (int*)(smem + lo);
-    const __amdgpu_buffer_rsrc_t rx1 = gm_rsrc(a.xa1), rx2 = gm_rsrc(a.xa2), rxz = gm_rsrc(a.xz);
+    const __amdgpu_buffer_rsrc_t rx1 = hx_rsrc(a.xa1), rx2 = hx_rsrc(a.xa2), rxz = hx_rsrc(a.xz);
 
     // ---- resident weights: B fragments of this wave's K units
     F wh[UPW][NT], wo[UPW][NZT];
@@ -345,9 +290,9 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         if (GV == 2) {
             const uint32_t mine = gm_bf16_bits(v);
             const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
-            if (own && (ec & 1) == 0) gm_put(dst + (size_t)er * DG + (c0 + ec) / 2, i, mine | (nb << 16), local);
+            if (own && (ec & 1) == 0) hx_put(dst + (size_t)er * DG + (c0 + ec) / 2, i, mine | (nb << 16), local);
         } else if (own) {
-            gm_put(dst + (size_t)er * DG + c0 + ec, i, gm_bits(v), local);
+            hx_put(dst + (size_t)er * DG + c0 + ec, i, gm_bits(v), local);
         }
     };
 
@@ -360,7 +305,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
 
     const int row = lane & 15;
     const bool rv = row < R;
-    const uint32_t rowg = (uint32_t)((g * R + row) * DG);
+    const uint32_t rowg = (uint32_t)((g * R + min(row, R - 1)) * DG);   // in-bounds for row >= R
     for (int s = 0; s < a.nsteps; ++s) {
         const int i = i0 + s;
         const uint32_t tag = (uint32_t)i;
@@ -390,16 +335,21 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             float v = 0.f;
             if (own) {
                 const int t = ec >> 4, ln = (er >> 2) * 16 + (ec & 15), ii = er & 3;
-                for (int kw = 0; kw < KW; ++kw) v += red[(kw * ntm + t) * 64 + ln][ii];
+                float pr[gm::NW];
+                #pragma unroll
+                for (int kw = 0; kw < gm::NW; ++kw)
+                    pr[kw] = red[(min(kw, KW - 1) * ntm + t) * 64 + ln][ii];
+                #pragma unroll
+                for (int kw = 0; kw < gm::NW; ++kw) v += kw < KW ? pr[kw] : 0.f;
                 v = fmaxf(v + bh, 0.f);
             }
             if (GV == 2) {
                 const uint32_t mine = gm_bf16_bits(v);
                 const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
                 if (own && (ec & 1) == 0)
-                    gm_put(dst + (size_t)er * DG + (c0 + ec) / 2, tag, mine | (nb << 16), local);
+                    hx_put(dst + (size_t)er * DG + (c0 + ec) / 2, tag, mine | (nb << 16), local);
             } else if (own) {
-                gm_put(dst + (size_t)er * DG + c0 + ec, tag, gm_bits(v), local);
+                hx_put(dst + (size_t)er * DG + c0 + ec, tag, gm_bits(v), local);
             }
             __syncthreads();                   // red is reused by the next phase
         }
@@ -428,8 +378,13 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 const int r = e / NZ, c = e % NZ;
                 const int t = c >> 4, ln = (r >> 2) * 16 + (c & 15), ii = r & 3;
                 float v = 0.f;
-                for (int kw = 0; kw < KW; ++kw) v += red[(kw * ntm + t) * 64 + ln][ii];
-                gm_put(a.xz + ((size_t)g * R + r) * Q + z0 + c, tag,
+                float pr[gm::NW];
+                #pragma unroll
+                for (int kw = 0; kw < gm::NW; ++kw)
+                    pr[kw] = red[(min(kw, KW - 1) * ntm + t) * 64 + ln][ii];
+                #pragma unroll
+                for (int kw = 0; kw < gm::NW; ++kw) v += kw < KW ? pr[kw] : 0.f;
+                hx_put(a.xz + ((size_t)g * R + r) * Q + z0 + c, tag,
                        gm_bits(v + (e < gm::NTHR ? bo : a.b_out[z0 + c])), local);
             }
             __syncthreads();
@@ -445,12 +400,12 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             floatx4 v;
             int spins = 0;
             for (;;) {
-                const uint4 x0 = gm_get2(rxz, zoff), x1 = gm_get2(rxz, zoff + 16);
+                const uint4 x0 = hx_get2(rxz, zoff), x1 = hx_get2(rxz, zoff + 16);
                 v = floatx4{__uint_as_float(x0.x), __uint_as_float(x0.z), __uint_as_float(x1.x),
                             __uint_as_float(x1.z)};
                 const bool ok = (x0.y == tag) & (x0.w == tag) & (x1.y == tag) & (x1.w == tag);
                 if (__all(ok)) break;
-                if (gm_spin_fail(spins, a.err, lane)) break;
+                if (hx_spin_fail(spins, a.err, lane)) break;
             }
             float* lrow = (p == 0 && valid && a.logp)
                               ? a.logp + ((int64_t)(i - a.L) * B + b) * Q : nullptr;

@@ -1,0 +1,299 @@
+// Whole-sequence GRU forward of one FrameLevelRNN layer (model.py:148-165, torch.nn.GRU
+// gate order [r | z | n]) as ONE persistent launch organised like the generation sample
+// loop (gen_mlp.hip): row groups that live on one XCD, weights resident in VGPRs,
+// data-tagged granule hand-offs through that XCD's L2.
+//
+// gru_seq.hip tiles 32 rows x 16 units per workgroup, so one row tile's 64 workgroups span
+// every XCD and each step's h hand-off (64 KiB per workgroup behind 64 step flags) crosses
+// the Infinity Fabric.  Here:
+//   * a group = 16 rows (one MFMA M tile) x all D units, split over P = D / 32 workgroups of
+//     32 units (B = 128, D = 1024: 8 groups x 32 = 256 workgroups, one group per XCD when the
+//     per-launch census (handoff.hpp) confirms the placement);
+//   * each of the 8 waves holds its K-slice of the workgroup's 96 W_hh rows (3 gates x 32
+//     units) as MFMA B fragments in VGPRs for the whole sequence (96 VGPRs at D = 1024);
+//   * per step every workgroup reads the group's h_{t-1} as 8-byte {2 x bf16, tag} granules
+//     (16 rows x D: 64 KiB, each wave its own K-slice) with sc1 loads -- the data is the flag
+//     -- and publishes its 16 x 32 slice of h_t the same way; h is double-buffered (a buffer
+//     is rewritten only after every member read the previous step from it);
+//   * gate math, outputs and saved gates are gru_seq's (fp32 state, bf16 MMA operands).
+#include "samplernn_hip_internal.hpp"
+#include "handoff.hpp"
+
+namespace gx {
+constexpr int NW = 8, NTHR = NW * 64;
+constexpr int RG = 16;                 // rows per group
+constexpr int CU = 32;                 // units per workgroup
+constexpr int NT = 6;                  // n tiles: 3 gates x 2 x 16 units
+constexpr int UK = 32;                 // k per bf16 MFMA unit
+}  // namespace gx
+
+struct GruXArgs {
+    const float* gi; int64_t ldgi; int64_t sgi;     // gi[b][t] (3D, includes b_ih)
+    const float* h0;                                // (B, D) fp32
+    const bf16* whh; const float* bhh;
+    float* out; bf16* out_lp; int64_t ldo; int64_t so;
+    float* gates; int64_t ldg; int64_t sg;          // r | z | n | gh_n per row and step
+    u64* xh;                                        // 2 x G x RG x D/2 granules
+    int* census;                                    // 9 zeroed words, or null (static map)
+    int* err;
+    int B, D, Fr, G, P;
+    unsigned long long* diag;                       // optional phase timestamps (timing only)
+};
+
+template <int UPW>
+__global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
+    using namespace gx;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int D = a.D, B = a.B;
+    const int NU = D / UK, KW = NW < NU ? NW : NU;
+    floatx4* red = (floatx4*)smem;                              // [KW][NT][64]
+    int* gsh = (int*)(smem + (size_t)KW * NT * 64 * sizeof(floatx4));
+    if (tid == 0) {
+        int g = blockIdx.x % a.G, p = blockIdx.x / a.G, loc = 0;
+        if (a.census) loc = hx_census(a.census, a.P, a.err, g, p) ? 1 : 0;
+        gsh[0] = g; gsh[1] = p; gsh[2] = loc;
+    }
+    __syncthreads();
+    const int g = gsh[0], p = gsh[1];
+    const bool local = gsh[2] != 0;
+    const int u0 = p * CU;
+    const int DG = D / 2;
+    unsigned long long* dg = (a.diag && blockIdx.x == 0 && tid == 0) ? a.diag : nullptr;
+    int nd = 0;
+#define GX_STAMP() do { if (dg && nd < 255) dg[nd++] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    if (dg) dg[255] = local ? 1 : 2;
+    // ---- resident W_hh fragments: unit j of this wave = k-range [(wave + NW j) * 32, +32)
+    bf16x8 wf[UPW][NT];
+    {
+        uint4 lw[UPW][NT];
+#pragma unroll
+        for (int j = 0; j < UPW; ++j) {
+            const int u = wave + NW * j;
+            const int ke = min(u * UK + (lane >> 4) * 8, D - 8);
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const int row = (t >> 1) * D + u0 + (t & 1) * 16 + (lane & 15);
+                lw[j][t] = *reinterpret_cast<const uint4*>(a.whh + (int64_t)row * D + ke);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UPW; ++j) {
+            const bool kv = wave + NW * j < NU;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                const uint4 v = kv ? lw[j][t] : make_uint4(0u, 0u, 0u, 0u);
+                __builtin_memcpy(&wf[j][t], &v, 16);
+            }
+        }
+    }
+    // ---- this thread's state element: row r of the group, unit u0 + uu
+    const int r = tid >> 5, uu = tid & 31;
+    const int b = min(g * RG + r, B - 1);
+    const bool wr = g * RG + r < B;
+    const int unit = u0 + uu;
+    const float bhr = a.bhh[unit], bhz = a.bhh[D + unit], bhn = a.bhh[2 * D + unit];
+    float hprev = a.h0[(int64_t)b * D + unit];
+    const __amdgpu_buffer_rsrc_t rx = hx_rsrc(a.xh);
+    const size_t bufw = (size_t)a.G * RG * DG;                  // granules per buffer
+    auto publish = [&](int s, float h) {        // h_s -> buffer (s + 1) & 1, tag s + 2
+        const uint32_t mine = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(h));
+        const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
+        if ((uu & 1) == 0)
+            hx_put(a.xh + ((s + 1) & 1) * bufw + (size_t)(g * RG + r) * DG + unit / 2,
+                   (uint32_t)(s + 2), mine | (nb << 16), local);
+    };
+    publish(-1, hprev);
+    const int lrow = lane & 15;
+    // input projections are loaded one step ahead: issued at the end of step t-1, they land
+    // during step t's hand-off wait instead of stalling its epilogue
+    const float* gp0 = a.gi + (int64_t)b * a.ldgi;
+    float gir = gp0[unit], giz = gp0[D + unit], gin = gp0[2 * D + unit];
+    for (int t = 0; t < a.Fr; ++t) {
+        floatx4 acc[NT];
+#pragma unroll
+        for (int i = 0; i < NT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (wave < KW) {
+            const uint32_t tag = (uint32_t)(t + 1);
+            const uint32_t base = (uint32_t)(((size_t)(t & 1) * bufw +
+                                              (size_t)(g * RG + lrow) * DG) * 8);
+            uint32_t w[UPW][4];
+            int spins = 0;
+            for (;;) {
+                // every load unconditional (clamped unit), so all 2 x UPW are in flight at
+                // once; a branch per unit would put a vmcnt(0) between them
+                uint4 x[UPW][2];
+#pragma unroll
+                for (int j = 0; j < UPW; ++j) {
+                    const int u = min(wave + NW * j, NU - 1);
+                    const uint32_t off = base + (uint32_t)((u * UK + (lane >> 4) * 8) / 2) * 8u;
+                    x[j][0] = hx_get2(rx, off);
+                    x[j][1] = hx_get2(rx, off + 16);
+                }
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < UPW; ++j) {
+                    const bool v = wave + NW * j < NU;
+                    w[j][0] = v ? x[j][0].x : 0u; w[j][1] = v ? x[j][0].z : 0u;
+                    w[j][2] = v ? x[j][1].x : 0u; w[j][3] = v ? x[j][1].z : 0u;
+                    ok &= !v || ((x[j][0].y == tag) & (x[j][0].w == tag) & (x[j][1].y == tag) &
+                                 (x[j][1].w == tag));
+                }
+                if (__all(ok)) break;
+                if (hx_spin_fail(spins, a.err, lane)) break;
+            }
+            GX_STAMP();
+#pragma unroll
+            for (int j = 0; j < UPW; ++j) {
+                const uint4 v = make_uint4(w[j][0], w[j][1], w[j][2], w[j][3]);
+                bf16x8 af;
+                __builtin_memcpy(&af, &v, 16);
+#pragma unroll
+                for (int i = 0; i < NT; ++i) Mma<bf16>::run(acc[i], af, wf[j][i]);
+            }
+#pragma unroll
+            for (int i = 0; i < NT; ++i) red[(wave * NT + i) * 64 + lane] = acc[i];
+        }
+        GX_STAMP();
+        __syncthreads();
+        GX_STAMP();
+        float gh[3];
+        {
+            const int ln = (r >> 2) * 16 + (uu & 15), ii = r & 3;
+#pragma unroll
+            for (int gt = 0; gt < 3; ++gt) {
+                const int tile = 2 * gt + (uu >> 4);
+                float v = 0.f;
+                float pr[NW];
+                #pragma unroll
+                for (int kw = 0; kw < NW; ++kw)
+                    pr[kw] = red[(min(kw, KW - 1) * NT + tile) * 64 + ln][ii];
+                #pragma unroll
+                for (int kw = 0; kw < NW; ++kw) v += kw < KW ? pr[kw] : 0.f;
+                gh[gt] = v;
+            }
+        }
+        const float ghr = gh[0] + bhr, ghz = gh[1] + bhz, ghn = gh[2] + bhn;
+        const float rr = 1.0f / (1.0f + expf(-(ghr + gir)));
+        const float zz = 1.0f / (1.0f + expf(-(ghz + giz)));
+        const float nn = tanhf(gin + ghn * rr);
+        const float hn = (hprev - nn) * zz + nn;
+        hprev = hn;
+        publish(t, hn);
+        {
+            const float* gp = a.gi + (int64_t)b * a.ldgi + (int64_t)min(t + 1, a.Fr - 1) * a.sgi;
+            gir = gp[unit]; giz = gp[D + unit]; gin = gp[2 * D + unit];
+        }
+        GX_STAMP();
+        if (wr) {
+            const int64_t o = (int64_t)b * a.ldo + (int64_t)t * a.so + unit;
+            a.out[o] = hn;
+            a.out_lp[o] = __float2bfloat16(hn);
+            float* gt = a.gates + (int64_t)b * a.ldg + (int64_t)t * a.sg;
+            gt[unit] = rr; gt[D + unit] = zz; gt[2 * D + unit] = nn; gt[3 * D + unit] = ghn;
+        }
+        __syncthreads();                       // red is rewritten next step
+        GX_STAMP();
+    }
+#undef GX_STAMP
+}
+
+// ------------------------------------------------------------------ host side
+static int g_gx_ncu = 0;
+
+static unsigned long long*& gx_diag_buf() {
+    static unsigned long long* p = nullptr;
+    return p;
+}
+
+// timing diagnostics only (SRNN_GRU_DIAG=1): prints the first armed launch's stamps
+extern "C" int srnn_gru_diag_dump(void) {
+    unsigned long long h[256];
+    if (!gx_diag_buf() || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(h, gx_diag_buf(), sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+        return 1;
+    fprintf(stderr, "gru_xcd diag mode: %s\n", h[255] == 1 ? "xcd-local" : "static map");
+    for (int k = 1; k < 255 && h[k]; ++k)
+        fprintf(stderr, "gru_xcd diag %3d: +%8.2f us\n", k, (double)(h[k] - h[k - 1]) / 100.0);
+    return 0;
+}
+
+static int gx_cus() {
+    if (!g_gx_ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&g_gx_ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
+                hipSuccess)
+            g_gx_ncu = 0;
+    }
+    return g_gx_ncu;
+}
+
+// work-buffer bytes of srnn_gru_xcd_fwd for (B, D); 0 if the shape / device is not supported
+extern "C" size_t srnn_gru_xcd_work_bytes(int dtype, int B, int D) {
+    if (dtype != SRNN_BF16 || D % 256 != 0 || D > 1024 || B <= 0) return 0;
+    const int G = cdiv(B, gx::RG), P = D / gx::CU;
+    const int ncu = gx_cus();
+    if (ncu <= 0 || G * P > ncu) return 0;
+    return 256 + (size_t)2 * G * gx::RG * (D / 2) * 8;
+}
+
+extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
+                                int64_t sgi, const float* h0, const void* whh, const float* bhh,
+                                float* out, void* out_lp, int64_t ldo, int64_t so, float* gates,
+                                int64_t ldg, int64_t sg, void* work, size_t work_bytes,
+                                void* stream) {
+    const size_t need = srnn_gru_xcd_work_bytes(dtype, B, D);
+    SRNN_REQUIRE(need > 0, "gru_xcd: shape/device not supported");
+    SRNN_REQUIRE(work && work_bytes >= need, "gru_xcd: workspace %zu < %zu", work_bytes, need);
+    if (Fr <= 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    // granules, census and error word start zeroed every call (tags count from 1)
+    SRNN_CHECK_HIP(hipMemsetAsync(work, 0, need, s));
+    GruXArgs a;
+    a.gi = gi; a.ldgi = ldgi; a.sgi = sgi;
+    a.h0 = h0; a.whh = (const bf16*)whh; a.bhh = bhh;
+    a.out = out; a.out_lp = (bf16*)out_lp; a.ldo = ldo; a.so = so;
+    a.gates = gates; a.ldg = ldg; a.sg = sg;
+    a.err = (int*)work;
+    a.census = env_flag("SRNN_GEN_LOCAL", 1) ? (int*)work + 16 : nullptr;
+    a.xh = (u64*)((char*)work + 256);
+    a.B = B; a.D = D; a.Fr = Fr;
+    a.diag = nullptr;
+    {
+        static unsigned long long* diag = nullptr;
+        static int armed = -1;
+        if (armed < 0) armed = env_flag("SRNN_GRU_DIAG", 0);
+        if (armed == 1 && Fr >= 32 && hipMalloc(&diag, 256 * 8) == hipSuccess) {
+            SRNN_CHECK_HIP(hipMemsetAsync(diag, 0, 256 * 8, s));
+            a.diag = diag;
+            armed = 2;
+            gx_diag_buf() = diag;
+        }
+    }
+    a.G = cdiv(B, gx::RG);
+    a.P = D / gx::CU;
+    const int NU = D / gx::UK;
+    const int KW = NU < gx::NW ? NU : gx::NW;
+    const size_t lds = (size_t)KW * gx::NT * 64 * 16 + 16;
+    const int upw = cdiv(NU, gx::NW);
+    void (*k)(GruXArgs) = upw <= 1 ? gru_xcd_fwd_kernel<1>
+                          : upw <= 2 ? gru_xcd_fwd_kernel<2> : gru_xcd_fwd_kernel<4>;
+    static bool attr[3] = {false, false, false};
+    const int ai = upw <= 1 ? 0 : upw <= 2 ? 1 : 2;
+    if (!attr[ai]) {
+        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+        attr[ai] = true;
+    }
+    hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// nonzero if the previous srnn_gru_xcd_fwd on `work` gave up a hand-off (synchronises)
+extern "C" int srnn_gru_xcd_error(const void* work) {
+    int e = 0;
+    if (hipMemcpy(&e, work, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return e;
+}

@@ -252,14 +252,23 @@ class _TierFn(torch.autograd.Function):
             gt = torch.empty((B, Fr, 4 * D), device=dev, dtype=torch.float32)
             hpf = h_in[l]
             hpT = H.cast(hpf, T)
-            if lp and H.gru_seq_supported(T, B, D):
+            xw = H.gru_xcd_work_bytes(T, B, D) if lp else 0
+            seq = lp and (xw > 0 or H.gru_seq_supported(T, B, D))
+            if xw > 0:
+                # whole sequence in one persistent launch, row groups per XCD, W_hh in VGPRs
+                work = torch.empty(xw, device=dev, dtype=torch.uint8)
+                H.lib().call('srnn_gru_xcd_fwd', H.dcode(T), B, D, Fr, H.ptr(gi), Fr * 3 * D,
+                             3 * D, H.ptr(hpf), H.ptr(Whh[l]), H.ptr(b_hh), H.ptr(out),
+                             H.ptr(outT), Fr * D, D, H.ptr(gt), Fr * 4 * D, 4 * D, H.ptr(work),
+                             xw, H.stream())
+            elif seq:
                 # whole sequence in one persistent launch (W_hh resident in LDS)
                 work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
                 H.lib().call('srnn_gru_seq_fwd', H.dcode(T), B, D, Fr, H.ptr(gi), Fr * 3 * D,
                              3 * D, H.ptr(hpf), H.ptr(hpT), H.ptr(Whh[l]), H.ptr(b_hh),
                              H.ptr(out), H.ptr(outT), Fr * D, D, H.ptr(gt), Fr * 4 * D, 4 * D,
                              H.ptr(work), work.numel() * 4, H.stream())
-            for t in range(0 if not (lp and H.gru_seq_supported(T, B, D)) else Fr, Fr):
+            for t in range(0 if not seq else Fr, Fr):
                 if t == 0:
                     hp_t, hp_f, ldh = hpT, hpf, D
                 else:

@@ -163,6 +163,53 @@ def test_gru_seq_fwd_matches_steps(hip, B, D, Fr):
         assert torch.equal(a, b)
 
 
+def _gru_ref(gi, h0, whh, bhh, Fr):
+    """torch fp32 GRU recurrence (model.py:148-165, gate order r|z|n) with bf16 W_hh and bf16
+    h_{t-1} operands as the MFMA path uses them; fp32 state."""
+    B, D = h0.shape
+    h = h0.clone()
+    out, gates = [], []
+    W = whh.float()
+    for t in range(Fr):
+        gh = h.to(torch.bfloat16).float() @ W.t() + bhh
+        g = gi.reshape(B, Fr, 3 * D)[:, t]
+        r = torch.sigmoid(gh[:, :D] + g[:, :D])
+        z = torch.sigmoid(gh[:, D:2 * D] + g[:, D:2 * D])
+        n = torch.tanh(g[:, 2 * D:] + gh[:, 2 * D:] * r)
+        h = (h - n) * z + n
+        out.append(h)
+        gates.append(torch.cat([r, z, n, gh[:, 2 * D:]], 1))
+    return torch.stack(out, 1), torch.stack(gates, 1)
+
+
+@pytest.mark.parametrize('B,D,Fr', [(128, 1024, 64), (64, 1024, 5), (100, 256, 9), (16, 512, 3)])
+def test_gru_xcd_fwd(hip, B, D, Fr):
+    """XCD-grouped persistent GRU forward (gru_xcd.hip) vs the torch recurrence; same outputs
+    as the gru_seq kernel within MFMA summation-order noise."""
+    T = torch.bfloat16
+    nb = hip.gru_xcd_work_bytes(T, B, D)
+    if not nb:
+        pytest.skip('gru_xcd not supported on this device')
+    g = torch.Generator().manual_seed(B + D + 1)
+    whh = (torch.randn(3 * D, D, generator=g) * 0.03).to(DEV, T)
+    bhh = (torch.randn(3 * D, generator=g) * 0.1).to(DEV)
+    gi = (torch.randn(B * Fr, 3 * D, generator=g) * 0.5).to(DEV)
+    h0 = (torch.randn(B, D, generator=g) * 0.5).to(DEV)
+    out = torch.full((B, Fr, D), float('nan'), device=DEV)
+    outT = torch.zeros((B, Fr, D), device=DEV, dtype=T)
+    gt = torch.full((B, Fr, 4 * D), float('nan'), device=DEV)
+    work = torch.full((nb,), 7, device=DEV, dtype=torch.uint8)
+    hip.lib().call('srnn_gru_xcd_fwd', hip.BF16, B, D, Fr, hip.ptr(gi), Fr * 3 * D, 3 * D,
+                   hip.ptr(h0), hip.ptr(whh), hip.ptr(bhh), hip.ptr(out), hip.ptr(outT), Fr * D,
+                   D, hip.ptr(gt), Fr * 4 * D, 4 * D, hip.ptr(work), nb, hip.stream())
+    torch.cuda.synchronize()
+    assert hip.lib().dll.srnn_gru_xcd_error(hip.ptr(work)) == 0, 'gru_xcd gave up waiting'
+    ref_out, ref_gt = _gru_ref(gi.cpu(), h0.cpu(), whh.cpu(), bhh.cpu(), Fr)
+    torch.testing.assert_close(out.cpu(), ref_out, atol=2e-3, rtol=0)
+    torch.testing.assert_close(gt.cpu(), ref_gt, atol=2e-3, rtol=0)
+    torch.testing.assert_close(outT.float().cpu(), out.cpu().to(T).float(), atol=0, rtol=0)
+
+
 @pytest.mark.parametrize('B,D,Fr', [(128, 1024, 16), (64, 1024, 5), (100, 256, 9)])
 def test_gru_seq_bwd_matches_steps(hip, B, D, Fr):
     """Persistent whole-sequence GRU backward == Fr per-step backward launches, bit for bit."""
