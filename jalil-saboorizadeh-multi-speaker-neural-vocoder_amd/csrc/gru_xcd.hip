@@ -37,6 +37,7 @@ struct GruXArgs {
     int* census;                                    // 9 zeroed words, or null (static map)
     int* err;
     int B, D, Fr, G, P;
+    int poll_sleep;                                 // s_sleep 1 repeats between polls
     unsigned long long* diag;                       // optional phase timestamps (timing only)
 };
 
@@ -140,7 +141,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
                                  (x[j][1].w == tag));
                 }
                 if (__all(ok)) break;
-                if (hx_spin_fail(spins, a.err, lane)) break;
+                if (hx_spin_fail(spins, a.err, lane, a.poll_sleep)) break;
             }
             GX_STAMP();
 #pragma unroll
@@ -260,6 +261,7 @@ extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi
     a.xh = (u64*)((char*)work + 256);
     a.B = B; a.D = D; a.Fr = Fr;
     a.diag = nullptr;
+    a.poll_sleep = env_flag("SRNN_POLL_SLEEP", 1);
     {
         static unsigned long long* diag = nullptr;
         static int armed = -1;
