@@ -84,6 +84,15 @@ int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t l
                      const float* h0, const void* whh, const float* bhh, float* out,
                      void* out_lp, int64_t ldo, int64_t so, float* gates, int64_t ldg,
                      int64_t sg, void* work, size_t work_bytes, void* stream);
+/* Reverse sweep of one layer in the same organisation (W_hh^T K-slices in VGPRs, dgh
+ * hand-offs as granules): same operands and outputs as srnn_gru_seq_bwd; work =
+ * srnn_gru_xcd_bwd_work_bytes(dtype, B, D) bytes. */
+size_t srnn_gru_xcd_bwd_work_bytes(int dtype, int B, int D);
+int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy, int64_t lddy, int64_t sdy,
+                     const float* gates, int64_t ldg, int64_t sg, const float* hout, int64_t ldo,
+                     int64_t so, const float* h0, const void* whh_t, float* dgh, void* dgh_lp,
+                     float* dgi, int64_t ldd, int64_t sd, float* ddir0, void* work,
+                     size_t work_bytes, void* stream);
 int srnn_gru_xcd_error(const void* work);
 int srnn_gru_seq_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
                      int64_t sgi, const float* h0, const void* h0_lp, const void* whh,

@@ -18,6 +18,7 @@
 //   * gate math, outputs and saved gates are gru_seq's (fp32 state, bf16 MMA operands).
 #include "samplernn_hip_internal.hpp"
 #include "handoff.hpp"
+#include "gru_point.hpp"
 
 namespace gx {
 constexpr int NW = 8, NTHR = NW * 64;
@@ -199,6 +200,173 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
 #undef GX_STAMP
 }
 
+// ------------------------------------------------------------------ backward
+// Reverse sweep of one layer (gru_seq.hip's backward, same pointwise code, gru_point.hpp):
+//   dh_t = dy_t + ddir_{t+1} + dgh_{t+1} . W_hh,  then the gate backward.
+// Same groups as the forward; each wave keeps its K-slice (3D / 8 = 384 k) of the
+// workgroup's 32 W_hh^T rows as B fragments (96 VGPRs at D = 1024); per step the group's
+// dgh_{t+1} (16 rows x 3D bf16) arrives as granules (double-buffered, tag = Fr - step).
+struct GruXBwdArgs {
+    const float* dy; int64_t lddy; int64_t sdy;
+    const float* gates; int64_t ldg; int64_t sg;
+    const float* hout; int64_t ldo; int64_t so;
+    const float* h0;
+    const bf16* whh_t;                              // (D, 3D)
+    float* dgh; bf16* dgh_lp; float* dgi; int64_t ldd; int64_t sd;
+    float* ddir0;                                   // (B, D)
+    u64* xg;                                        // 2 x G x RG x 3D/2 granules
+    int* census;
+    int* err;
+    int B, D, Fr, G, P;
+};
+
+template <int UPW>
+__global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a) {
+    using namespace gx;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int D = a.D, B = a.B, K3 = 3 * D;
+    const int NU = K3 / UK, KW = NW < NU ? NW : NU;
+    constexpr int NTB = 2;                                      // 32 units = 2 n tiles
+    floatx4* red = (floatx4*)smem;                              // [KW][2][64]
+    int* gsh = (int*)(smem + (size_t)KW * NTB * 64 * sizeof(floatx4));
+    if (tid == 0) {
+        int g = blockIdx.x % a.G, p = blockIdx.x / a.G, loc = 0;
+        if (a.census) loc = hx_census(a.census, a.P, a.err, g, p) ? 1 : 0;
+        gsh[0] = g; gsh[1] = p; gsh[2] = loc;
+    }
+    __syncthreads();
+    const int g = gsh[0], p = gsh[1];
+    const bool local = gsh[2] != 0;
+    const int u0 = p * CU;
+    const int KG = K3 / 2;                                      // granules per row
+    bf16x8 wf[UPW][NTB];
+    {
+        uint4 lw[UPW][NTB];
+#pragma unroll
+        for (int j = 0; j < UPW; ++j) {
+            const int u = wave + NW * j;
+            const int ke = min(u * UK + (lane >> 4) * 8, K3 - 8);
+#pragma unroll
+            for (int t = 0; t < NTB; ++t) {
+                const int row = u0 + t * 16 + (lane & 15);
+                lw[j][t] = *reinterpret_cast<const uint4*>(a.whh_t + (int64_t)row * K3 + ke);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UPW; ++j) {
+            const bool kv = wave + NW * j < NU;
+#pragma unroll
+            for (int t = 0; t < NTB; ++t) {
+                const uint4 v = kv ? lw[j][t] : make_uint4(0u, 0u, 0u, 0u);
+                __builtin_memcpy(&wf[j][t], &v, 16);
+            }
+        }
+    }
+    const int r = tid >> 5, uu = tid & 31;
+    const int b = min(g * RG + r, B - 1);
+    const bool wr = g * RG + r < B;
+    const int unit = u0 + uu;
+    const __amdgpu_buffer_rsrc_t rx = hx_rsrc(a.xg);
+    const size_t bufw = (size_t)a.G * RG * KG;
+    const int lrow = lane & 15;
+    float ddir = 0.f;
+    // this step's operands, loaded one step ahead (see the forward)
+    auto fetch = [&](int t, float& dyv, float& gr, float& gz, float& gn, float& gg, float& hp) {
+        dyv = a.dy[(int64_t)b * a.lddy + (int64_t)t * a.sdy + unit];
+        const float* gp = a.gates + (int64_t)b * a.ldg + (int64_t)t * a.sg;
+        gr = gp[unit]; gz = gp[D + unit]; gn = gp[2 * D + unit]; gg = gp[3 * D + unit];
+        hp = t > 0 ? a.hout[(int64_t)b * a.ldo + (int64_t)(t - 1) * a.so + unit]
+                   : a.h0[(int64_t)b * D + unit];
+    };
+    float dyv, gr, gz, gn, gg, hp;
+    fetch(a.Fr - 1, dyv, gr, gz, gn, gg, hp);
+    for (int t = a.Fr - 1; t >= 0; --t) {
+        const bool has_next = t + 1 < a.Fr;
+        floatx4 acc[NTB];
+#pragma unroll
+        for (int i = 0; i < NTB; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (has_next) {
+            if (wave < KW) {
+                const uint32_t tag = (uint32_t)(a.Fr - 1 - t);     // dgh_{t+1}
+                const uint32_t base = (uint32_t)((((size_t)((t + 1) & 1)) * bufw +
+                                                  (size_t)(g * RG + lrow) * KG) * 8);
+                uint4 x[UPW][2];
+                int spins = 0;
+                for (;;) {
+#pragma unroll
+                    for (int j = 0; j < UPW; ++j) {
+                        const int u = min(wave + NW * j, NU - 1);
+                        const uint32_t off = base + (uint32_t)((u * UK + (lane >> 4) * 8) / 2) * 8u;
+                        x[j][0] = hx_get2(rx, off);
+                        x[j][1] = hx_get2(rx, off + 16);
+                    }
+                    bool ok = true;
+#pragma unroll
+                    for (int j = 0; j < UPW; ++j)
+                        ok &= (wave + NW * j >= NU) ||
+                              ((x[j][0].y == tag) & (x[j][0].w == tag) & (x[j][1].y == tag) &
+                               (x[j][1].w == tag));
+                    if (__all(ok)) break;
+                    if (hx_spin_fail(spins, a.err, lane)) break;
+                }
+#pragma unroll
+                for (int j = 0; j < UPW; ++j) {
+                    const bool kv = wave + NW * j < NU;      // (weights are zero there too)
+                    const uint4 v = kv ? make_uint4(x[j][0].x, x[j][0].z, x[j][1].x, x[j][1].z)
+                                       : make_uint4(0u, 0u, 0u, 0u);
+                    bf16x8 af;
+                    __builtin_memcpy(&af, &v, 16);
+#pragma unroll
+                    for (int i = 0; i < NTB; ++i) Mma<bf16>::run(acc[i], af, wf[j][i]);
+                }
+#pragma unroll
+                for (int i = 0; i < NTB; ++i) red[(wave * NTB + i) * 64 + lane] = acc[i];
+            }
+            __syncthreads();
+        }
+        float s = 0.f;
+        if (has_next) {
+            const int ln = (r >> 2) * 16 + (uu & 15), ii = r & 3, tile = uu >> 4;
+            float pr[NW];
+#pragma unroll
+            for (int kw = 0; kw < NW; ++kw) pr[kw] = red[(min(kw, KW - 1) * NTB + tile) * 64 + ln][ii];
+#pragma unroll
+            for (int kw = 0; kw < NW; ++kw) s += kw < KW ? pr[kw] : 0.f;
+        }
+        float dh = s + dyv;
+        if (has_next) dh += ddir;
+        const GruBwdPoint o = gru_bwd_point(dh, gr, gz, gn, gg, hp);
+        ddir = o.ddir;
+        // publish dgh_t = [dar | daz | dghn] (bf16 granules, pairs of units), tag Fr - t
+        {
+            const float vals[3] = {o.dar, o.daz, o.dghn};
+            u64* dst = a.xg + (size_t)(t & 1) * bufw + (size_t)(g * RG + r) * KG;
+#pragma unroll
+            for (int gt = 0; gt < 3; ++gt) {
+                const uint32_t mine = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(vals[gt]));
+                const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
+                if ((uu & 1) == 0)
+                    hx_put(dst + (gt * D + unit) / 2, (uint32_t)(a.Fr - t), mine | (nb << 16), local);
+            }
+        }
+        const float cdar = o.dar, cdaz = o.daz, cdghn = o.dghn, cdan = o.dan;
+        if (t > 0) fetch(t - 1, dyv, gr, gz, gn, gg, hp);
+        if (wr) {
+            const int64_t ob = (int64_t)b * a.ldd + (int64_t)t * a.sd;
+            float* dg = a.dgh + ob;
+            dg[unit] = cdar; dg[D + unit] = cdaz; dg[2 * D + unit] = cdghn;
+            bf16* dl = a.dgh_lp + ob;
+            dl[unit] = __float2bfloat16(cdar); dl[D + unit] = __float2bfloat16(cdaz);
+            dl[2 * D + unit] = __float2bfloat16(cdghn);
+            float* di = a.dgi + ob;
+            di[unit] = cdar; di[D + unit] = cdaz; di[2 * D + unit] = cdan;
+            if (t == 0) a.ddir0[(int64_t)b * D + unit] = ddir;
+        }
+        __syncthreads();
+    }
+}
+
 // ------------------------------------------------------------------ host side
 static int g_gx_ncu = 0;
 
@@ -293,7 +461,51 @@ extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi
     return 0;
 }
 
-// nonzero if the previous srnn_gru_xcd_fwd on `work` gave up a hand-off (synchronises)
+
+// work-buffer bytes of srnn_gru_xcd_bwd for (B, D); 0 if not supported
+extern "C" size_t srnn_gru_xcd_bwd_work_bytes(int dtype, int B, int D) {
+    if (!srnn_gru_xcd_work_bytes(dtype, B, D)) return 0;
+    const int G = cdiv(B, gx::RG);
+    return 256 + (size_t)2 * G * gx::RG * (3 * D / 2) * 8;
+}
+
+extern "C" int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy, int64_t lddy,
+                                int64_t sdy, const float* gates, int64_t ldg, int64_t sg,
+                                const float* hout, int64_t ldo, int64_t so, const float* h0,
+                                const void* whh_t, float* dgh, void* dgh_lp, float* dgi,
+                                int64_t ldd, int64_t sd, float* ddir0, void* work,
+                                size_t work_bytes, void* stream) {
+    const size_t need = srnn_gru_xcd_bwd_work_bytes(dtype, B, D);
+    SRNN_REQUIRE(need > 0, "gru_xcd_bwd: shape/device not supported");
+    SRNN_REQUIRE(work && work_bytes >= need, "gru_xcd_bwd: workspace %zu < %zu", work_bytes, need);
+    if (Fr <= 0) return 0;
+    hipStream_t s = (hipStream_t)stream;
+    SRNN_CHECK_HIP(hipMemsetAsync(work, 0, need, s));
+    GruXBwdArgs a;
+    a.dy = dy; a.lddy = lddy; a.sdy = sdy;
+    a.gates = gates; a.ldg = ldg; a.sg = sg;
+    a.hout = hout; a.ldo = ldo; a.so = so; a.h0 = h0;
+    a.whh_t = (const bf16*)whh_t;
+    a.dgh = dgh; a.dgh_lp = (bf16*)dgh_lp; a.dgi = dgi; a.ldd = ldd; a.sd = sd;
+    a.ddir0 = ddir0;
+    a.err = (int*)work;
+    a.census = env_flag("SRNN_GEN_LOCAL", 1) ? (int*)work + 16 : nullptr;
+    a.xg = (u64*)((char*)work + 256);
+    a.B = B; a.D = D; a.Fr = Fr;
+    a.G = cdiv(B, gx::RG);
+    a.P = D / gx::CU;
+    const int NU = 3 * D / gx::UK;
+    const int KW = NU < gx::NW ? NU : gx::NW;
+    const size_t lds = (size_t)KW * 2 * 64 * 16 + 16;
+    const int upw = cdiv(NU, gx::NW);
+    void (*k)(GruXBwdArgs) = upw <= 3 ? gru_xcd_bwd_kernel<3>
+                             : upw <= 6 ? gru_xcd_bwd_kernel<6> : gru_xcd_bwd_kernel<12>;
+    hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// nonzero if the previous srnn_gru_xcd_fwd/bwd on `work` gave up a hand-off (synchronises)
 extern "C" int srnn_gru_xcd_error(const void* work) {
     int e = 0;
     if (hipMemcpy(&e, work, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;

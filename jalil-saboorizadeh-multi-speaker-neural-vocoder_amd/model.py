@@ -341,8 +341,17 @@ class _TierFn(torch.autograd.Function):
             ddir = [torch.empty((B, D), device=dev, dtype=torch.float32) for _ in range(2)]
             # W_hh^T (D, 3D): k-contiguous operand for the deep-ring backward kernel
             WhhT = H.permute3(Whh[l].float().reshape(1, 3 * D, D), (0, 2, 1), dtype=T)
-            seq = lp and H.gru_seq_supported(T, B, D)
-            if seq:
+            xbw = H.gru_xcd_bwd_work_bytes(T, B, D) if lp else 0
+            seq = lp and (xbw > 0 or H.gru_seq_supported(T, B, D))
+            if xbw > 0:
+                # reverse sweep in one persistent launch, row groups per XCD, W_hh^T in VGPRs
+                work = torch.empty(xbw, device=dev, dtype=torch.uint8)
+                dOutc = dOut.contiguous()
+                H.lib().call('srnn_gru_xcd_bwd', H.dcode(T), B, D, Fr, H.ptr(dOutc), Fr * D, D,
+                             H.ptr(gates[l]), Fr * 4 * D, 4 * D, H.ptr(outs[l]), Fr * D, D,
+                             H.ptr(h_in[l]), H.ptr(WhhT), H.ptr(dGH), H.ptr(dGHT), H.ptr(dGI),
+                             Fr * 3 * D, 3 * D, H.ptr(ddir[0]), H.ptr(work), xbw, st())
+            elif seq:
                 # the whole reverse sweep in one persistent launch (W_hh^T resident in LDS)
                 work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
                 dOutc = dOut.contiguous()

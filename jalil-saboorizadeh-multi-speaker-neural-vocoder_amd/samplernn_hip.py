@@ -64,6 +64,8 @@ _SIGS = {
                          _L, _L, _P, _P, _SZ, _P],
     'srnn_gru_xcd_fwd': [_I, _I, _I, _I, _P, _L, _L, _P, _P, _P, _P, _P, _L, _L, _P, _L, _L, _P,
                          _SZ, _P],
+    'srnn_gru_xcd_bwd': [_I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L, _P, _P, _P, _P, _P,
+                         _L, _L, _P, _P, _SZ, _P],
     'srnn_gen_workspace_size': [_P, _I, ctypes.POINTER(_SZ)],
     'srnn_generate': [_P, _I, _I, _P, _P, _P, _U64, _P, _P, _P, _SZ, _I, _P],
 }
@@ -117,7 +119,7 @@ def lib():
 def exported_symbols():
     return sorted(_SIGS) + ['srnn_last_error', 'srnn_abi_version', 'srnn_gru_seq_supported',
                             'srnn_gen_persistent_rows', 'srnn_gru_xcd_work_bytes',
-                            'srnn_gru_xcd_error']
+                            'srnn_gru_xcd_bwd_work_bytes', 'srnn_gru_xcd_error']
 
 
 _GRU_XCD = {}
@@ -131,6 +133,20 @@ def gru_xcd_work_bytes(dtype, B, D):
     key = (dtype, B, D)
     if key not in _GRU_XCD:
         fn = lib().dll.srnn_gru_xcd_work_bytes
+        fn.argtypes = [_I, _I, _I]
+        fn.restype = _SZ
+        _GRU_XCD[key] = int(fn(dcode(dtype), B, D))
+    return _GRU_XCD[key]
+
+
+def gru_xcd_bwd_work_bytes(dtype, B, D):
+    """Work-buffer bytes of the XCD-grouped persistent GRU backward, 0 when it does not
+    apply (SRNN_GRU_XCD=0 disables it)."""
+    if os.environ.get('SRNN_GRU_XCD', '1') == '0':
+        return 0
+    key = ('bwd', dtype, B, D)
+    if key not in _GRU_XCD:
+        fn = lib().dll.srnn_gru_xcd_bwd_work_bytes
         fn.argtypes = [_I, _I, _I]
         fn.restype = _SZ
         _GRU_XCD[key] = int(fn(dcode(dtype), B, D))

@@ -210,6 +210,60 @@ def test_gru_xcd_fwd(hip, B, D, Fr):
     torch.testing.assert_close(outT.float().cpu(), out.cpu().to(T).float(), atol=0, rtol=0)
 
 
+@pytest.mark.parametrize('B,D,Fr', [(128, 1024, 64), (64, 1024, 5), (100, 256, 9), (16, 512, 3)])
+def test_gru_xcd_bwd(hip, B, D, Fr):
+    """XCD-grouped persistent GRU backward vs torch autograd of the same recurrence (bf16
+    W_hh and bf16 dgh operands on the MFMA path: tolerance, not bits)."""
+    T = torch.bfloat16
+    nb = hip.gru_xcd_bwd_work_bytes(T, B, D)
+    if not nb:
+        pytest.skip('gru_xcd not supported on this device')
+    g = torch.Generator().manual_seed(B * 7 + D)
+    whh = (torch.randn(3 * D, D, generator=g) * 0.03).to(T)
+    bhh = torch.randn(3 * D, generator=g) * 0.1
+    gi = torch.randn(B * Fr, 3 * D, generator=g) * 0.5
+    h0 = torch.randn(B, D, generator=g) * 0.5
+    dy = torch.randn(B, Fr, D, generator=g) * 0.1
+    # forward (fp32, with the saved gates the kernel consumes)
+    out, gates = _gru_ref(gi, h0, whh, bhh, Fr)
+    # reference backward: autograd through the fp32 recurrence with fp32 weights
+    W = whh.float().requires_grad_(False)
+    gi_r = gi.clone().requires_grad_(True)
+    h0_r = h0.clone().requires_grad_(True)
+    h = h0_r
+    outs = []
+    for t in range(Fr):
+        gh = h @ W.t() + bhh
+        gg = gi_r.reshape(B, Fr, 3 * D)[:, t]
+        r = torch.sigmoid(gh[:, :D] + gg[:, :D])
+        z = torch.sigmoid(gh[:, D:2 * D] + gg[:, D:2 * D])
+        n = torch.tanh(gg[:, 2 * D:] + gh[:, 2 * D:] * r)
+        h = (h - n) * z + n
+        outs.append(h)
+    torch.autograd.backward(torch.stack(outs, 1), dy)
+    whh_t = whh.float().t().contiguous().to(DEV, T)
+    dgh = torch.full((B, Fr, 3 * D), float('nan'), device=DEV)
+    dgh_lp = torch.zeros((B, Fr, 3 * D), device=DEV, dtype=T)
+    dgi = torch.full((B, Fr, 3 * D), float('nan'), device=DEV)
+    ddir0 = torch.full((B, D), float('nan'), device=DEV)
+    work = torch.full((nb,), 7, device=DEV, dtype=torch.uint8)
+    dyd, gtd, outd, h0d = dy.to(DEV), gates.to(DEV), out.to(DEV), h0.to(DEV)
+    hip.lib().call('srnn_gru_xcd_bwd', hip.BF16, B, D, Fr, hip.ptr(dyd), Fr * D, D, hip.ptr(gtd),
+                   Fr * 4 * D, 4 * D, hip.ptr(outd), Fr * D, D, hip.ptr(h0d), hip.ptr(whh_t),
+                   hip.ptr(dgh), hip.ptr(dgh_lp), hip.ptr(dgi), Fr * 3 * D, 3 * D,
+                   hip.ptr(ddir0), hip.ptr(work), nb, hip.stream())
+    torch.cuda.synchronize()
+    assert hip.lib().dll.srnn_gru_xcd_error(hip.ptr(work)) == 0, 'gru_xcd_bwd gave up waiting'
+    # dgi = dL/d(gi): exactly the reference's input-projection gradient
+    ref_dgi = gi_r.grad.reshape(B, Fr, 3 * D)
+    scale = ref_dgi.abs().max().item()
+    torch.testing.assert_close(dgi.cpu(), ref_dgi, atol=2e-2 * scale, rtol=0)
+    # dh_0 = dgh_0 . W_hh + ddir0
+    dh0 = dgh[:, 0].cpu() @ whh.float() + ddir0.cpu()
+    torch.testing.assert_close(dh0, h0_r.grad, atol=2e-2 * h0_r.grad.abs().max().item(), rtol=0)
+    torch.testing.assert_close(dgh_lp.float().cpu(), dgh.cpu().to(T).float(), atol=0, rtol=0)
+
+
 @pytest.mark.parametrize('B,D,Fr', [(128, 1024, 16), (64, 1024, 5), (100, 256, 9)])
 def test_gru_seq_bwd_matches_steps(hip, B, D, Fr):
     """Persistent whole-sequence GRU backward == Fr per-step backward launches, bit for bit."""
