@@ -29,6 +29,8 @@
 //   identical indices), so the sampled index needs no hand-off; workgroup 0 writes seq/logp.
 // * Spins are bounded: a lost hand-off sets the error word and the loop runs out instead of
 //   hanging.
+#include <algorithm>
+
 #include "samplernn_hip_internal.hpp"
 #include "sampler.hpp"
 #include "gen_mlp.hpp"
@@ -144,22 +146,9 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                               (size_t)min(gm::NW, (a.D + UK - 1) / UK) *
                                   max(a.CW / 16, a.NZ / 16) * 64 * sizeof(floatx4) +
                               (size_t)a.R * gm::HIST * 4));
-    if (tid == 0) {
-        int gg = blockIdx.x % a.G, pp = blockIdx.x / a.G, loc = 0;
-        if (a.census) {
-            const int n = (*a.base + a.off - a.L) / FS0;          // launch index in this call
-            int* cur = a.census + (n & 1) * 16;
-            if (blockIdx.x == 0)          // the next launch's census array (last used 2 ago)
-                for (int j = 0; j < 9; ++j)
-                    __hip_atomic_store(a.census + ((n + 1) & 1) * 16 + j, 0, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-            loc = hx_census(cur, a.P, a.err, gg, pp) ? 1 : 0;
-        }
-        gsh[0] = gg; gsh[1] = pp; gsh[2] = loc;
-    }
-    __syncthreads();
-    const int g = gsh[0], p = gsh[1];
-    const bool local = gsh[2] != 0;
+    // member p is fixed by the block index (the weights below depend only on p and load
+    // while the census runs); the census only assigns the row group g
+    const int p = blockIdx.x / a.G;
     const int c0 = p * CW, z0 = p * NZ;
     const int NU = (D + UK - 1) / UK;
     const int KW = min(gm::NW, NU);
@@ -168,10 +157,12 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     const T* __restrict__ tab = (const T*)a.tab;
     // optional phase timestamps (workgroup 0, thread 0; s_memrealtime = 100 MHz)
     unsigned long long* dg = (a.diag && blockIdx.x == 0 && tid == 0) ? a.diag : nullptr;
+    unsigned long long* dgb = (a.diag && tid == 0 && blockIdx.x < 1024)
+                                  ? a.diag + 512 + 3 * blockIdx.x : nullptr;
+    if (dgb) dgb[0] = __builtin_amdgcn_s_memrealtime();
     int nd = 0;
 #define GM_STAMP() do { if (dg && nd < 511) dg[nd++] = __builtin_amdgcn_s_memrealtime(); } while (0)
     GM_STAMP();
-    if (dg) dg[511] = local ? 1 : 2;
     // LDS: [tab15 Q x CW][red KW x ntm x 64 floatx4][hist R x HIST]
     T* tab15 = (T*)smem;
     size_t lo = ((size_t)Q * CW * sizeof(T) + 15) & ~(size_t)15;
@@ -184,7 +175,39 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     F wh[UPW][NT], wo[UPW][NZT];
     // (loads from clamped addresses with no branches, so all of them are in flight at once;
     //  fragments outside the shape are zeroed afterwards)
+    int g;
+    bool local;
     {
+        // census arrival first (thread 0)
+        int* cen = nullptr;
+        int slot = 0;
+        unsigned xcc = 0;
+        if (a.census) {
+            const int n = (*a.base + a.off - a.L) / FS0;          // launch index in this call
+            cen = a.census + (n & 1) * HX_KEYED_WORDS;
+            if (tid == 0) slot = hx_census_arrive(cen, p, xcc);
+            else if (blockIdx.x == 0 && wave == 1) {
+                // zero the next launch's array (last used two launches ago)
+                int* nxt = a.census + ((n + 1) & 1) * HX_KEYED_WORDS;
+                for (int j = lane; j < HX_KEYED_WORDS; j += 64)
+                    __hip_atomic_store(nxt + j, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        // ---- row group: static (block % G) or the XCD census.  Wave 0 settles it before
+        //      issuing its own loads (a wave's loads return in order, so a census poll queued
+        //      behind them would wait for the weights); the other waves' loads already fly.
+        if (wave == 0) {
+            int gg = blockIdx.x % a.G;
+            slot = __shfl(slot, 0);
+            xcc = (unsigned)__builtin_amdgcn_readfirstlane((int)xcc);
+            const int loc = cen && hx_census_finish(cen, a.P, slot, xcc, a.err, gg) ? 1 : 0;
+            if (!loc) gg = blockIdx.x % a.G;
+            if (tid == 0) {
+                gsh[0] = gg; gsh[2] = loc;
+                GM_STAMP();
+                if (dgb) dgb[1] = __builtin_amdgcn_s_memrealtime();
+            }
+        }
         uint4 lw[UPW][NT], lz[UPW][NZT];
 #pragma unroll
         for (int j = 0; j < UPW; ++j) {
@@ -201,6 +224,22 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 lz[j][t] = *reinterpret_cast<const uint4*>((const T*)a.w_out + (int64_t)n * D + ke);
             }
         }
+        constexpr int PER = 16 / sizeof(T);
+        const int cpr = CW / PER;                       // pieces per table row
+        const int npc = Q * cpr;
+        constexpr int MAXIT = gm::Q * 64 * 4 / 16 / gm::NTHR;   // fp32, CW = 64: 8
+        uint4 buf[MAXIT];
+#pragma unroll
+        for (int it = 0; it < MAXIT; ++it) {
+            const int e = min(tid + it * gm::NTHR, npc - 1);
+            const int q = e / cpr, c = (e % cpr) * PER;
+            buf[it] = *reinterpret_cast<const uint4*>(
+                tab + ((int64_t)(FS0 - 1) * Q + q) * D + c0 + c);
+        }
+        __syncthreads();
+        g = gsh[0];
+        local = gsh[2] != 0;
+        if (dg) dg[511] = local ? 1 : 2;
 #pragma unroll
         for (int j = 0; j < UPW; ++j) {
             const int u = wave + gm::NW * j;
@@ -218,30 +257,17 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                                       v ? lz[j][t].z : 0u, v ? lz[j][t].w : 0u);
             }
         }
-    }
-    // ---- newest-tap table slice and the sample history of this group's rows
-    const int i0 = *a.base + a.off;
-    {
-        // Q x CW slice in 16-B pieces, all loads in flight before the LDS stores
-        constexpr int PER = 16 / sizeof(T);
-        const int cpr = CW / PER;                       // pieces per table row
-        const int npc = Q * cpr;
-        constexpr int MAXIT = gm::Q * 64 * 4 / 16 / gm::NTHR;   // fp32, CW = 64: 8
-        uint4 buf[MAXIT];
-#pragma unroll
-        for (int it = 0; it < MAXIT; ++it) {
-            const int e = min(tid + it * gm::NTHR, npc - 1);
-            const int q = e / cpr, c = (e % cpr) * PER;
-            buf[it] = *reinterpret_cast<const uint4*>(
-                tab + ((int64_t)(FS0 - 1) * Q + q) * D + c0 + c);
-        }
+        // newest-tap table slice (Q x CW, loaded in 16-B pieces above, before the census wait)
         // (clamped pieces store the same bytes to the same slot: no branch)
 #pragma unroll
         for (int it = 0; it < MAXIT; ++it) {
             const int e = min(tid + it * gm::NTHR, npc - 1);
             *reinterpret_cast<uint4*>(tab15 + (size_t)e * PER) = buf[it];
         }
+        GM_STAMP();
     }
+    // ---- the sample history of this group's rows
+    const int i0 = *a.base + a.off;
     for (int e = tid; e < R * FS0; e += gm::NTHR) {
         const int r = e / FS0, k = e % FS0;
         const int b = min(g * R + r, B - 1);
@@ -297,6 +323,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     };
 
     GM_STAMP();
+    if (dgb) dgb[2] = __builtin_amdgcn_s_memrealtime();
     issue_part(i0);
     finish_part();
     publish_a1(i0);
@@ -500,19 +527,32 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     return 1;
 }
 
+#define GM_DIAG_BLOCKS 1024
+#define GM_DIAG_WORDS (512 + 3 * GM_DIAG_BLOCKS)
 unsigned long long*& gm_diag_buf() {
     static unsigned long long* p = nullptr;
     return p;
 }
 
 extern "C" int srnn_gen_diag_dump(void) {
-    unsigned long long h[512];
+    static unsigned long long h[GM_DIAG_WORDS];
     if (!gm_diag_buf() || hipDeviceSynchronize() != hipSuccess ||
         hipMemcpy(h, gm_diag_buf(), sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
         return 1;
     fprintf(stderr, "gen_mlp diag mode: %s\n", h[511] == 1 ? "xcd-local" : "static map");
     for (int k = 1; k < 511 && h[k]; ++k)
         fprintf(stderr, "gen_mlp diag %3d: +%8.2f us\n", k, (double)(h[k] - h[k - 1]) / 100.0);
+    // per-workgroup start / group known / prologue done, relative to the earliest start
+    unsigned long long t0 = ~0ull, smax = 0, cmax = 0, pmax = 0;
+    int nb = 0;
+    for (int b = 0; b < GM_DIAG_BLOCKS && h[512 + 3 * b]; ++b, ++nb) t0 = std::min(t0, h[512 + 3 * b]);
+    for (int b = 0; b < nb; ++b) {
+        smax = std::max(smax, h[512 + 3 * b] - t0);
+        cmax = std::max(cmax, h[513 + 3 * b] - t0);
+        pmax = std::max(pmax, h[514 + 3 * b] - t0);
+    }
+    fprintf(stderr, "gen_mlp diag %d blocks: last start +%.2f us, last group +%.2f us, "
+            "last prologue +%.2f us\n", nb, smax / 100.0, cmax / 100.0, pmax / 100.0);
     return 0;
 }
 
@@ -527,13 +567,15 @@ int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
     {
         // SRNN_GEN_DIAG=1: phase timestamps of the first launch into a device buffer that
         // srnn_gen_diag_dump prints (timing diagnostics only)
+        // (SRNN_GEN_DIAG=n: the n-th launch of the process, so n > 1 skips the cold one)
         static unsigned long long* diag = nullptr;
         static int armed = -1;
         if (armed < 0) armed = env_flag("SRNN_GEN_DIAG", 0);
-        if (armed == 1 && !diag && hipMalloc(&diag, 512 * 8) == hipSuccess) {
-            (void)hipMemsetAsync(diag, 0, 512 * 8, s);
+        // (allocated at the first launch, which runs eagerly, not inside a graph capture)
+        if (armed >= 1 && !diag && hipMalloc(&diag, GM_DIAG_WORDS * 8) == hipSuccess)
+            (void)hipMemset(diag, 0, GM_DIAG_WORDS * 8);
+        if (armed >= 1 && diag && --armed == 0) {
             a.diag = diag;
-            armed = 2;
             gm_diag_buf() = diag;
         }
     }

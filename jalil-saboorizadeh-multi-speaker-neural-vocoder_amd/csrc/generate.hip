@@ -126,7 +126,7 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
     b->gm_bytes = 0;
     if (pl && pl->ok) {
         const size_t start = off;
-        b->gerr = (int*)take(512);           // [0] error word, [64..96) XCD census
+        b->gerr = (int*)take(8192);          // [0] error word, [64..) 2 keyed census arrays
         b->xa1 = (unsigned long long*)take(pl->xa_words * 8);
         b->xa2 = (unsigned long long*)take(pl->xa_words * 8);
         b->xz = (unsigned long long*)take(pl->xz_words * 8);

@@ -59,7 +59,9 @@ __device__ __forceinline__ bool hx_census(int* cur, int P, int* err, int& g, int
     xcc &= 7;
     const int slot = __hip_atomic_fetch_add(cur + xcc, 1, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(cur + 8, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (the arrival depends on the slot, so it issues after the count is performed; relaxed:
+    //  an agent-scope release / acquire would write back / invalidate the whole L2)
+    __hip_atomic_fetch_add(cur + 8, 1 + (slot >> 30), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int spins = 0;
     while (__hip_atomic_load(cur + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
            (int)(gridDim.x * gridDim.y)) {
@@ -74,5 +76,52 @@ __device__ __forceinline__ bool hx_census(int* cur, int P, int* err, int& g, int
     if (!ok) return false;
     g = before / P + slot / P;
     p = slot % P;
+    return true;
+}
+
+// Keyed census: the member index p of every workgroup is fixed by the caller (so everything
+// that depends only on p -- resident weight fragments -- can be loaded before the census);
+// only the group g is assigned.  cur: HX_KEYED_WORDS zeroed words ([x * 64 + p] per-XCC
+// per-member counters, [512] arrivals), P <= 64.  Local mode iff on every XCD all P members
+// occur equally often: then the c_x groups of XCD x take indices [sum_{x'<x} c_x', + c_x)
+// and the member's slot picks one.  Otherwise g keeps the caller's static value.
+#define HX_KEYED_WORDS 520
+// Split in two so the caller can issue its own loads between arrival and the wait.
+// Returns this member's slot on its XCD.
+__device__ __forceinline__ int hx_census_arrive(int* cur, int p, unsigned& xcc) {
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+    xcc &= 7;
+    const int slot = __hip_atomic_fetch_add(cur + xcc * 64 + p, 1, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    // (data-dependent on the slot, so ordered after the count without a release fence,
+    //  which at agent scope would write back the whole L2)
+    __hip_atomic_fetch_add(cur + 512, 1 + (slot >> 30), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return slot;
+}
+// Called by a whole wave (uniform slot / xcc, from the arriving lane): lane q reads the
+// 8 per-XCC counters of member q at once, so the check costs one round trip, not 8 x P.
+__device__ __forceinline__ bool hx_census_finish(int* cur, int P, int slot, unsigned xcc,
+                                                 int* err, int& g) {
+    const int lane = threadIdx.x & 63;
+    int spins = 0;
+    while (__hip_atomic_load(cur + 512, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+           (int)(gridDim.x * gridDim.y)) {
+        if (hx_spin_fail(spins, err, lane)) return false;
+    }
+    const int q = min(lane, P - 1);
+    int v[8];
+#pragma unroll
+    for (int x = 0; x < 8; ++x)
+        v[x] = __hip_atomic_load(cur + x * 64 + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bool ok = true;
+    int before = 0;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) {
+        const int c = __shfl(v[x], 0);
+        ok = ok && __ballot(v[x] != c) == 0;
+        before += x < (int)xcc ? c : 0;
+    }
+    if (!ok) return false;
+    g = before + slot;
     return true;
 }
