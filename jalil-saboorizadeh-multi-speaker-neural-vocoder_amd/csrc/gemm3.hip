@@ -543,7 +543,7 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
         if (++ktc == nk) {
             int m0, n0, kb;
             unit(ic, m0, n0, kb);
-            g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+            if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
             ktc = 0;
             ++ic;
             epi = true;
