@@ -37,10 +37,10 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_model(dtype, seed=77977):
+def make_model(dtype, seed=77977, frame_sizes=(16, 4), cond_dim=43):
     import model as M
     torch.manual_seed(seed)
-    m = M.SampleRNN([16, 4], 1, 1024, True, 256, True, False, 43, 6)
+    m = M.SampleRNN(list(frame_sizes), 1, 1024, True, 256, True, False, cond_dim, 6)
     m.compute_dtype = dtype
     pred = M.Predictor(m)
     return m, pred
@@ -115,11 +115,15 @@ def run_tbptt(args, dev, dist_mod):
     return dt, loss_vals, pred, m
 
 
-def run_gen(args, dev, n_seqs, n_cond, dtype):
+def run_gen(args, dev, n_seqs, n_cond, dtype, frame_sizes=(16, 4), cond_dim=43):
+    """One timed Generator call; returns (seconds, algorithmic weight elements read per
+    generation step: the sample-level MLP every step, tier k once per nfs_k steps)."""
     import model as M
-    m, _ = make_model(dtype, seed=4242)
+    m, _ = make_model(dtype, seed=4242, frame_sizes=frame_sizes, cond_dim=cond_dim)
     m = m.to(dev)
-    cond = torch.rand(n_seqs, n_cond, 43, generator=torch.Generator().manual_seed(1))
+    w_step = sum(p.numel() for p in m.sample_level_mlp.parameters()) + sum(
+        sum(p.numel() for p in t.parameters()) / t.n_frame_samples for t in m.frame_level_rnns)
+    cond = torch.rand(n_seqs, n_cond, cond_dim, generator=torch.Generator().manual_seed(1))
     spk = np.arange(n_seqs) % 6
     gen = M.Generator(m, True)
     # warm-up (graph capture, kernel attributes) on a short run
@@ -128,7 +132,7 @@ def run_gen(args, dev, n_seqs, n_cond, dtype):
     t0 = time.perf_counter()
     gen(n_seqs, 0, cond, spk, sampler='philox', seed=5)
     torch.cuda.synchronize()
-    return time.perf_counter() - t0
+    return time.perf_counter() - t0, w_step
 
 
 def kernel_roofline_gemm(dev, M, N, K, dtype, reps=20):
@@ -207,6 +211,7 @@ def main():
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--gen-dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--no-gen-fp32', action='store_true')
+    ap.add_argument('--no-gen-e', action='store_true')
     ap.add_argument('--gen-seqs', type=int, default=128)
     ap.add_argument('--gen-cond', type=int, default=750)
     ap.add_argument('--no-gen', action='store_true')
@@ -230,16 +235,18 @@ def main():
     del pred, m
     torch.cuda.empty_cache()
 
-    def gen_line(dname):
+    def gen_line(dname, frame_sizes=(16, 4), cond_dim=43, n_cond=None, tag='3-tier dim1024 '
+                 'FS=[16,4]'):
         gdt = torch.bfloat16 if dname == 'bf16' else torch.float32
-        t = run_gen(args, dev, args.gen_seqs, args.gen_cond, gdt)
+        n_cond = n_cond or args.gen_cond
+        L = int(np.prod(frame_sizes))
+        t, W_step = run_gen(args, dev, args.gen_seqs, n_cond, gdt, frame_sizes, cond_dim)
         t = D.max_over_ranks(t, dev)
-        gs = N * args.gen_seqs * args.gen_cond * 64 / t
-        steps_per_s = args.gen_cond * 64 / t
+        gs = N * args.gen_seqs * n_cond * L / t
+        steps_per_s = n_cond * L / t
         # algorithmic bytes per generation step: weights read once per step,
-        # tiers amortised by their clocks, + per-row activations
+        # tiers amortised by their clocks (config C: 7,182,145 weights), + per-row activations
         es = 2 if dname == 'bf16' else 4
-        W_step = 5571840 + 23110656 / 16 + 10616868 / 64
         bytes_step = es * W_step + args.gen_seqs * (4 * (1024 + 256) + 8 * 16 + 8)
         import samplernn_hip as H
         rows_pg = H.gen_persistent_rows(gdt, args.gen_seqs, 1024, 16)
@@ -250,9 +257,9 @@ def main():
                 'us_per_step': round(1e6 / steps_per_s, 2),
                 'sample_loop': ('persistent (gen_mlp.hip, %d rows/group)' % rows_pg) if rows_pg
                                else 'per-sample kernels (hipGraph)',
-                'config': {'workload': 'generate 3-tier dim1024 FS=[16,4], %d utt x %d cond '
-                                       'rows (%d samples) per GPU, Philox sampler'
-                                       % (args.gen_seqs, args.gen_cond, args.gen_cond * 64)},
+                'config': {'workload': 'generate %s cond %d, %d utt x %d cond rows (%d samples) '
+                                       'per GPU, Philox sampler'
+                                       % (tag, cond_dim, args.gen_seqs, n_cond, n_cond * L)},
                 'roofline': {'bound': 'hbm',
                              'achieved': round(bytes_step * steps_per_s / 1e9, 1),
                              'peak': MI355X_HBM_TBS * 1000, 'unit': 'GB/s',
@@ -260,11 +267,16 @@ def main():
                                            (MI355X_HBM_TBS * 1000), 4),
                              'traffic': None}}
 
-    gen = gen_fp32 = None
+    gen = gen_fp32 = gen_e = None
     if not args.no_gen:
         gen = gen_line(args.gen_dtype)
         if args.gen_dtype != 'fp32' and not args.no_gen_fp32:
             gen_fp32 = gen_line('fp32')       # parity-grade numerics (bit-replay tests)
+        if not args.no_gen_e:
+            # configs[4]: 4-tier + look-ahead conditioning (C = 86), 1024 utterances over 8
+            # GPUs = 128 per GPU (replicas), 188 cond rows x 256 = 48,128 samples each
+            gen_e = gen_line(args.gen_dtype, (16, 4, 4), 86, 188,
+                             '4-tier dim1024 FS=[16,4,4] look-ahead')
 
     # dominant kernel of the TBPTT step: the MLP hidden layer GEMM (B*T x D x D, bf16)
     tdt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
@@ -297,6 +309,7 @@ def main():
                            'parallelism': 'dp%d' % N},
                 'tbptt_steps_per_s': round(args.steps / dt, 3),
                 'roofline': roof, 'cpu_baseline': cpu, 'gen': gen, 'gen_fp32': gen_fp32,
+                'gen_config_e': gen_e,
                 'final_loss': round(losses[-1], 4)}
         print(json.dumps(line), flush=True)
     D.barrier()
