@@ -110,6 +110,8 @@ def run_tbptt(args, dev, dist_mod):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     sys.stderr.write('tbptt host enqueue %.2f ms/step\n' % (t_host * 1e3 / max(args.steps, 1)))
+    import samplernn_hip as H
+    H.check_persistent_errors()            # (after the timed region) no hand-off given up
     dt = dist_mod.max_over_ranks(dt, dev)
     loss_vals = [float(l.detach()) if torch.is_tensor(l) else float(l) for l in losses]
     return dt, loss_vals, pred, m

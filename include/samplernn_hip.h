@@ -94,6 +94,11 @@ int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy, int64_t l
                      float* dgi, int64_t ldd, int64_t sd, float* ddir0, void* work,
                      size_t work_bytes, void* stream);
 int srnn_gru_xcd_error(const void* work);
+/* Sticky form for callers that do not keep the work buffer: nonzero if ANY persistent GRU
+ * sweep (srnn_gru_xcd_fwd/bwd) since the previous call gave up a hand-off, -1 on a HIP
+ * error; clears the flag and synchronises the device.  The training path checks it once per
+ * Trainer iteration (the reference has no equivalent: its cuDNN GRU cannot fail this way). */
+int srnn_persistent_error_take(void);
 int srnn_gru_seq_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
                      int64_t sgi, const float* h0, const void* h0_lp, const void* whh,
                      const float* bhh, float* out, void* out_lp, int64_t ldo, int64_t so,

@@ -28,6 +28,15 @@ constexpr int NT = 6;                  // n tiles: 3 gates x 2 x 16 units
 constexpr int UK = 32;                 // k per bf16 MFMA unit
 }  // namespace gx
 
+// Sticky failure flag of the persistent sweeps: the per-call error word lives in a work
+// buffer the next call re-zeroes, so every workgroup folds it in here on exit and the host
+// reads it at its own sync points (srnn_persistent_error_take).
+__device__ int gx_sticky_err;
+__device__ __forceinline__ void gx_note_failure(const int* err) {
+    if (threadIdx.x == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        __hip_atomic_store(&gx_sticky_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 struct GruXArgs {
     const float* gi; int64_t ldgi; int64_t sgi;     // gi[b][t] (3D, includes b_ih)
     const float* h0;                                // (B, D) fp32
@@ -198,6 +207,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
         GX_STAMP();
     }
 #undef GX_STAMP
+    gx_note_failure(a.err);
 }
 
 // ------------------------------------------------------------------ backward
@@ -365,6 +375,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
         }
         __syncthreads();
     }
+    gx_note_failure(a.err);
 }
 
 // ------------------------------------------------------------------ host side
@@ -503,6 +514,17 @@ extern "C" int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy
     hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;
+}
+
+// nonzero if any persistent GRU sweep since the last call gave up a hand-off (its results
+// are invalid); clears the flag.  Synchronises the device.
+extern "C" int srnn_persistent_error_take(void) {
+    int v = 0, z = 0;
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(&v, HIP_SYMBOL(gx_sticky_err), sizeof(int)) != hipSuccess)
+        return -1;
+    if (v && hipMemcpyToSymbol(HIP_SYMBOL(gx_sticky_err), &z, sizeof(int)) != hipSuccess) return -1;
+    return v;
 }
 
 // nonzero if the previous srnn_gru_xcd_fwd/bwd on `work` gave up a hand-off (synchronises)

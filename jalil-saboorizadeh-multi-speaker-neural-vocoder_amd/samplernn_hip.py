@@ -119,7 +119,21 @@ def lib():
 def exported_symbols():
     return sorted(_SIGS) + ['srnn_last_error', 'srnn_abi_version', 'srnn_gru_seq_supported',
                             'srnn_gen_persistent_rows', 'srnn_gru_xcd_work_bytes',
-                            'srnn_gru_xcd_bwd_work_bytes', 'srnn_gru_xcd_error']
+                            'srnn_gru_xcd_bwd_work_bytes', 'srnn_gru_xcd_error',
+                            'srnn_persistent_error_take']
+
+
+def check_persistent_errors():
+    """Raise if a persistent GRU sweep gave up a hand-off since the last check (its outputs
+    are invalid).  Synchronises the device; the Trainer calls it once per iteration."""
+    fn = lib().dll.srnn_persistent_error_take
+    fn.restype = ctypes.c_int
+    fn.argtypes = []
+    v = fn()
+    if v:
+        raise RuntimeError('persistent GRU sweep gave up a hand-off (bounded spin) -- results of '
+                           'this step are invalid' if v > 0 else
+                           'srnn_persistent_error_take: HIP error')
 
 
 _GRU_XCD = {}

@@ -11,6 +11,8 @@ import heapq
 
 import torch
 
+import samplernn_hip as H
+
 
 class Trainer(object):
 
@@ -111,6 +113,8 @@ class Trainer(object):
 
             self._zero_grad()
             self.optimizer.step(closure)
+            if self.cuda:
+                H.check_persistent_errors()
             self.call_plugins('iteration', self.iterations, batch_inputs, batch_target,
                               *plugin_data)
             self.call_plugins('update', self.iterations, self.model)

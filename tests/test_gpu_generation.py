@@ -76,6 +76,31 @@ def test_persistent_bf16_d1024(hip, B):
     assert err.mean().item() < 0.02, err.mean().item()
 
 
+def test_config_e_bf16_d1024(hip):
+    """configs[4] at full width: 4 tiers FS=[16,4,4], look-ahead conditioning (C = 86),
+    D = 1024, 128 utterances (one GPU's share of 1024), bf16 persistent loop.  Same sampler
+    identity and teacher-forced bound as the 3-tier test; 2 top-tier frames = 512 samples."""
+    cfg = dict(recipe.CONFIGS['t4la'], dim=1024)
+    m, pred = build(cfg, 13, torch.bfloat16)
+    B, n_cond = 128, 2
+    assert hip.gen_persistent_rows(torch.bfloat16, B, 1024, 16) > 0
+    cond = recipe.synth_cond((B, n_cond, cfg['cond_dim']), 7)
+    spk = np.arange(B) % cfg['spk_dim']
+    L = m.lookback
+    assert L == 256
+    noise = torch.from_numpy(recipe.synth_noise((n_cond * L, B, 256), 4))
+    seq, lp = generate(m, B, cond, spk, True, noise=noise)
+    drawn = torch.argmax(torch.exp(lp) / noise.permute(1, 0, 2), dim=-1)
+    assert torch.equal(drawn, seq[:, L:])
+    m.compute_dtype = torch.float32
+    with torch.no_grad():
+        tf = pred(seq[:, :-1], True, torch.from_numpy(cond),
+                  torch.from_numpy(spk).reshape(-1, 1)).cpu()
+    err = (tf - lp).abs()
+    assert err.max().item() < 0.25, err.max().item()
+    assert err.mean().item() < 0.02, err.mean().item()
+
+
 def test_persistent_philox_matches_per_sample_fp32(hip):
     """Device RNG: both paths draw Philox4x32-10(seed) noise with the same counters."""
     cfg = dict(recipe.CONFIGS['t3'], dim=128)
