@@ -112,6 +112,13 @@ def run_tbptt(args, dev, dist_mod):
     sys.stderr.write('tbptt host enqueue %.2f ms/step\n' % (t_host * 1e3 / max(args.steps, 1)))
     import samplernn_hip as H
     H.check_persistent_errors()            # (after the timed region) no hand-off given up
+    if H.HOST_TIME:
+        n_all = args.warmup + args.steps
+        tot = sum(s for _, s in H.HOST_TIME.values())
+        sys.stderr.write('host time in C entry points: %.2f ms/step (%d calls/step)\n' % (
+            tot * 1e3 / n_all, sum(n for n, _ in H.HOST_TIME.values()) // n_all))
+        for name, (n, s) in sorted(H.HOST_TIME.items(), key=lambda kv: -kv[1][1])[:30]:
+            sys.stderr.write('  %-34s %6d calls %8.1f us/call\n' % (name, n, s * 1e6 / n))
     dt = dist_mod.max_over_ranks(dt, dev)
     loss_vals = [float(l.detach()) if torch.is_tensor(l) else float(l) for l in losses]
     return dt, loss_vals, pred, m

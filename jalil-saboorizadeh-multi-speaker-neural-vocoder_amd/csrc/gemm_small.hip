@@ -212,7 +212,12 @@ __global__ __launch_bounds__(256) void gemm_small_nt_sum_kernel(const float* __r
     C[(int64_t)m * ldc + n] = alpha * s;
 }
 
-static bool g_pool_set = false;
+// Split-K partials of the thin NT path: one grow-only scratch buffer reused by every call
+// (stream-ordered on the caller's stream).  A stream-ordered hipMallocAsync per call cost
+// up to 4 ms of host time per TBPTT step (the 1024 x 64 x 2048 input-projection weight
+// gradient), which stalled the launch queue; growth only happens on the first calls.
+static float* g_nt_scratch = nullptr;
+static size_t g_nt_bytes = 0;
 
 template <typename T>
 static int launch_small_nt(const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
@@ -222,17 +227,16 @@ static int launch_small_nt(const void* A, int64_t lda, const void* B, int64_t ld
     int nks = std::max(1, std::min(cdiv(K, 4 * gsn::KR), cdiv(768, mblk * ngrp)));
     const int kchunk = cdiv(cdiv(K, nks), 4 * gsn::KR) * 4 * gsn::KR;
     nks = cdiv(K, kchunk);
-    if (!g_pool_set) {   // keep freed scratch in the stream-ordered pool
-        int dev = 0;
-        hipMemPool_t pool;
-        if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
-            uint64_t thr = ~0ull;
-            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
-        }
-        g_pool_set = true;
+    const size_t need = (size_t)nks * N * M * sizeof(float);
+    if (need > g_nt_bytes) {
+        // (hipFree waits for the device, so no in-flight call still reads the old buffer)
+        if (g_nt_scratch) SRNN_CHECK_HIP(hipFree(g_nt_scratch));
+        g_nt_scratch = nullptr;
+        g_nt_bytes = 0;
+        SRNN_CHECK_HIP(hipMalloc((void**)&g_nt_scratch, need));
+        g_nt_bytes = need;
     }
-    float* P = nullptr;
-    SRNN_CHECK_HIP(hipMallocAsync((void**)&P, (size_t)nks * N * M * sizeof(float), s));
+    float* P = g_nt_scratch;
     hipLaunchKernelGGL((gemm_small_nt_part_kernel<T>), dim3(mblk, ngrp, nks), dim3(256), 0, s,
                        (const T*)A, lda, (const T*)B, ldb, P, M, N, K, kchunk);
     SRNN_LAUNCH_CHECK();
@@ -240,7 +244,6 @@ static int launch_small_nt(const void* A, int64_t lda, const void* B, int64_t ld
     hipLaunchKernelGGL(gemm_small_nt_sum_kernel, dim3((unsigned)cdiv(tot, (int64_t)256)),
                        dim3(256), 0, s, P, C, ldc, M, N, nks, alpha);
     SRNN_LAUNCH_CHECK();
-    SRNN_CHECK_HIP(hipFreeAsync(P, s));
     return 0;
 }
 

@@ -630,23 +630,23 @@ def generation_weights(model, dtype=None):
                 t.in_dim = nfs
                 b_in = rnn.input_expand.bias.detach().contiguous()
                 keep.append(b_in)
-                t.b_in = H.ptr(b_in).value
+                t.b_in = H.ptr(b_in)
             keep.append(w_in)
-            t.w_in = H.ptr(w_in).value
+            t.w_in = H.ptr(w_in)
             for l in range(model.n_rnn):
                 wih = H.cast(getattr(rnn.rnn, 'weight_ih_l%d' % l).detach().contiguous(), T)
                 whh = H.cast(getattr(rnn.rnn, 'weight_hh_l%d' % l).detach().contiguous(), T)
                 bih = getattr(rnn.rnn, 'bias_ih_l%d' % l).detach().contiguous()
                 bhh = getattr(rnn.rnn, 'bias_hh_l%d' % l).detach().contiguous()
                 keep += [wih, whh, bih, bhh]
-                t.w_ih[l], t.w_hh[l] = H.ptr(wih).value, H.ptr(whh).value
-                t.b_ih[l], t.b_hh[l] = H.ptr(bih).value, H.ptr(bhh).value
+                t.w_ih[l], t.w_hh[l] = H.ptr(wih), H.ptr(whh)
+                t.b_ih[l], t.b_hh[l] = H.ptr(bih), H.ptr(bhh)
             k_ = rnn.frame_size
             w_up = H.permute3(nn.weight_of(rnn.upsampling.conv_t), (2, 1, 0), dtype=T)
             b_up = H.permute3(rnn.upsampling.bias.detach().reshape(1, D, k_), (0, 2, 1))
             h0 = rnn.h0.detach().float().contiguous()
             keep += [w_up, b_up, h0]
-            t.w_up, t.b_up, t.h0 = H.ptr(w_up).value, H.ptr(b_up).value, H.ptr(h0).value
+            t.w_up, t.b_up, t.h0 = H.ptr(w_up), H.ptr(b_up), H.ptr(h0)
         mlp = model.sample_level_mlp
         tab = mlp.tab(T)
         w_hid = H.cast(nn.weight_of(mlp.hidden).reshape(D, D).contiguous(), T)
@@ -654,8 +654,8 @@ def generation_weights(model, dtype=None):
         b_hid = mlp.hidden.bias.detach().contiguous()
         b_out = mlp.output.bias.detach().contiguous()
         keep += [tab, w_hid, w_out, b_hid, b_out]
-        m.tab, m.w_hid, m.w_out = H.ptr(tab).value, H.ptr(w_hid).value, H.ptr(w_out).value
-        m.b_hid, m.b_out = H.ptr(b_hid).value, H.ptr(b_out).value
+        m.tab, m.w_hid, m.w_out = H.ptr(tab), H.ptr(w_hid), H.ptr(w_out)
+        m.b_hid, m.b_out = H.ptr(b_hid), H.ptr(b_out)
     return m, keep
 
 

@@ -97,12 +97,36 @@ class _Lib:
             fn = getattr(self.dll, name)
             fn.argtypes = args
             fn.restype = _I
+        # query entry points called on .dll directly (pointers are passed as plain ints, so
+        # every pointer argument needs its declared type)
+        for name, args in (('srnn_gru_xcd_error', [_P]), ('srnn_persistent_error_take', [])):
+            fn = getattr(self.dll, name)
+            fn.argtypes = args
+            fn.restype = _I
 
     def call(self, name, *args):
         rc = getattr(self.dll, name)(*args)
         if rc != 0:
             raise RuntimeError('%s failed (%d): %s' % (name, rc,
                                                        self.dll.srnn_last_error().decode()))
+
+    def call_timed(self, name, *args):
+        t0 = time.perf_counter()
+        try:
+            self._call(name, *args)
+        finally:
+            key = name if name != 'srnn_gemm' else 'gemm %dx%dx%d t%d%d' % (
+                args[4], args[5], args[6], args[2], args[3])
+            n, s = HOST_TIME.get(key, (0, 0.0))
+            HOST_TIME[key] = (n + 1, s + time.perf_counter() - t0)
+
+
+# SRNN_HOST_PROF=1: host seconds spent inside each C entry point (argument conversion + the
+# HIP launch calls), to find launch-bound stretches of a step; bench.py prints the table
+HOST_TIME = {}
+if os.environ.get('SRNN_HOST_PROF', '0') == '1':
+    _Lib._call = _Lib.call
+    _Lib.call = _Lib.call_timed
 
 
 _LIB = None
@@ -195,14 +219,21 @@ def gru_seq_supported(dtype, B, D):
 
 # ------------------------------------------------------------------ helpers
 def ptr(t):
-    """Device/host pointer of a tensor (None -> NULL)."""
+    """Device/host pointer of a tensor (None -> NULL).  A plain int: ctypes converts it for
+    c_void_p arguments and struct fields without building an object per call."""
     if t is None:
         return None
-    return ctypes.c_void_p(t.data_ptr())
+    return t.data_ptr()
+
+
+_raw_stream = torch._C._cuda_getCurrentRawStream
+_cur_dev = torch._C._cuda_getDevice
 
 
 def stream():
-    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    """hipStream_t of the current torch stream, as an int (hundreds of calls per TBPTT step:
+    no torch.cuda.Stream object is built per call)."""
+    return _raw_stream(_cur_dev())
 
 
 def dcode(t_or_dtype):
