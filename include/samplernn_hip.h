@@ -177,7 +177,8 @@ int srnn_adam_clip(float* p, float* g, float* m, float* v, void* p_bf16, int64_t
                    float clip_lo, float clip_hi, double lr, double beta1, double beta2,
                    double eps, int64_t step, void* stream);
 /* The same for `ntensors` parameters in one launch (per 64 tensors): host arrays of device
- * pointers and element counts; p_bf16 may be NULL (no copies) or hold NULL entries.      */
+ * pointers and element counts; p_bf16 may be NULL (no copies) or hold NULL entries; a NULL
+ * entry of g is an all-zero gradient (a parameter the step's backward did not reach).    */
 int srnn_adam_clip_multi(int ntensors, float* const* p, float* const* g, float* const* m,
                          float* const* v, void* const* p_bf16, const int64_t* n, float clip_lo,
                          float clip_hi, double lr, double beta1, double beta2, double eps,

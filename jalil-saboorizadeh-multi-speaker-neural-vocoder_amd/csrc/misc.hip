@@ -647,8 +647,13 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
     for (int i = threadIdx.x; i < CH; i += 256) {
         const int64_t j = j0 + i;
         if (j >= n) return;
-        float gi = fminf(fmaxf(G[j], lo), hi);
-        G[j] = gi;
+        // (a null gradient is an all-zero one: a parameter backward did not reach this
+        //  step, e.g. the learned h0 on a carried chunk -- torch-0.4 zero_grad semantics)
+        float gi = 0.f;
+        if (G) {
+            gi = fminf(fmaxf(G[j], lo), hi);
+            G[j] = gi;
+        }
         float mi = Mm[j];
         mi = mi + w1 * (gi - mi);
         float vi = V[j] * b2;

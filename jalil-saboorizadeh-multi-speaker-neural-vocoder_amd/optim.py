@@ -33,9 +33,9 @@ def _fused_adam_step(optimizer, lo, hi):
                 st['step'] = torch.tensor(0.0, dtype=torch.float32)
                 st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
-            if p.grad is None:
-                p.grad = torch.zeros_like(p)
-            elif not p.grad.is_contiguous() or p.grad.dtype != torch.float32:
+            # a None grad goes to the kernel as NULL = all-zero (no zero-fill launch)
+            if p.grad is not None and (not p.grad.is_contiguous() or
+                                       p.grad.dtype != torch.float32):
                 p.grad = p.grad.float().contiguous()
             if not (p.is_contiguous() and p.dtype == torch.float32):
                 raise NotImplementedError('fused clip+Adam: contiguous fp32 parameters only')
@@ -43,7 +43,8 @@ def _fused_adam_step(optimizer, lo, hi):
             by_step.setdefault(int(st['step'].item()), []).append((p, st))
         for step, items in sorted(by_step.items()):
             n = len(items)
-            arr = lambda ts: (ctypes.c_void_p * n)(*[t.data_ptr() for t in ts])  # noqa: E731
+            arr = lambda ts: (ctypes.c_void_p * n)(  # noqa: E731
+                *[t.data_ptr() if t is not None else None for t in ts])
             H.lib().call('srnn_adam_clip_multi', n, arr([p for p, _ in items]),
                          arr([p.grad for p, _ in items]), arr([s['exp_avg'] for _, s in items]),
                          arr([s['exp_avg_sq'] for _, s in items]), None,
