@@ -38,6 +38,8 @@ struct Gemm3Args {
     float alpha, beta;
     int bias_mode, relu;
     int diag;   // timing experiments (SRNN_G3DIAG): 1 no MFMA, 2 no DMA wait, 4 no DMA, 8 no epilogue
+    float* part;  // split-K: [ksplit][M][N] fp32 partial tiles (summed in k order by
+                  // g3_splitk_sum_kernel: deterministic); null -> fp32 atomics into C
 };
 
 namespace g3 {
@@ -146,9 +148,26 @@ __device__ __forceinline__ void g3_store4(bf16* p, const float (&v)[4]) {
 // epilogue of one finished tile (registers -> C); zeroes the accumulators
 template <typename TO, bool SW, bool CIN>
 __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
-                                              int n0, int wm, int wn, int lane) {
+                                              int n0, int wm, int wn, int lane, int kb) {
     if constexpr (!SW) {
         // plain fp32 partials: lane holds 4 rows x 1 column per fragment
+        if (g.ksplit > 1 && g.part) {
+            // this k-slice's partial tile, plain stores (rows of 16 consecutive columns)
+            float* Pz = g.part + (size_t)(kb / (g.K / g.ksplit)) * g.M * g.N;
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int col = n0 + wn * 64 + j * 16 + (lane & 15);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int row = m0 + wm * 128 + i * 16 + (lane >> 4) * 4 + e;
+                        Pz[(int64_t)row * g.N + col] = g.alpha * acc[i][j][e];
+                    }
+                    acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+                }
+            return;
+        }
         float* Cf = reinterpret_cast<float*>(g.C);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
@@ -241,9 +260,23 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 // for every store issued before it (32 serialised store round trips per tile).
 template <typename TO, bool SW>
 __device__ __forceinline__ void g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
-                                            int n0, int wm, int wn, int lane) {
-    if (SW && g.beta != 0.f) g3_epilogue_t<TO, SW, true>(g, acc, m0, n0, wm, wn, lane);
-    else g3_epilogue_t<TO, SW, false>(g, acc, m0, n0, wm, wn, lane);
+                                            int n0, int wm, int wn, int lane, int kb) {
+    if (SW && g.beta != 0.f) g3_epilogue_t<TO, SW, true>(g, acc, m0, n0, wm, wn, lane, kb);
+    else g3_epilogue_t<TO, SW, false>(g, acc, m0, n0, wm, wn, lane, kb);
+}
+
+// C[m][n] = sum_z part[z][m][n], z in order (4 columns per thread)
+__global__ __launch_bounds__(256) void g3_splitk_sum_kernel(const float* __restrict__ part,
+                                                             float* __restrict__ C, int64_t ldc,
+                                                             int M, int N, int ks) {
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;      // float4 index
+    const int64_t MN = (int64_t)M * N;
+    if (q * 4 >= MN) return;
+    const int64_t e = q * 4;
+    const int m = (int)(e / N), n = (int)(e % N);
+    floatx4 s = *reinterpret_cast<const floatx4*>(part + e);
+    for (int z = 1; z < ks; ++z) s += *reinterpret_cast<const floatx4*>(part + z * MN + e);
+    *reinterpret_cast<floatx4*>(C + (int64_t)m * ldc + n) = s;
 }
 
 // Persistent: workgroup w owns work units w, w + G, ... (unit = output tile x k-slice);
@@ -349,7 +382,7 @@ __global__ __launch_bounds__(512, 1) void gemm3_kernel(Gemm3Args g) {
         if (++ktc == nk) {
             int m0, n0, kb;
             unit(ic, m0, n0, kb);
-            g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+            g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
             ktc = 0;
             ++ic;
             epi = true;
@@ -543,7 +576,7 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
         if (++ktc == nk) {
             int m0, n0, kb;
             unit(ic, m0, n0, kb);
-            if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+            if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
             ktc = 0;
             ++ic;
             epi = true;
@@ -712,7 +745,7 @@ __global__ __launch_bounds__(512, 1) void gemm3pp_kernel(Gemm3Args g) {
         if (epi) {
             int m0, n0, kb;
             unit(ic - 1, m0, n0, kb);
-            if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+            if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
             epi = false;
         }
 #pragma unroll
@@ -754,7 +787,7 @@ __global__ __launch_bounds__(512, 1) void gemm3pp_kernel(Gemm3Args g) {
     if (epi) {
         int m0, n0, kb;
         unit(ic - 1, m0, n0, kb);
-        g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+        g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
     }
 }
 
@@ -860,7 +893,7 @@ __global__ __launch_bounds__(512, 1) void gemm3q_kernel(Gemm3Args g) {
         if (epi) {
             int m0, n0, kb;
             unit(ic - 1, m0, n0, kb);
-            if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+            if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
             epi = false;
         }
         {
@@ -907,7 +940,7 @@ __global__ __launch_bounds__(512, 1) void gemm3q_kernel(Gemm3Args g) {
     if (epi) {
         int m0, n0, kb;
         unit(ic - 1, m0, n0, kb);
-        if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane);
+        if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
     }
 }
 
@@ -1011,7 +1044,23 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
         if (wg3 < 192 && wg2 > wg3) return -1;
     }
     g.ksplit = ks;
-    if (ks > 1) {
+    g.part = nullptr;
+    const bool det = ks > 1 && env_flag("SRNN_G3_SPLITK_PART", 1) && g3_mode() <= 2 &&
+                     ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
+    if (ks > 1 && det) {
+        // partial tiles in a grow-only scratch, then one ordered sum (no memset, no atomics)
+        static float* scratch = nullptr;
+        static size_t bytes = 0;
+        const size_t need = (size_t)ks * M * N * sizeof(float);
+        if (need > bytes) {
+            if (scratch) SRNN_CHECK_HIP(hipFree(scratch));
+            scratch = nullptr;
+            bytes = 0;
+            SRNN_CHECK_HIP(hipMalloc((void**)&scratch, need));
+            bytes = need;
+        }
+        g.part = scratch;
+    } else if (ks > 1) {
         if (ldc == N) {
             SRNN_CHECK_HIP(hipMemsetAsync(C, 0, (size_t)M * N * 4, s));
         } else {
@@ -1019,7 +1068,15 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
         }
     }
     const bool kca = !transA, kcb = transB;
-    if (ks > 1) return launch3_layout<float, false>(g, kca, kcb, s);
+    if (ks > 1) {
+        const int rc = launch3_layout<float, false>(g, kca, kcb, s);
+        if (rc || !g.part) return rc;
+        const int64_t nq = (int64_t)M * N / 4;
+        hipLaunchKernelGGL(g3_splitk_sum_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0,
+                           s, (const float*)g.part, (float*)C, ldc, M, N, ks);
+        SRNN_LAUNCH_CHECK();
+        return 0;
+    }
     if (out_dtype == SRNN_F32) return launch3_layout<float, true>(g, kca, kcb, s);
     return launch3_layout<bf16, true>(g, kca, kcb, s);
 }
