@@ -64,7 +64,7 @@ def _train(model, data, rows, grad_sync):
             closure.h = h_new
             return loss
         opt.zero_grad(set_to_none=False)
-        losses.append(float(opt.step(closure)))
+        losses.append(float(opt.step(closure).detach()))
         h = closure.h
     return losses, [p.detach().clone() for p in model.parameters()]
 

@@ -96,7 +96,7 @@ def test_tbptt_golden(hip, name):
 
     def criterion(out, tgt):
         loss = snn.sequence_nll_loss_bits(out, tgt)
-        losses.append(float(loss))
+        losses.append(float(loss.detach()))
         return loss
     data = [(torch.from_numpy(g['input_%d' % s]), torch.tensor([int(g['reset_%d' % s])] * B),
              torch.from_numpy(g['target_%d' % s]), torch.from_numpy(g['cond_%d' % s]),
