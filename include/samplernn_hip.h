@@ -95,10 +95,16 @@ int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy, int64_t l
                      size_t work_bytes, void* stream);
 int srnn_gru_xcd_error(const void* work);
 /* Sticky form for callers that do not keep the work buffer: nonzero if ANY persistent GRU
- * sweep (srnn_gru_xcd_fwd/bwd) since the previous call gave up a hand-off, -1 on a HIP
- * error; clears the flag and synchronises the device.  The training path checks it once per
- * Trainer iteration (the reference has no equivalent: its cuDNN GRU cannot fail this way). */
+ * sweep (srnn_gru_xcd_fwd/bwd, srnn_gru_seq_fwd/bwd) since the previous call gave up a
+ * hand-off, -1 on a HIP error; clears the flag and synchronises the device.  While the flag
+ * is up srnn_adam_clip_multi skips its update (the failed step's gradients never reach the
+ * weights).  The training path checks it once per Trainer iteration (the reference has no
+ * equivalent: its cuDNN GRU cannot fail this way).                                        */
 int srnn_persistent_error_take(void);
+/* Stream-ordered access to that flag for data parallelism: dst = flag ? 1.f : 0.f, and
+ * flag |= (src > 0).  The flag rides in a gradient bucket so every rank agrees.           */
+int srnn_persistent_flag_to_f32(float* dst, void* stream);
+int srnn_persistent_flag_or_f32(const float* src, void* stream);
 int srnn_gru_seq_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
                      int64_t sgi, const float* h0, const void* h0_lp, const void* whh,
                      const float* bhh, float* out, void* out_lp, int64_t ldo, int64_t so,
@@ -178,7 +184,8 @@ int srnn_adam_clip(float* p, float* g, float* m, float* v, void* p_bf16, int64_t
                    double eps, int64_t step, void* stream);
 /* The same for `ntensors` parameters in one launch (per 64 tensors): host arrays of device
  * pointers and element counts; p_bf16 may be NULL (no copies) or hold NULL entries; a NULL
- * entry of g is an all-zero gradient (a parameter the step's backward did not reach).    */
+ * entry of g is an all-zero gradient (a parameter the step's backward did not reach).
+ * Skipped entirely (on the device) while the persistent-sweep failure flag is up.        */
 int srnn_adam_clip_multi(int ntensors, float* const* p, float* const* g, float* const* m,
                          float* const* v, void* const* p_bf16, const int64_t* n, float clip_lo,
                          float clip_hi, double lr, double beta1, double beta2, double eps,

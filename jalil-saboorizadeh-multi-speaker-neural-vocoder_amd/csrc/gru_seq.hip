@@ -24,7 +24,7 @@ constexpr int NSTAGE = MAXK / R::KB;
 constexpr int WIMG = BN * R::KSB * NSTAGE;         // 96 KiB resident W_hh slice
 constexpr int HIMG = BM * R::KSB * NSTAGE;         // 64 KiB h rows of one step
 constexpr int LDS = WIMG + HIMG;                   // 160 KiB
-constexpr long long SPIN_LIMIT = 1ll << 24;        // ~ seconds of polling
+constexpr long long SPIN_LIMIT = 1ll << 24;        // ~ seconds of polling (fits an int)
 }  // namespace gseq
 
 struct GruSeqArgs {
@@ -35,6 +35,9 @@ struct GruSeqArgs {
     float* gates; int64_t ldg; int64_t sg;                   // (4D per row and step)
     int* cnt;                          // step flags [row tile][64 unit tiles], zeroed
     int* err;
+    int* sticky;                       // persist.hip flag, raised by a workgroup that gives up
+    long long spin_limit;
+    int withhold;                      // test switch: workgroup (0, 0) never publishes
     int B, D, Fr;
     int diag;          // timing diagnostics only (SRNN_GSEQ_DIAG): 1 no wait, 2 no h load,
                        // 4 no epilogue
@@ -44,7 +47,7 @@ struct GruSeqArgs {
 // device-scope load per poll (lane i reads flag i), a ballot decides.  Flags are plain
 // write-through stores of the step count -- no atomics serialising on one address.
 __device__ __forceinline__ bool gseq_wait_flags(const int* flags, int n, int target, int* err,
-                                                int lane) {
+                                                int* sticky, long long limit, int lane) {
     long long spins = 0;
     for (;;) {
         const int v = lane < n ? __hip_atomic_load(flags + lane, __ATOMIC_RELAXED,
@@ -52,13 +55,18 @@ __device__ __forceinline__ bool gseq_wait_flags(const int* flags, int n, int tar
                                : target;
         if (__builtin_amdgcn_ballot_w64(v < target) == 0) return true;
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > gseq::SPIN_LIMIT) {
-            if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (++spins > limit) {
+            if (lane == 0) {
+                __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             return false;
         }
         if ((spins & 63) == 0 &&
-            __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            if (lane == 0) __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return false;
+        }
     }
 }
 
@@ -128,7 +136,9 @@ __global__ __launch_bounds__(256, 1) void gru_seq_fwd_kernel(GruSeqArgs a) {
         if (t > 0 && !(a.diag & 1)) {
             // every wave polls for itself (all 160 KiB of LDS hold operands, no room for a
             // broadcast word); the counter is monotonic, so all waves reach the same verdict
-            if (!gseq_wait_flags(a.cnt + blockIdx.y * 64, nunits, t, a.err, lane)) return;
+            if (!gseq_wait_flags(a.cnt + blockIdx.y * 64, nunits, t, a.err, a.sticky, a.spin_limit,
+                                 lane))
+                return;
         }
         // h_{t-1} rows of this row tile (bf16)
         const bf16* hsrc = t == 0 ? a.h0_lp : a.out_lp + (int64_t)(t - 1) * a.so;
@@ -185,7 +195,7 @@ __global__ __launch_bounds__(256, 1) void gru_seq_fwd_kernel(GruSeqArgs a) {
         // write-back fence: the handed-off bytes are already coherent)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0)
+        if (tid == 0 && !(a.withhold && blockIdx.x == 0 && blockIdx.y == 0))
             __hip_atomic_store(a.cnt + blockIdx.y * 64 + blockIdx.x, t + 1, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         // outputs nobody inside this launch reads: fire and forget
@@ -227,6 +237,9 @@ struct GruSeqBwdArgs {
     float* dgh; bf16* dgh_lp; float* dgi; int64_t ldd; int64_t sd;   // (3D per row/step)
     float* ddir0;                                        // (B, D): dh_direct of step 0
     int* flags; int* err;
+    int* sticky;
+    long long spin_limit;
+    int withhold;
     int B, D, Fr;
 };
 
@@ -267,7 +280,8 @@ __global__ __launch_bounds__(256, 1) void gru_seq_bwd_kernel(GruSeqBwdArgs a) {
         floatx4 acc[1][1];
         acc[0][0] = floatx4{0.f, 0.f, 0.f, 0.f};
         if (has_next) {
-            if (!gseq_wait_flags(a.flags + blockIdx.y * 64, nunits, a.Fr - 1 - t, a.err, lane))
+            if (!gseq_wait_flags(a.flags + blockIdx.y * 64, nunits, a.Fr - 1 - t, a.err, a.sticky,
+                                 a.spin_limit, lane))
                 return;
             const bf16* src = a.dgh_lp + (int64_t)(t + 1) * a.sd;
             auto issue = [&](int kt) {
@@ -332,7 +346,7 @@ __global__ __launch_bounds__(256, 1) void gru_seq_bwd_kernel(GruSeqBwdArgs a) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (tid == 0)
+        if (tid == 0 && !(a.withhold && blockIdx.x == 0 && blockIdx.y == 0))
             __hip_atomic_store(a.flags + blockIdx.y * 64 + blockIdx.x, a.Fr - t, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         if (epi) {
@@ -394,6 +408,10 @@ extern "C" int srnn_gru_seq_bwd(int dtype, int B, int D, int Fr, const float* dy
     a.dgh = dgh; a.dgh_lp = (bf16*)dgh_lp; a.dgi = dgi; a.ldd = ldd; a.sd = sd;
     a.ddir0 = ddir0;
     a.flags = work; a.err = work + (size_t)nm * 64;
+    a.sticky = srnn_sticky_flag();
+    SRNN_REQUIRE(a.sticky, "gru_seq: sticky flag allocation failed");
+    a.spin_limit = srnn_persist_spin_limit((int)gseq::SPIN_LIMIT);
+    a.withhold = env_flag("SRNN_PERSIST_FORCE_FAIL", 0);
     a.B = B; a.D = D; a.Fr = Fr;
     hipLaunchKernelGGL(gru_seq_bwd_kernel, dim3(D / 16, nm), dim3(256), gseqb::LDS, s, a);
     SRNN_LAUNCH_CHECK();
@@ -426,6 +444,10 @@ extern "C" int srnn_gru_seq_fwd(int dtype, int B, int D, int Fr, const float* gi
     a.out = out; a.out_lp = (bf16*)out_lp; a.ldo = ldo; a.so = so;
     a.gates = gates; a.ldg = ldg; a.sg = sg;
     a.cnt = work; a.err = work + (size_t)nm * 64;
+    a.sticky = srnn_sticky_flag();
+    SRNN_REQUIRE(a.sticky, "gru_seq: sticky flag allocation failed");
+    a.spin_limit = srnn_persist_spin_limit((int)gseq::SPIN_LIMIT);
+    a.withhold = env_flag("SRNN_PERSIST_FORCE_FAIL", 0);
     a.B = B; a.D = D; a.Fr = Fr;
     {
         const char* e = getenv("SRNN_GSEQ_DIAG");

@@ -28,13 +28,13 @@ constexpr int NT = 6;                  // n tiles: 3 gates x 2 x 16 units
 constexpr int UK = 32;                 // k per bf16 MFMA unit
 }  // namespace gx
 
-// Sticky failure flag of the persistent sweeps: the per-call error word lives in a work
-// buffer the next call re-zeroes, so every workgroup folds it in here on exit and the host
-// reads it at its own sync points (srnn_persistent_error_take).
-__device__ int gx_sticky_err;
-__device__ __forceinline__ void gx_note_failure(const int* err) {
+// Failure reporting: the per-call error word lives in a work buffer the next call re-zeroes,
+// so every workgroup folds it into the per-device sticky flag (persist.hip) on exit; the
+// fused Adam skips its update while that flag is up and the host reads it at its own sync
+// points (srnn_persistent_error_take).
+__device__ __forceinline__ void gx_note_failure(const int* err, int* sticky) {
     if (threadIdx.x == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        __hip_atomic_store(&gx_sticky_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 struct GruXArgs {
@@ -46,6 +46,9 @@ struct GruXArgs {
     u64* xh;                                        // 2 x G x RG x D/2 granules
     int* census;                                    // 9 zeroed words, or null (static map)
     int* err;
+    int* sticky;                                    // persist.hip flag
+    int spin_limit;
+    int withhold;                                   // test switch: workgroup 0 never publishes
     int B, D, Fr, G, P;
     int poll_sleep;                                 // s_sleep 1 repeats between polls
     unsigned long long* diag;                       // optional phase timestamps (timing only)
@@ -110,7 +113,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     auto publish = [&](int s, float h) {        // h_s -> buffer (s + 1) & 1, tag s + 2
         const uint32_t mine = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(h));
         const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
-        if ((uu & 1) == 0)
+        if ((uu & 1) == 0 && !(a.withhold && blockIdx.x == 0))
             hx_put(a.xh + ((s + 1) & 1) * bufw + (size_t)(g * RG + r) * DG + unit / 2,
                    (uint32_t)(s + 2), mine | (nb << 16), local);
     };
@@ -151,7 +154,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
                                  (x[j][1].w == tag));
                 }
                 if (__all(ok)) break;
-                if (hx_spin_fail(spins, a.err, lane, a.poll_sleep)) break;
+                if (hx_spin_fail(spins, a.err, lane, a.poll_sleep, a.spin_limit)) break;
             }
             GX_STAMP();
 #pragma unroll
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
         GX_STAMP();
     }
 #undef GX_STAMP
-    gx_note_failure(a.err);
+    gx_note_failure(a.err, a.sticky);
 }
 
 // ------------------------------------------------------------------ backward
@@ -227,6 +230,9 @@ struct GruXBwdArgs {
     u64* xg;                                        // 2 x G x RG x 3D/2 granules
     int* census;
     int* err;
+    int* sticky;
+    int spin_limit;
+    int withhold;
     int B, D, Fr, G, P;
 };
 
@@ -318,7 +324,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
                               ((x[j][0].y == tag) & (x[j][0].w == tag) & (x[j][1].y == tag) &
                                (x[j][1].w == tag));
                     if (__all(ok)) break;
-                    if (hx_spin_fail(spins, a.err, lane)) break;
+                    if (hx_spin_fail(spins, a.err, lane, 1, a.spin_limit)) break;
                 }
 #pragma unroll
                 for (int j = 0; j < UPW; ++j) {
@@ -356,7 +362,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
             for (int gt = 0; gt < 3; ++gt) {
                 const uint32_t mine = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(vals[gt]));
                 const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
-                if ((uu & 1) == 0)
+                if ((uu & 1) == 0 && !(a.withhold && blockIdx.x == 0))
                     hx_put(dst + (gt * D + unit) / 2, (uint32_t)(a.Fr - t), mine | (nb << 16), local);
             }
         }
@@ -375,7 +381,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
         }
         __syncthreads();
     }
-    gx_note_failure(a.err);
+    gx_note_failure(a.err, a.sticky);
 }
 
 // ------------------------------------------------------------------ host side
@@ -436,6 +442,10 @@ extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi
     a.out = out; a.out_lp = (bf16*)out_lp; a.ldo = ldo; a.so = so;
     a.gates = gates; a.ldg = ldg; a.sg = sg;
     a.err = (int*)work;
+    a.sticky = srnn_sticky_flag();
+    SRNN_REQUIRE(a.sticky, "gru_xcd: sticky flag allocation failed");
+    a.spin_limit = srnn_persist_spin_limit(hx::SPIN_LIMIT);
+    a.withhold = env_flag("SRNN_PERSIST_FORCE_FAIL", 0);
     a.census = env_flag("SRNN_GEN_LOCAL", 1) ? (int*)work + 16 : nullptr;
     a.xh = (u64*)((char*)work + 256);
     a.B = B; a.D = D; a.Fr = Fr;
@@ -500,6 +510,10 @@ extern "C" int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy
     a.dgh = dgh; a.dgh_lp = (bf16*)dgh_lp; a.dgi = dgi; a.ldd = ldd; a.sd = sd;
     a.ddir0 = ddir0;
     a.err = (int*)work;
+    a.sticky = srnn_sticky_flag();
+    SRNN_REQUIRE(a.sticky, "gru_xcd_bwd: sticky flag allocation failed");
+    a.spin_limit = srnn_persist_spin_limit(hx::SPIN_LIMIT);
+    a.withhold = env_flag("SRNN_PERSIST_FORCE_FAIL", 0);
     a.census = env_flag("SRNN_GEN_LOCAL", 1) ? (int*)work + 16 : nullptr;
     a.xg = (u64*)((char*)work + 256);
     a.B = B; a.D = D; a.Fr = Fr;
@@ -514,17 +528,6 @@ extern "C" int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy
     hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;
-}
-
-// nonzero if any persistent GRU sweep since the last call gave up a hand-off (its results
-// are invalid); clears the flag.  Synchronises the device.
-extern "C" int srnn_persistent_error_take(void) {
-    int v = 0, z = 0;
-    if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpyFromSymbol(&v, HIP_SYMBOL(gx_sticky_err), sizeof(int)) != hipSuccess)
-        return -1;
-    if (v && hipMemcpyToSymbol(HIP_SYMBOL(gx_sticky_err), &z, sizeof(int)) != hipSuccess) return -1;
-    return v;
 }
 
 // nonzero if the previous srnn_gru_xcd_fwd/bwd on `work` gave up a hand-off (synchronises)

@@ -36,9 +36,10 @@ __device__ __forceinline__ uint4 hx_get2(__amdgpu_buffer_rsrc_t r, uint32_t byte
 
 // One poll of a bounded spin: sleeps, and returns true (give up) once the spin limit is hit
 // (raising the error word) or another workgroup raised it.
-__device__ __forceinline__ bool hx_spin_fail(int& spins, int* err, int lane, int sleep = 1) {
+__device__ __forceinline__ bool hx_spin_fail(int& spins, int* err, int lane, int sleep = 1,
+                                             int limit = hx::SPIN_LIMIT) {
     for (int i = 0; i < sleep; ++i) __builtin_amdgcn_s_sleep(1);
-    if (++spins > hx::SPIN_LIMIT) {
+    if (++spins > limit) {
         if (lane == 0) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return true;
     }

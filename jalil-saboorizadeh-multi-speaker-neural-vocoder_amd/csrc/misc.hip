@@ -630,8 +630,13 @@ struct AdamMulti {
 __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float lo, float hi,
                                                               float w1, float b2, float omb2,
                                                               float step_size, float bc2s,
-                                                              float eps) {
+                                                              float eps, const int* skip) {
     constexpr int CH = 2048;
+    // a persistent sweep of this step gave up a hand-off (persist.hip): its gradients are
+    // invalid, so neither the weights nor the Adam moments move (the host raises after)
+    if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(skip, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)))
+        return;
     // workgroups never straddle tensors, so the tensor index is uniform and its pointers
     // come from the argument block with scalar loads
     int t = 0;
@@ -678,12 +683,17 @@ extern "C" int srnn_adam_clip_multi(int ntensors, float* const* p, float* const*
     const double bc2 = 1.0 - pow(beta2, (double)step);
     const float step_size = (float)(lr / bc1);
     const float bc2s = (float)sqrt(bc2);
-    for (int t0 = 0; t0 < ntensors; t0 += ADAM_MT) {
+    const int* skip = srnn_sticky_flag();
+    SRNN_REQUIRE(skip, "adam_multi: sticky flag allocation failed");
+    // chunks of up to ADAM_MT non-empty tensors; the next chunk starts where this one's scan
+    // stopped (empty tensors are skipped, so that is not t0 + ADAM_MT)
+    for (int t0 = 0; t0 < ntensors;) {
         AdamMulti a;
         a.nt = 0;
         a.off[0] = 0;
         a.boff[0] = 0;
-        for (int t = t0; t < ntensors && a.nt < ADAM_MT; ++t) {
+        int t = t0;
+        for (; t < ntensors && a.nt < ADAM_MT; ++t) {
             if (n[t] <= 0) continue;
             const int k = a.nt++;
             a.p[k] = p[t]; a.g[k] = g[t]; a.m[k] = m[t]; a.v[k] = v[t];
@@ -691,11 +701,12 @@ extern "C" int srnn_adam_clip_multi(int ntensors, float* const* p, float* const*
             a.off[k + 1] = a.off[k] + n[t];
             a.boff[k + 1] = a.boff[k] + (int)((n[t] + 2047) / 2048);
         }
+        t0 = t;
         if (a.nt == 0) continue;
         const int64_t nblk = a.boff[a.nt];
         hipLaunchKernelGGL(adam_clip_multi_kernel, dim3((unsigned)nblk), dim3(256), 0,
                            (hipStream_t)stream, a, clip_lo, clip_hi, (float)(1.0 - beta1),
-                           (float)beta2, (float)(1.0 - beta2), step_size, bc2s, (float)eps);
+                           (float)beta2, (float)(1.0 - beta2), step_size, bc2s, (float)eps, skip);
         SRNN_LAUNCH_CHECK();
     }
     return 0;

@@ -23,3 +23,9 @@ static inline int env_flag(const char* name, int dflt) {
     const char* e = getenv(name);
     return (e && *e) ? atoi(e) : dflt;
 }
+
+// persist.hip: the per-device sticky failure flag of the persistent sweeps (device pointer,
+// allocated zeroed on first use; null on a HIP error) and their spin limit (short when the
+// SRNN_PERSIST_FORCE_FAIL test switch is set)
+int* srnn_sticky_flag();
+int srnn_persist_spin_limit(int dflt);

@@ -10,7 +10,10 @@ for the TBPTT step:
     (torch.distributed 'nccl' = RCCL on ROCm) AFTER backward and BEFORE the [-1, 1]
     clamp, so the clamp sees the full-batch gradient exactly as the reference's
     single-process step does (optim.py:11-13);
-  * the loss is a mean over equal shards, so the mean of rank losses is the global loss.
+  * the loss is a mean over equal shards, so the mean of rank losses is the global loss;
+  * a persistent GRU sweep that gave up a hand-off raises a device flag (persist.hip); the
+    flag rides in the last gradient bucket, so every rank's fused clip+Adam skips the step
+    and every rank's Trainer raises, together (no rank is left waiting in a collective).
 
 Generation needs no collective: utterances are independent (replicas only).
 """
@@ -98,6 +101,8 @@ class GradAllReduce:
     reductions run under the rest of the backward; __call__ then only waits.  Groups whose
     grads never arrive this step (h0 on non-reset chunks) are reduced at the sync point.
     The reduced values are identical to the non-overlapped path (same buckets, same sums).
+    A persistent GRU sweep enqueued while reductions are in flight first makes the stream
+    wait for them (_fence): RCCL kernels and a sweep never share the CUs.
     """
 
     def __init__(self, bucket_mb=64, group=None, overlap_groups=None):
@@ -107,6 +112,8 @@ class GradAllReduce:
         self._groups = None
         self._hooks = []
         self._pending = {}
+        self._fenced = set()
+        self._flag_buf = None
         if overlap_groups is not None and dist.is_available() and dist.is_initialized() and \
                 dist.get_world_size(group) > 1:
             self._install(overlap_groups)
@@ -125,8 +132,8 @@ class GradAllReduce:
             buckets.append(cur)
         return buckets
 
-    def _flat(self, key, bucket):
-        total = sum(p.numel() for p in bucket)
+    def _flat(self, key, bucket, extra=0):
+        total = sum(p.numel() for p in bucket) + extra
         k = (key, total, bucket[0].dtype, bucket[0].device)
         flat = self._bufs.get(k)
         if flat is None:
@@ -134,8 +141,11 @@ class GradAllReduce:
             self._bufs[k] = flat
         return flat
 
-    def _launch(self, key, bucket, async_op):
-        flat = self._flat(key, bucket)
+    def _launch(self, key, bucket, async_op, flag=False):
+        """Pack a bucket and start its SUM all-reduce.  flag: the bucket carries one extra
+        element, this rank's persistent-sweep failure flag (0 / 1, persist.hip), so after the
+        reduction every rank holds the same verdict."""
+        flat = self._flat((key, flag), bucket, 1 if flag else 0)
         off = 0
         for p in bucket:
             k = p.numel()
@@ -144,6 +154,8 @@ class GradAllReduce:
             else:
                 flat[off:off + k].copy_(p.grad.reshape(-1))
             off += k
+        if flag:
+            _flag_to(flat[off:])
         work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
         return flat, work
 
@@ -156,9 +168,13 @@ class GradAllReduce:
                 p.grad = torch.zeros_like(p)
             p.grad.copy_(flat[off:off + k].view_as(p.grad))
             off += k
+        if flat.numel() > off:          # the carried failure flag: any rank's -> this rank's
+            _flag_from(flat[off:])
 
     # ---- overlapped mode
     def _install(self, groups):
+        import samplernn_hip as H
+        H.BEFORE_PERSISTENT.append(self._fence)
         self._groups = []
         for gi, params in enumerate(groups):
             for bi, bucket in enumerate(self._split(params)):
@@ -172,6 +188,15 @@ class GradAllReduce:
             for p in bucket:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
 
+    def _fence(self):
+        """Before a persistent GRU sweep: the current stream waits for every all-reduce in
+        flight (a stream-level wait under RCCL, no host synchronisation), so the sweep never
+        shares the CUs with RCCL kernels (samplernn_hip.BEFORE_PERSISTENT)."""
+        for idx, (flat, work) in self._pending.items():
+            if idx not in self._fenced:
+                work.wait()
+                self._fenced.add(idx)
+
     def _on_grad(self, p):
         idx = self._owner[id(p)]
         self._ready[idx] += 1
@@ -184,25 +209,86 @@ class GradAllReduce:
             return
         n = dist.get_world_size(self.group)
         if self._groups is not None:
-            for idx, (key, bucket) in enumerate(self._groups):
-                if idx not in self._pending:          # grads that never arrived this step
-                    self._pending[idx] = self._launch(key, bucket, True)
+            # every backward kernel is enqueued by now, so the failure flag read here covers
+            # all persistent sweeps of the step: it rides in the last bucket launched here, or
+            # alone when the hooks already launched every bucket (reset chunks)
+            late = [idx for idx in range(len(self._groups)) if idx not in self._pending]
+            dev = self._groups[0][1][0].is_cuda
+            for idx in late:                          # grads that never arrived this step
+                key, bucket = self._groups[idx]
+                self._pending[idx] = self._launch(key, bucket, True,
+                                                  flag=dev and idx == late[-1])
+            solo = None
+            if dev and not late:
+                if self._flag_buf is None:
+                    self._flag_buf = torch.zeros(1, device=self._groups[0][1][0].device)
+                _flag_to(self._flag_buf)
+                solo = dist.all_reduce(self._flag_buf, op=dist.ReduceOp.SUM, group=self.group,
+                                       async_op=True)
             for idx, (key, bucket) in enumerate(self._groups):
                 flat, work = self._pending[idx]
                 work.wait()
                 self._unpack(bucket, flat, n)
+            if solo is not None:
+                solo.wait()
+                _flag_from(self._flag_buf)
             self._pending = {}
+            self._fenced = set()
             self._ready = [0] * len(self._groups)
             return
         params = [p for g in optimizer.param_groups for p in g['params'] if p.requires_grad]
-        for bi, bucket in enumerate(self._split(params)):
-            flat, _ = self._launch(bi, bucket, False)
+        buckets = self._split(params)
+        for bi, bucket in enumerate(buckets):
+            flat, _ = self._launch(bi, bucket, False,
+                                   flag=bucket[0].is_cuda and bi == len(buckets) - 1)
             self._unpack(bucket, flat, n)
+
+
+def _flag_to(dst):
+    """dst (1-element fp32 device tensor) = this rank's persistent-sweep failure flag."""
+    import samplernn_hip as H
+    H.lib().call('srnn_persistent_flag_to_f32', H.ptr(dst), H.stream())
+
+
+def _flag_from(src):
+    """Raise this rank's failure flag if the reduced value says any rank failed: the fused
+    clip+Adam then skips the update on every rank and every rank's Trainer raises."""
+    import samplernn_hip as H
+    H.lib().call('srnn_persistent_flag_or_f32', H.ptr(src), H.stream())
 
 
 def barrier():
     if dist.is_available() and dist.is_initialized():
         dist.barrier()
+
+
+def _active():
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
+def _coll_device():
+    """Where a small host-value collective runs: the rank's GPU under nccl (RCCL reduces
+    device tensors only), the CPU under gloo."""
+    if dist.get_backend() == 'nccl':
+        return torch.device('cuda', torch.cuda.current_device())
+    return torch.device('cpu')
+
+
+def sum_over_ranks(values):
+    """Element-wise sum of a list of python floats over ranks (identity for one process)."""
+    if not _active():
+        return [float(v) for v in values]
+    t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=_coll_device())
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return [float(v) for v in t.tolist()]
+
+
+def mean_over_ranks(x):
+    """Mean of a python float over ranks: the global loss of a row-sharded step (every rank
+    holds an equal shard, so the mean of shard means is the full-batch mean)."""
+    if not _active():
+        return float(x)
+    return sum_over_ranks([x])[0] / dist.get_world_size()
 
 
 def max_over_ranks(x, device=None):

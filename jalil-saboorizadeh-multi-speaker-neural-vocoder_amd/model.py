@@ -254,6 +254,8 @@ class _TierFn(torch.autograd.Function):
             hpT = H.cast(hpf, T)
             xw = H.gru_xcd_work_bytes(T, B, D) if lp else 0
             seq = lp and (xw > 0 or H.gru_seq_supported(T, B, D))
+            if seq:
+                H.before_persistent_sweep()
             if xw > 0:
                 # whole sequence in one persistent launch, row groups per XCD, W_hh in VGPRs
                 work = torch.empty(xw, device=dev, dtype=torch.uint8)
@@ -343,6 +345,8 @@ class _TierFn(torch.autograd.Function):
             WhhT = H.permute3(Whh[l].float().reshape(1, 3 * D, D), (0, 2, 1), dtype=T)
             xbw = H.gru_xcd_bwd_work_bytes(T, B, D) if lp else 0
             seq = lp and (xbw > 0 or H.gru_seq_supported(T, B, D))
+            if seq:
+                H.before_persistent_sweep()   # (DP: in-flight all-reduces finish first)
             if xbw > 0:
                 # reverse sweep in one persistent launch, row groups per XCD, W_hh^T in VGPRs
                 work = torch.empty(xbw, device=dev, dtype=torch.uint8)

@@ -68,6 +68,8 @@ _SIGS = {
                          _L, _L, _P, _P, _SZ, _P],
     'srnn_gen_workspace_size': [_P, _I, ctypes.POINTER(_SZ)],
     'srnn_generate': [_P, _I, _I, _P, _P, _P, _U64, _P, _P, _P, _SZ, _I, _P],
+    'srnn_persistent_flag_to_f32': [_P, _P],
+    'srnn_persistent_flag_or_f32': [_P, _P],
 }
 
 
@@ -147,9 +149,23 @@ def exported_symbols():
                             'srnn_persistent_error_take']
 
 
+# Callbacks run just before a persistent sweep (gru_xcd / gru_seq) is enqueued.  Such a sweep
+# needs every workgroup co-resident (one per CU, up to the whole register file), so it must
+# not share the GPU with RCCL kernels: partially resident, a sweep and an all-reduce could
+# wait on each other across ranks.  distributed.GradAllReduce registers a callback that makes
+# the current stream wait for every gradient all-reduce already in flight.
+BEFORE_PERSISTENT = []
+
+
+def before_persistent_sweep():
+    for f in BEFORE_PERSISTENT:
+        f()
+
+
 def check_persistent_errors():
     """Raise if a persistent GRU sweep gave up a hand-off since the last check (its outputs
-    are invalid).  Synchronises the device; the Trainer calls it once per iteration."""
+    are invalid; the fused clip+Adam already skipped that step's update on the device).
+    Synchronises the device; the Trainer calls it once per iteration."""
     fn = lib().dll.srnn_persistent_error_take
     fn.restype = ctypes.c_int
     fn.argtypes = []

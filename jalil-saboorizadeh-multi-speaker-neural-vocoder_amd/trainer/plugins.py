@@ -162,14 +162,20 @@ class Logger(Plugin):
 
 # ---------------------------------------------------------------- reference plugins
 class TrainingLossMonitor(LossMonitor):
-    """plugins.py:22-24."""
+    """plugins.py:22-24.  Under row-sharded data parallelism (distributed.py) the logged value
+    is the mean of the ranks' shard losses = the full-batch loss the single-process run logs."""
 
     stat_name = 'training_loss'
+
+    def _get_value(self, iteration, input, target, output, loss):
+        import distributed
+        return distributed.mean_over_ranks(super()._get_value(iteration, input, target, output,
+                                                              loss))
 
 
 class ValidationPlugin(Plugin):
     """plugins.py:27-96: teacher-forced loss over the validation and test loaders each
-    epoch (model in eval mode, no autograd graph)."""
+    epoch (model in eval mode, no autograd graph); row shards summed over ranks under DP."""
 
     def __init__(self, val_dataset, test_dataset, writer):
         super().__init__([(1, 'epoch')])
@@ -205,6 +211,10 @@ class ValidationPlugin(Plugin):
                 bs = target.size(0)
                 loss_sum += loss.item() * bs
                 n_examples += bs
+        # under data parallelism each rank saw its row shard: sum (loss, rows) over ranks so
+        # every rank -- and SaverPlugin's best-checkpoint choice -- sees the full-batch value
+        import distributed
+        loss_sum, n_examples = distributed.sum_over_ranks([loss_sum, n_examples])
         return loss_sum / n_examples if n_examples else float('nan')
 
 

@@ -32,12 +32,17 @@ class _Toy(torch.nn.Module):
         self.h0 = torch.nn.Parameter(torch.zeros(5))
 
     def forward(self, x, h):
+        import samplernn_hip as H
         B, T, _ = x.shape
         if h is None:
             h = self.h0.expand(B, 5)
         out = []
         for t in range(T):
             h = torch.tanh(x[:, t] @ self.W.t() + h @ self.U.t())
+            if t == T // 2:
+                # stands in for a persistent GRU sweep inside the backward: the fence makes
+                # it wait for every all-reduce already in flight (results must not change)
+                h.register_hook(lambda g: (H.before_persistent_sweep(), g)[1])
             out.append(h)
         return torch.stack(out, 1), h.detach()
 
@@ -112,3 +117,59 @@ def test_shard_rows():
     assert D.shard_rows(512, 3, 8) == slice(192, 256)
     with pytest.raises(ValueError):
         D.shard_rows(10, 0, 3)
+
+
+class _FakeTrainer:
+    cuda = False
+
+    def __init__(self, shift):
+        self.shift = shift
+        self.stats = {}
+
+    def model(self, inputs, reset, cond, spk, writer, idx):
+        return inputs.float() + self.shift
+
+    @staticmethod
+    def criterion(out, target):
+        return (out - target.float()).abs().mean()
+
+
+def _plugin_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import distributed as D
+    from trainer.plugins import TrainingLossMonitor, ValidationPlugin
+    D.init(backend='gloo')
+    # rank r sees rows r*2 .. r*2+1 of a 4-row batch; per-rank losses differ
+    full = torch.arange(4 * 3, dtype=torch.float32).reshape(4, 3)
+    rows = D.shard_rows(4)
+    batch = [(full[rows], torch.ones(1), torch.zeros(2, 3), torch.zeros(2, 1), torch.zeros(2, 1))]
+    tr = _FakeTrainer(shift=0.0)
+    vp = ValidationPlugin(batch, batch, None)
+    vp.register(tr)
+    val = vp._evaluate(batch, 0)
+    mon = TrainingLossMonitor()
+    mon.register(tr)
+    local = float(full[rows].mean())
+    mon.iteration(1, None, None, None, torch.tensor(local))
+    q.put((rank, val, tr.stats['training_loss']['last']))
+    dist.destroy_process_group()
+
+
+def test_dp_plugins_report_full_batch_losses():
+    """Under DP the validation loss and the logged training loss are the full-batch values,
+    not rank 0's shard (ValidationPlugin sums (loss, rows), TrainingLossMonitor averages)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plugin_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    full = torch.arange(12, dtype=torch.float32).reshape(4, 3).mean().item()
+    for _, val, tl in got:
+        assert abs(val - full) < 1e-9
+        assert abs(tl - full) < 1e-6

@@ -593,6 +593,32 @@ def test_adam_clip_multi_matches_torch(hip):
         torch.testing.assert_close(p.cpu(), r.detach(), atol=1e-7, rtol=1e-6)
 
 
+def test_adam_clip_multi_empty_tensors_across_chunks(hip):
+    """> 64 tensors with empty ones among them: each chunk of 64 non-empty tensors starts
+    where the previous chunk's scan stopped, so no tensor is updated twice or skipped."""
+    import ctypes
+    sizes = []
+    for i in range(150):
+        sizes.append(0 if i % 7 == 3 else 1 + (i * 37) % 3000)
+    ps = [_rand(max(n, 1), seed=i)[:n].contiguous().to(DEV) for i, n in enumerate(sizes)]
+    ms = [torch.zeros(n, device=DEV) for n in sizes]
+    vs = [torch.zeros(n, device=DEV) for n in sizes]
+    refs = [p.detach().cpu().clone().requires_grad_(True) for p in ps]
+    opt = torch.optim.Adam([r for r in refs if r.numel()], lr=1e-3)
+    gs = [_rand(max(n, 1), scale=3.0, seed=500 + i)[:n].contiguous() for i, n in enumerate(sizes)]
+    gd = [g.to(DEV) for g in gs]
+    arr = lambda ts: (ctypes.c_void_p * len(ts))(*[t.data_ptr() if t.numel() else None  # noqa
+                                                   for t in ts])
+    hip.lib().call('srnn_adam_clip_multi', len(sizes), arr(ps), arr(gd), arr(ms), arr(vs), None,
+                   (ctypes.c_int64 * len(sizes))(*sizes), -1.0, 1.0, 1e-3, 0.9, 0.999, 1e-8, 1,
+                   hip.stream())
+    for r, g in zip(refs, gs):
+        r.grad = g.clamp(-1, 1)
+    opt.step()
+    for p, r in zip(ps, refs):
+        torch.testing.assert_close(p.cpu(), r.detach(), atol=1e-7, rtol=1e-6)
+
+
 def test_adam_clip_matches_torch(hip):
     n = 10007
     p0 = _rand(n, seed=1)
