@@ -93,6 +93,15 @@ int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy, int64_t l
                      int64_t so, const float* h0, const void* whh_t, float* dgh, void* dgh_lp,
                      float* dgi, int64_t ldd, int64_t sd, float* ddir0, void* work,
                      size_t work_bytes, void* stream);
+/* Same sweep with the bf16 TBPTT step's outputs: dgh / dgi (fp32) may be NULL; dgi_lp (bf16,
+ * dgi's layout, the operand of the dW_ih / dX GEMMs) and bsum ((B, 4D) fp32: per batch row the
+ * sums over t of [dar | daz | dghn | dan], from which b_hh / b_ih gradients are one column sum)
+ * are optional.  Replaces the cast of dgi and the two bias column sums over B x Fr rows. */
+int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* dy, int64_t lddy, int64_t sdy,
+                      const float* gates, int64_t ldg, int64_t sg, const float* hout, int64_t ldo,
+                      int64_t so, const float* h0, const void* whh_t, float* dgh, void* dgh_lp,
+                      float* dgi, void* dgi_lp, float* bsum, int64_t ldd, int64_t sd,
+                      float* ddir0, void* work, size_t work_bytes, void* stream);
 int srnn_gru_xcd_error(const void* work);
 /* Sticky form for callers that do not keep the work buffer: nonzero if ANY persistent GRU
  * sweep (srnn_gru_xcd_fwd/bwd, srnn_gru_seq_fwd/bwd) since the previous call gave up a
@@ -158,6 +167,16 @@ int srnn_weight_norm_fwd(const float* g, const float* v, float* w, float* norm, 
                          int64_t R, void* stream);
 int srnn_weight_norm_bwd(const float* g, const float* v, const float* dw, float* dg, float* dv,
                          int O, int64_t R, int accumulate, void* stream);
+/* The always-on weight norm of LearnedUpsampling1d.conv_t (model.py:177-178) folded into its
+ * GEMM operand: scale[i] = g[i] / ||v[i]||; dst[(j * Cout + o) * Cin + i] = v[i][o][j] * scale[i]
+ * (dst fp32 or bf16; scale NULL = 1: a plain (2, 1, 0) permute); backward from the GEMM's
+ * transposed weight gradient dwt[i][(j * Cout + o)] to dg[i] and dv (v's layout).          */
+int srnn_weight_norm_scale(const float* g, const float* v, float* scale, int O, int64_t R,
+                           void* stream);
+int srnn_convt_fold(const float* v, const float* scale, void* dst, int dst_dtype, int Cin,
+                    int Cout, int k, void* stream);
+int srnn_convt_wn_bwd(const float* g, const float* v, const float* dwt, float* dg, float* dv,
+                      int Cin, int Cout, int k, void* stream);
 
 /* ---- layout / elementwise helpers ------------------------------------------------- */
 int srnn_permute3(const float* src, void* dst, int dst_dtype, int d0, int d1, int d2, int p0,

@@ -225,7 +225,10 @@ struct GruXBwdArgs {
     const float* hout; int64_t ldo; int64_t so;
     const float* h0;
     const bf16* whh_t;                              // (D, 3D)
-    float* dgh; bf16* dgh_lp; float* dgi; int64_t ldd; int64_t sd;
+    float* dgh; bf16* dgh_lp; float* dgi; int64_t ldd; int64_t sd;   // dgh / dgi optional
+    bf16* dgi_lp;                                   // optional bf16 dgi (same layout)
+    float* bsum;                                    // optional (B, 4D): per-row sums over t of
+                                                    // [dar | daz | dghn | dan] (bias grads)
     float* ddir0;                                   // (B, D)
     u64* xg;                                        // 2 x G x RG x 3D/2 granules
     int* census;
@@ -296,6 +299,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
                    : a.h0[(int64_t)b * D + unit];
     };
     float dyv, gr, gz, gn, gg, hp;
+    float sar = 0.f, saz = 0.f, sghn = 0.f, san = 0.f;   // bias-gradient row sums (over t)
     fetch(a.Fr - 1, dyv, gr, gz, gn, gg, hp);
     for (int t = a.Fr - 1; t >= 0; --t) {
         const bool has_next = t + 1 < a.Fr;
@@ -370,16 +374,29 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
         if (t > 0) fetch(t - 1, dyv, gr, gz, gn, gg, hp);
         if (wr) {
             const int64_t ob = (int64_t)b * a.ldd + (int64_t)t * a.sd;
-            float* dg = a.dgh + ob;
-            dg[unit] = cdar; dg[D + unit] = cdaz; dg[2 * D + unit] = cdghn;
+            if (a.dgh) {
+                float* dg = a.dgh + ob;
+                dg[unit] = cdar; dg[D + unit] = cdaz; dg[2 * D + unit] = cdghn;
+            }
             bf16* dl = a.dgh_lp + ob;
-            dl[unit] = __float2bfloat16(cdar); dl[D + unit] = __float2bfloat16(cdaz);
-            dl[2 * D + unit] = __float2bfloat16(cdghn);
-            float* di = a.dgi + ob;
-            di[unit] = cdar; di[D + unit] = cdaz; di[2 * D + unit] = cdan;
+            const bf16 har = __float2bfloat16(cdar), haz = __float2bfloat16(cdaz);
+            dl[unit] = har; dl[D + unit] = haz; dl[2 * D + unit] = __float2bfloat16(cdghn);
+            if (a.dgi) {
+                float* di = a.dgi + ob;
+                di[unit] = cdar; di[D + unit] = cdaz; di[2 * D + unit] = cdan;
+            }
+            if (a.dgi_lp) {
+                bf16* dj = a.dgi_lp + ob;
+                dj[unit] = har; dj[D + unit] = haz; dj[2 * D + unit] = __float2bfloat16(cdan);
+            }
+            sar += cdar; saz += cdaz; sghn += cdghn; san += cdan;
             if (t == 0) a.ddir0[(int64_t)b * D + unit] = ddir;
         }
         __syncthreads();
+    }
+    if (a.bsum && wr) {
+        float* bs = a.bsum + (int64_t)b * 4 * D;
+        bs[unit] = sar; bs[D + unit] = saz; bs[2 * D + unit] = sghn; bs[3 * D + unit] = san;
     }
     gx_note_failure(a.err, a.sticky);
 }
@@ -490,12 +507,12 @@ extern "C" size_t srnn_gru_xcd_bwd_work_bytes(int dtype, int B, int D) {
     return 256 + (size_t)2 * G * gx::RG * (3 * D / 2) * 8;
 }
 
-extern "C" int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy, int64_t lddy,
-                                int64_t sdy, const float* gates, int64_t ldg, int64_t sg,
-                                const float* hout, int64_t ldo, int64_t so, const float* h0,
-                                const void* whh_t, float* dgh, void* dgh_lp, float* dgi,
-                                int64_t ldd, int64_t sd, float* ddir0, void* work,
-                                size_t work_bytes, void* stream) {
+extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* dy, int64_t lddy,
+                                 int64_t sdy, const float* gates, int64_t ldg, int64_t sg,
+                                 const float* hout, int64_t ldo, int64_t so, const float* h0,
+                                 const void* whh_t, float* dgh, void* dgh_lp, float* dgi,
+                                 void* dgi_lp, float* bsum, int64_t ldd, int64_t sd, float* ddir0,
+                                 void* work, size_t work_bytes, void* stream) {
     const size_t need = srnn_gru_xcd_bwd_work_bytes(dtype, B, D);
     SRNN_REQUIRE(need > 0, "gru_xcd_bwd: shape/device not supported");
     SRNN_REQUIRE(work && work_bytes >= need, "gru_xcd_bwd: workspace %zu < %zu", work_bytes, need);
@@ -507,7 +524,9 @@ extern "C" int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy
     a.gates = gates; a.ldg = ldg; a.sg = sg;
     a.hout = hout; a.ldo = ldo; a.so = so; a.h0 = h0;
     a.whh_t = (const bf16*)whh_t;
+    SRNN_REQUIRE(dgh_lp, "gru_xcd_bwd: dgh_lp is required");
     a.dgh = dgh; a.dgh_lp = (bf16*)dgh_lp; a.dgi = dgi; a.ldd = ldd; a.sd = sd;
+    a.dgi_lp = (bf16*)dgi_lp; a.bsum = bsum;
     a.ddir0 = ddir0;
     a.err = (int*)work;
     a.sticky = srnn_sticky_flag();
@@ -528,6 +547,17 @@ extern "C" int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy
     hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int srnn_gru_xcd_bwd(int dtype, int B, int D, int Fr, const float* dy, int64_t lddy,
+                                int64_t sdy, const float* gates, int64_t ldg, int64_t sg,
+                                const float* hout, int64_t ldo, int64_t so, const float* h0,
+                                const void* whh_t, float* dgh, void* dgh_lp, float* dgi,
+                                int64_t ldd, int64_t sd, float* ddir0, void* work,
+                                size_t work_bytes, void* stream) {
+    return srnn_gru_xcd_bwd2(dtype, B, D, Fr, dy, lddy, sdy, gates, ldg, sg, hout, ldo, so, h0,
+                             whh_t, dgh, dgh_lp, dgi, nullptr, nullptr, ldd, sd, ddir0, work,
+                             work_bytes, stream);
 }
 
 // nonzero if the previous srnn_gru_xcd_fwd/bwd on `work` gave up a hand-off (synchronises)

@@ -246,6 +246,155 @@ extern "C" int srnn_weight_norm_bwd(const float* g, const float* v, const float*
     return 0;
 }
 
+// ------------------------------------------------------------------ weight norm of conv_t
+// The always-on weight norm of LearnedUpsampling1d.conv_t (model.py:177-178, nn.py:33-43)
+// feeds ONE consumer: the upsampling GEMM operand W_up[(j * Cout + o)][i] = w[i][o][j].
+// Forward: s[i] = g[i] / ||v[i]|| (srnn_weight_norm_scale, reads v once, writes Cin floats),
+// then srnn_convt_fold writes the scaled, permuted operand straight from v (no fp32 w).
+// Backward: the GEMM produces dW^T[i][(j * Cout + o)] (rows per input channel), and one
+// block per channel computes dg and dv in v's own layout (srnn_convt_wn_bwd): the same
+// per-thread element order and block reduction as wn_bwd_kernel, so the results are the
+// ones weight_norm_bwd would give for the permuted gradient.
+__global__ void wn_scale_kernel(const float* __restrict__ g, const float* __restrict__ v,
+                                float* __restrict__ scale, int64_t R) {
+    __shared__ float sh[16];
+    const int64_t o = blockIdx.x;
+    const float* vr = v + o * R;
+    float s = 0.f;
+    for (int64_t r = threadIdx.x; r < R; r += blockDim.x) s += vr[r] * vr[r];
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) scale[o] = g[o] / sqrtf(s);
+}
+
+extern "C" int srnn_weight_norm_scale(const float* g, const float* v, float* scale, int O,
+                                      int64_t R, void* stream) {
+    if (O <= 0) return 0;
+    hipLaunchKernelGGL(wn_scale_kernel, dim3(O), dim3(256), 0, (hipStream_t)stream, g, v, scale, R);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// dst[(j * Cout + o) * Cin + i] = v[i][o][j] * scale[i]: 64 channels x 64 (o, j) per block
+// (64 / k output channels), 256-B row reads, 128-B (bf16) / 256-B (fp32) row writes
+template <typename TO>
+__global__ __launch_bounds__(256) void convt_fold_kernel(const float* __restrict__ v,
+                                                         const float* __restrict__ scale,
+                                                         TO* __restrict__ dst, int Cin, int Cout,
+                                                         int k) {
+    __shared__ float tile[64][65];
+    const int tid = threadIdx.x;
+    const int i0 = blockIdx.x * 64;
+    const int e0 = blockIdx.y * 64;                // flat (o, j) = o * k + j
+    const int64_t R = (int64_t)Cout * k;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int row = p * 16 + (tid >> 4), c4 = (tid & 15) * 4;
+        const floatx4 x = *reinterpret_cast<const floatx4*>(v + (int64_t)(i0 + row) * R + e0 + c4);
+        const float sc = scale ? scale[i0 + row] : 1.f;
+        tile[row][c4 + 0] = x[0] * sc;
+        tile[row][c4 + 1] = x[1] * sc;
+        tile[row][c4 + 2] = x[2] * sc;
+        tile[row][c4 + 3] = x[3] * sc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        const int e = p * 16 + (tid >> 4), i4 = (tid & 15) * 4;
+        const int ef = e0 + e, o = ef / k, j = ef - o * k;
+        TO* q = dst + ((int64_t)j * Cout + o) * Cin + i0 + i4;
+        float w[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) w[u] = tile[i4 + u][e];
+        if constexpr (sizeof(TO) == 4) {
+            *reinterpret_cast<floatx4*>(q) = floatx4{w[0], w[1], w[2], w[3]};
+        } else {
+            unsigned short h[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) h[u] = __bfloat16_as_ushort(__float2bfloat16(w[u]));
+            *reinterpret_cast<uint2*>(q) = make_uint2(h[0] | ((unsigned)h[1] << 16),
+                                                      h[2] | ((unsigned)h[3] << 16));
+        }
+    }
+}
+
+extern "C" int srnn_convt_fold(const float* v, const float* scale, void* dst, int dst_dtype,
+                               int Cin, int Cout, int k, void* stream) {
+    if ((int64_t)Cin * Cout * k <= 0) return 0;
+    SRNN_REQUIRE(Cin % 64 == 0 && ((int64_t)Cout * k) % 64 == 0 && 64 % k == 0,
+                 "convt_fold: needs Cin %% 64 == 0, 64 %% k == 0 (Cin %d Cout %d k %d)", Cin, Cout, k);
+    SRNN_REQUIRE((uintptr_t)v % 16 == 0, "convt_fold: v must be 16-B aligned");
+    dim3 grid(Cin / 64, (unsigned)(((int64_t)Cout * k) / 64));
+    hipStream_t s = (hipStream_t)stream;
+    if (dst_dtype == SRNN_F32)
+        hipLaunchKernelGGL(convt_fold_kernel<float>, grid, dim3(256), 0, s, v, scale, (float*)dst,
+                           Cin, Cout, k);
+    else
+        hipLaunchKernelGGL(convt_fold_kernel<bf16>, grid, dim3(256), 0, s, v, scale, (bf16*)dst,
+                           Cin, Cout, k);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+// one block per input channel i: dW^T row [j][o] staged in LDS (row pitch Cout + 4 floats:
+// the reads at flat (o, j) order hit distinct banks for k = 16), then wn_bwd_kernel's math
+template <bool HAS_G>
+__global__ __launch_bounds__(256) void convt_wn_bwd_kernel(const float* __restrict__ g,
+                                                           const float* __restrict__ v,
+                                                           const float* __restrict__ dwt,
+                                                           float* __restrict__ dg,
+                                                           float* __restrict__ dv, int Cout,
+                                                           int k) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    float* dl = reinterpret_cast<float*>(smem);           // [k][Cout + 4]
+    __shared__ float sh[16];
+    const int64_t i = blockIdx.x;
+    const int64_t R = (int64_t)Cout * k;
+    const int pitch = Cout + 4;
+    const float* drow = dwt + i * R;
+    for (int64_t e = threadIdx.x * 4; e < R; e += 256 * 4) {
+        const floatx4 x = *reinterpret_cast<const floatx4*>(drow + e);
+        const int j = (int)(e / Cout), o = (int)(e - (int64_t)j * Cout);
+        *reinterpret_cast<floatx4*>(dl + j * pitch + o) = x;
+    }
+    __syncthreads();
+    const float* vr = v + i * R;
+    float s = 0.f, d = 0.f;
+    for (int64_t r = threadIdx.x; r < R; r += 256) {
+        const int o = (int)(r / k), j = (int)(r - (int64_t)o * k);
+        const float vv = vr[r];
+        s += vv * vv;
+        d += dl[j * pitch + o] * vv;
+    }
+    s = block_sum(s, sh);
+    d = block_sum(d, sh);
+    const float n = sqrtf(s);
+    const float dgo = d / n;
+    const float gn = (HAS_G ? g[i] : 1.f) / n;
+    if (threadIdx.x == 0) dg[i] = dgo;
+    for (int64_t r = threadIdx.x; r < R; r += 256) {
+        const int o = (int)(r / k), j = (int)(r - (int64_t)o * k);
+        dv[i * R + r] = gn * (dl[j * pitch + o] - dgo / n * vr[r]);
+    }
+}
+
+extern "C" int srnn_convt_wn_bwd(const float* g, const float* v, const float* dwt, float* dg,
+                                 float* dv, int Cin, int Cout, int k, void* stream) {
+    if ((int64_t)Cin * Cout * k <= 0) return 0;
+    SRNN_REQUIRE(Cout % 4 == 0 && (uintptr_t)dwt % 16 == 0, "convt_wn_bwd: Cout %% 4, 16-B dW^T");
+    const size_t lds = (size_t)k * (Cout + 4) * sizeof(float);
+    SRNN_REQUIRE(lds <= 150 * 1024, "convt_wn_bwd: k * Cout too large for LDS (%d x %d)", k, Cout);
+    static bool attr = false;
+    if (!attr) {
+        SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)convt_wn_bwd_kernel<true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+        attr = true;
+    }
+    hipLaunchKernelGGL(convt_wn_bwd_kernel<true>, dim3(Cin), dim3(256), lds, (hipStream_t)stream, g,
+                       v, dwt, dg, dv, Cout, k);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
 // ------------------------------------------------------------------ layout permutes
 // dst = src.permute(p0, p1, p2) made contiguous, src (d0, d1, d2) row-major fp32; dst
 // fp32 (optionally accumulated) or bf16.  When the innermost axis changes (o = p2 != 2)
@@ -516,10 +665,28 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ src, 
 }
 
 template <typename T>
+__global__ __launch_bounds__(256) void colsum_narrow_kernel(const T* __restrict__ src, int64_t lds,
+                                                            int64_t rows, float* __restrict__ dst,
+                                                            float alpha, int accumulate) {
+    __shared__ float sh[16];
+    const int c = blockIdx.x;
+    float s = 0.f;
+    for (int64_t r = threadIdx.x; r < rows; r += 256) s += to_f(src[r * lds + c]);
+    s = block_sum(s, sh);
+    if (threadIdx.x == 0) dst[c] = accumulate ? dst[c] + alpha * s : alpha * s;
+}
+
+template <typename T>
 static void colsum_pass(const T* src, int64_t lds, int64_t rows, int cols, int64_t rpb, int nrb,
                         float* dst, float alpha, int accumulate, bool final_, hipStream_t s) {
     const bool vec = (lds % 4 == 0) && ((uintptr_t)src % (4 * sizeof(T)) == 0);
     dim3 grid(cdiv(cols, 64), nrb);
+    if (final_ && cols < 16 && nrb == 1) {
+        // few columns (the loss sum): every thread of a block strides the rows of one column
+        hipLaunchKernelGGL((colsum_narrow_kernel<T>), dim3(cols), dim3(256), 0, s, src, lds, rows,
+                           dst, alpha, accumulate);
+        return;
+    }
     if (final_) {
         if (vec) hipLaunchKernelGGL((colsum_kernel<T, true, true>), grid, dim3(256), 0, s, src, lds, rows, cols, rpb, dst, alpha, accumulate);
         else hipLaunchKernelGGL((colsum_kernel<T, false, true>), grid, dim3(256), 0, s, src, lds, rows, cols, rpb, dst, alpha, accumulate);

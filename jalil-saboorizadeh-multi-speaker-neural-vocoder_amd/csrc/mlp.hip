@@ -319,10 +319,35 @@ extern "C" int srnn_nll_fwd(const float* logp, int64_t ldl, const int64_t* targe
     return 0;
 }
 
+// Q = 256: one wave per row, 16-B stores (the dense gradient is 4 B x Q per row)
+__global__ __launch_bounds__(256) void nll_bwd_q256_kernel(const int64_t* __restrict__ target,
+                                                           int64_t ldt, int Tlen, int64_t rows,
+                                                           float* __restrict__ dl, int64_t ldd,
+                                                           float gscale,
+                                                           const float* __restrict__ gmul) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= rows) return;
+    if (gmul) gscale *= *gmul;
+    const int64_t b = r / Tlen, t = r - b * Tlen;
+    const int tq = (int)target[b * ldt + t] - 4 * lane;
+    floatx4 v = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+        if (tq == e) v[e] = -gscale;
+    *reinterpret_cast<floatx4*>(dl + r * ldd + 4 * lane) = v;
+}
+
 extern "C" int srnn_nll_bwd(const int64_t* target, int64_t ldt, int Tlen, int64_t rows, int Q,
                             float* dlogp, int64_t ldd, float gscale, const float* gmul,
                             void* stream) {
     if (rows <= 0) return 0;
+    if (Q == 256 && ldd % 4 == 0 && (uintptr_t)dlogp % 16 == 0) {
+        hipLaunchKernelGGL(nll_bwd_q256_kernel, dim3(cdiv(rows, 4)), dim3(256), 0,
+                           (hipStream_t)stream, target, ldt, Tlen, rows, dlogp, ldd, gscale, gmul);
+        SRNN_LAUNCH_CHECK();
+        return 0;
+    }
     hipLaunchKernelGGL(nll_bwd_kernel, dim3(cdiv(rows * Q, 256)), dim3(256), 0,
                        (hipStream_t)stream, target, ldt, Tlen, rows, Q, dlogp, ldd, gscale, gmul);
     SRNN_LAUNCH_CHECK();

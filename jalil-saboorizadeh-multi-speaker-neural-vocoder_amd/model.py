@@ -288,7 +288,7 @@ class _TierFn(torch.autograd.Function):
         up_p = take_w(mod.upsampling.conv_t)
         up_b = next(it)
         k = mod.frame_size
-        W_up = H.permute3(nn.weight_of(mod.upsampling.conv_t), (2, 1, 0), dtype=T)  # (k, D, D)
+        W_up = nn.convt_operand(mod.upsampling.conv_t, T)                        # (k, D, D)
         b_up = H.permute3(up_b.reshape(1, D, k), (0, 2, 1)).reshape(k * D)
         # the bottom tier feeds the MLP's gather directly: its upsampled output (and so the
         # gradient coming back) is in the compute dtype; upper tiers stay fp32 (Cin input)
@@ -326,35 +326,46 @@ class _TierFn(torch.autograd.Function):
         else:
             dY2 = dY.reshape(M, k * D).float().contiguous()
             dYT = H.cast(dY2, T)
-        dWup = H.gemm(dYT, outsT[-1].reshape(M, D), transA=True)          # (k*D, D)
+        # weight gradient transposed, [i][j*D + o]: one row per input channel for the
+        # per-channel weight-norm backward (no permute of the 16 x D x D gradient)
+        dWupT = H.gemm(outsT[-1].reshape(M, D), dYT, transA=True)         # (D, k*D)
         db_up = H.colsum(dY2, M, k * D)
         dX = H.gemm(dYT, W_up.reshape(k * D, D))                          # (M, D)
-        dW_conv = H.permute3(dWup.reshape(k, D, D), (2, 1, 0))            # (D_in, D_out, k)
-        g_up = nn.weight_grad_to_params(mod.upsampling.conv_t, dW_conv)
+        g_up = nn.convt_grad_to_params(mod.upsampling.conv_t, dWupT)
         g_up_b = H.permute3(db_up.reshape(1, k, D), (0, 2, 1)).reshape(D, k)
         # --- GRU layers, top layer first
         g_rnn = [None] * L
         dh_in = [None] * L
         for l in reversed(range(L)):
             dOut = dX.reshape(B, Fr, D)
-            dGH = torch.empty((B, Fr, 3 * D), device=dev, dtype=torch.float32)
-            dGHT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T) if lp else dGH
-            dGI = torch.empty((B, Fr, 3 * D), device=dev, dtype=torch.float32)
-            ddir = [torch.empty((B, D), device=dev, dtype=torch.float32) for _ in range(2)]
             # W_hh^T (D, 3D): k-contiguous operand for the deep-ring backward kernel
             WhhT = H.permute3(Whh[l].float().reshape(1, 3 * D, D), (0, 2, 1), dtype=T)
             xbw = H.gru_xcd_bwd_work_bytes(T, B, D) if lp else 0
             seq = lp and (xbw > 0 or H.gru_seq_supported(T, B, D))
+            ddir = [torch.empty((B, D), device=dev, dtype=torch.float32) for _ in range(2)]
+            dGIT = bsum = None
+            if xbw > 0:
+                # the sweep writes bf16 dgh / dgi (the GEMM operands) and per-row bias sums;
+                # no fp32 copies of either
+                dGH = dGI = None
+                dGHT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T)
+                dGIT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T)
+                bsum = torch.empty((B, 4 * D), device=dev, dtype=torch.float32)
+            else:
+                dGH = torch.empty((B, Fr, 3 * D), device=dev, dtype=torch.float32)
+                dGHT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T) if lp else dGH
+                dGI = torch.empty((B, Fr, 3 * D), device=dev, dtype=torch.float32)
             if seq:
                 H.before_persistent_sweep()   # (DP: in-flight all-reduces finish first)
             if xbw > 0:
                 # reverse sweep in one persistent launch, row groups per XCD, W_hh^T in VGPRs
                 work = torch.empty(xbw, device=dev, dtype=torch.uint8)
                 dOutc = dOut.contiguous()
-                H.lib().call('srnn_gru_xcd_bwd', H.dcode(T), B, D, Fr, H.ptr(dOutc), Fr * D, D,
+                H.lib().call('srnn_gru_xcd_bwd2', H.dcode(T), B, D, Fr, H.ptr(dOutc), Fr * D, D,
                              H.ptr(gates[l]), Fr * 4 * D, 4 * D, H.ptr(outs[l]), Fr * D, D,
-                             H.ptr(h_in[l]), H.ptr(WhhT), H.ptr(dGH), H.ptr(dGHT), H.ptr(dGI),
-                             Fr * 3 * D, 3 * D, H.ptr(ddir[0]), H.ptr(work), xbw, st())
+                             H.ptr(h_in[l]), H.ptr(WhhT), None, H.ptr(dGHT), None, H.ptr(dGIT),
+                             H.ptr(bsum), Fr * 3 * D, 3 * D, H.ptr(ddir[0]), H.ptr(work), xbw,
+                             st())
             elif seq:
                 # the whole reverse sweep in one persistent launch (W_hh^T resident in LDS)
                 work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
@@ -387,12 +398,18 @@ class _TierFn(torch.autograd.Function):
             if Fr > 1:
                 H.lib().call('srnn_copy2d', H.dcode(T), H.dcode(T), B, (Fr - 1) * D,
                              H.ptr(outsT[l]), Fr * D, H.ptr(hprevT[:, 1:]), Fr * D, st())
-            dGH2, dGI2 = dGH.reshape(M, 3 * D), dGI.reshape(M, 3 * D)
             dW_hh = H.gemm(dGHT.reshape(M, 3 * D), hprevT.reshape(M, D), transA=True)
-            db_hh = H.colsum(dGH2, M, 3 * D)
-            dGIT = H.cast(dGI2, T)
+            if bsum is not None:
+                bs = H.colsum(bsum, B, 4 * D)               # sums of [dar | daz | dghn | dan]
+                db_hh = bs[:3 * D]
+                db_ih = torch.cat([bs[:2 * D], bs[3 * D:]])
+                dGIT = dGIT.reshape(M, 3 * D)
+            else:
+                dGH2, dGI2 = dGH.reshape(M, 3 * D), dGI.reshape(M, 3 * D)
+                db_hh = H.colsum(dGH2, M, 3 * D)
+                dGIT = H.cast(dGI2, T)
+                db_ih = H.colsum(dGI2, M, 3 * D)
             dW_ih = H.gemm(dGIT, xs[l], transA=True)
-            db_ih = H.colsum(dGI2, M, 3 * D)
             dX = H.gemm(dGIT, Wih[l])                                     # (M, D)
             g_rnn[l] = [dW_ih, dW_hh, db_ih, db_hh]
         # --- input projections
@@ -646,7 +663,7 @@ def generation_weights(model, dtype=None):
                 t.w_ih[l], t.w_hh[l] = H.ptr(wih), H.ptr(whh)
                 t.b_ih[l], t.b_hh[l] = H.ptr(bih), H.ptr(bhh)
             k_ = rnn.frame_size
-            w_up = H.permute3(nn.weight_of(rnn.upsampling.conv_t), (2, 1, 0), dtype=T)
+            w_up = nn.convt_operand(rnn.upsampling.conv_t, T)
             b_up = H.permute3(rnn.upsampling.bias.detach().reshape(1, D, k_), (0, 2, 1))
             h0 = rnn.h0.detach().float().contiguous()
             keep += [w_up, b_up, h0]

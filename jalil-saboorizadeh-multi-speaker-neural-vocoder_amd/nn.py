@@ -31,6 +31,28 @@ def weight_grad_to_params(mod, dw):
     return [dw]
 
 
+def convt_operand(conv_t, dtype):
+    """GEMM operand of a ConvTranspose1d weight (Cin, Cout, k): W (k, Cout, Cin) in `dtype`,
+    the weight norm (when present) folded in on the device without an fp32 weight."""
+    v = conv_t.weight_v if hasattr(conv_t, 'weight_g') else conv_t.weight
+    Cin, Cout, k = v.shape
+    if H.convt_operand_ok(Cin, Cout, k):
+        g = conv_t.weight_g if hasattr(conv_t, 'weight_g') else None
+        return H.convt_operand(g, v, k, dtype)
+    return H.permute3(weight_of(conv_t), (2, 1, 0), dtype=dtype)
+
+
+def convt_grad_to_params(conv_t, dwt):
+    """Parameter gradients of a ConvTranspose1d weight from the transposed GEMM weight
+    gradient dwt (Cin, k * Cout) = [i][j * Cout + o]."""
+    v = conv_t.weight_v if hasattr(conv_t, 'weight_g') else conv_t.weight
+    Cin, Cout, k = v.shape
+    if hasattr(conv_t, 'weight_g') and Cout % 4 == 0 and k * (Cout + 4) * 4 <= 150 * 1024:
+        return list(H.convt_wn_bwd(conv_t.weight_g, v, dwt, k))
+    dw = H.permute3(dwt.reshape(Cin, k, Cout), (0, 2, 1))            # (Cin, Cout, k)
+    return weight_grad_to_params(conv_t, dw)
+
+
 def weight_params(mod):
     if hasattr(mod, 'weight_g'):
         return [mod.weight_g, mod.weight_v]

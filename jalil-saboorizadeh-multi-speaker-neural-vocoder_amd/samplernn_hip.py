@@ -66,6 +66,11 @@ _SIGS = {
                          _SZ, _P],
     'srnn_gru_xcd_bwd': [_I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L, _P, _P, _P, _P, _P,
                          _L, _L, _P, _P, _SZ, _P],
+    'srnn_gru_xcd_bwd2': [_I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L, _P, _P, _P, _P, _P,
+                          _P, _P, _L, _L, _P, _P, _SZ, _P],
+    'srnn_weight_norm_scale': [_P, _P, _P, _I, _L, _P],
+    'srnn_convt_fold': [_P, _P, _P, _I, _I, _I, _I, _P],
+    'srnn_convt_wn_bwd': [_P, _P, _P, _P, _P, _I, _I, _I, _P],
     'srnn_gen_workspace_size': [_P, _I, ctypes.POINTER(_SZ)],
     'srnn_generate': [_P, _I, _I, _P, _P, _P, _U64, _P, _P, _P, _SZ, _I, _P],
     'srnn_persistent_flag_to_f32': [_P, _P],
@@ -363,6 +368,38 @@ def weight_norm(g, v):
     O = v.shape[0]
     lib().call('srnn_weight_norm_fwd', ptr(g), ptr(v), ptr(w), None, O, v.numel() // O, stream())
     return w
+
+
+def convt_operand(g, v, k, dtype):
+    """The upsampling GEMM operand W_up (k, Cout, Cin) = (g * v / ||v||).permute(2, 1, 0) in
+    `dtype`, straight from v (conv_t weight (Cin, Cout, k)); g None = no weight norm."""
+    need_cuda(v)
+    v = v.contiguous()
+    Cin, Cout = v.shape[0], v.shape[1]
+    out = torch.empty((k, Cout, Cin), device=v.device, dtype=dtype)
+    scale = None
+    if g is not None:
+        scale = torch.empty(Cin, device=v.device, dtype=torch.float32)
+        lib().call('srnn_weight_norm_scale', ptr(g), ptr(v), ptr(scale), Cin, v.numel() // Cin,
+                   stream())
+    lib().call('srnn_convt_fold', ptr(v), ptr(scale), ptr(out), dcode(out), Cin, Cout, k, stream())
+    return out
+
+
+def convt_operand_ok(Cin, Cout, k):
+    return Cin % 64 == 0 and (Cout * k) % 64 == 0 and 64 % k == 0
+
+
+def convt_wn_bwd(g, v, dwt, k):
+    """(dg, dv) of the weight norm from the transposed GEMM gradient dwt (Cin, k * Cout),
+    rows [i][j * Cout + o]."""
+    v = v.contiguous()
+    Cin, Cout = v.shape[0], v.shape[1]
+    dg = torch.empty_like(g)
+    dv = torch.empty_like(v)
+    lib().call('srnn_convt_wn_bwd', ptr(g), ptr(v), ptr(dwt.contiguous()), ptr(dg), ptr(dv), Cin,
+               Cout, k, stream())
+    return dg, dv
 
 
 def weight_norm_bwd(g, v, dw):

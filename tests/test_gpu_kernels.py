@@ -554,7 +554,7 @@ def test_permute3(hip, perm, shape):
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('rows,cols', [(131072, 256), (8192, 1024), (100, 37), (1, 1030), (0, 8),
-                                       (5000, 16384)])
+                                       (5000, 16384), (131072, 1), (5000, 3), (7, 2)])
 def test_colsum(hip, dtype, rows, cols):
     x = _rand(max(rows, 1), cols + 4, seed=rows + cols)[:rows].to(DEV, dtype)
     view = x[:, 2:cols + 2] if dtype == torch.float32 else x[:, :cols]
@@ -674,3 +674,90 @@ def test_learned_upsampling_module(hip):
     torch.testing.assert_close(x.grad.cpu(), xr.grad, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(m.conv_t.weight.grad.cpu(), Wr.grad, atol=1e-5, rtol=1e-5)
     torch.testing.assert_close(m.bias.grad.cpu(), br.grad, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize('Cin,Cout,k', [(1024, 1024, 16), (128, 64, 4), (64, 96, 2)])
+def test_convt_fold_matches_weight_norm_permute(hip, Cin, Cout, k):
+    """W_up = (g v / ||v||).permute(2, 1, 0) straight from v: bit-identical to the weight-norm
+    kernel followed by the permute (same per-channel scale), fp32 and bf16."""
+    g = (torch.rand(Cin, 1, 1) + 0.5).to(DEV)
+    v = _rand(Cin, Cout, k, seed=Cin + k).to(DEV)
+    ref = hip.permute3(hip.weight_norm(g, v), (2, 1, 0))
+    for dt in (torch.float32, torch.bfloat16):
+        out = hip.convt_operand(g, v, k, dt)
+        torch.testing.assert_close(out, ref.to(dt), atol=0, rtol=0)
+    plain = hip.convt_operand(None, v, k, torch.float32)
+    torch.testing.assert_close(plain, hip.permute3(v, (2, 1, 0)), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize('Cin,Cout,k', [(1024, 1024, 16), (256, 1024, 4), (20, 12, 3)])
+def test_convt_wn_bwd_matches_weight_norm_bwd(hip, Cin, Cout, k):
+    """Per-channel weight-norm backward from the transposed GEMM gradient [i][j*Cout + o]
+    == weight_norm_bwd on the permuted gradient, bit for bit."""
+    g = (torch.rand(Cin, 1, 1) + 0.5).to(DEV)
+    v = _rand(Cin, Cout, k, seed=11).to(DEV)
+    dwt = _rand(Cin, k * Cout, seed=12).to(DEV)
+    dw = hip.permute3(dwt.reshape(Cin, k, Cout), (0, 2, 1))
+    dg_ref, dv_ref = hip.weight_norm_bwd(g, v, dw)
+    dg, dv = hip.convt_wn_bwd(g, v, dwt, k)
+    torch.testing.assert_close(dg, dg_ref, atol=0, rtol=0)
+    torch.testing.assert_close(dv, dv_ref, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize('B,T', [(4, 1024), (3, 17)])
+def test_nll_bwd_dense_gradient(hip, B, T):
+    """srnn_nll_bwd (vectorised Q = 256 path): -scale * g at the target, zero elsewhere."""
+    Q = 256
+    tgt = torch.randint(0, Q, (B, T), generator=torch.Generator().manual_seed(B + T))
+    gd = torch.full((1,), 0.75, device=DEV)
+    d = torch.full((B, T, Q), float('nan'), device=DEV)
+    tgd = tgt.to(DEV)
+    hip.lib().call('srnn_nll_bwd', hip.ptr(tgd), T, T, B * T, Q, hip.ptr(d), Q, 0.5, hip.ptr(gd),
+                   hip.stream())
+    ref = torch.zeros(B, T, Q)
+    ref.scatter_(2, tgt.unsqueeze(-1), -0.375)
+    torch.testing.assert_close(d.cpu(), ref, atol=0, rtol=0)
+
+
+@pytest.mark.parametrize('B,D,Fr', [(128, 1024, 64), (100, 256, 9)])
+def test_gru_xcd_bwd2_lowp_outputs(hip, B, D, Fr):
+    """srnn_gru_xcd_bwd2 without fp32 dgh/dgi: dgh_lp and dgi_lp equal the bf16 casts of the
+    fp32 sweep's outputs, bsum the per-row sums over t of [dar | daz | dghn | dan]."""
+    T = torch.bfloat16
+    nb = hip.gru_xcd_bwd_work_bytes(T, B, D)
+    if not nb:
+        pytest.skip('gru_xcd not supported on this device')
+    g = torch.Generator().manual_seed(B + D)
+    whh = (torch.randn(3 * D, D, generator=g) * 0.03).to(T)
+    bhh = torch.randn(3 * D, generator=g) * 0.1
+    gi = torch.randn(B * Fr, 3 * D, generator=g) * 0.5
+    h0 = torch.randn(B, D, generator=g) * 0.5
+    dy = (torch.randn(B, Fr, D, generator=g) * 0.1).to(DEV)
+    out, gates = _gru_ref(gi, h0, whh, bhh, Fr)
+    whh_t = whh.float().t().contiguous().to(DEV, T)
+    gtd, outd, h0d = gates.to(DEV), out.to(DEV), h0.to(DEV)
+
+    def run(full):
+        dgh = torch.full((B, Fr, 3 * D), float('nan'), device=DEV) if full else None
+        dgi = torch.full((B, Fr, 3 * D), float('nan'), device=DEV) if full else None
+        dgh_lp = torch.zeros((B, Fr, 3 * D), device=DEV, dtype=T)
+        dgi_lp = None if full else torch.zeros((B, Fr, 3 * D), device=DEV, dtype=T)
+        bsum = None if full else torch.full((B, 4 * D), float('nan'), device=DEV)
+        ddir0 = torch.full((B, D), float('nan'), device=DEV)
+        work = torch.full((nb,), 7, device=DEV, dtype=torch.uint8)
+        hip.lib().call('srnn_gru_xcd_bwd2', hip.BF16, B, D, Fr, hip.ptr(dy), Fr * D, D,
+                       hip.ptr(gtd), Fr * 4 * D, 4 * D, hip.ptr(outd), Fr * D, D, hip.ptr(h0d),
+                       hip.ptr(whh_t), hip.ptr(dgh), hip.ptr(dgh_lp), hip.ptr(dgi),
+                       hip.ptr(dgi_lp), hip.ptr(bsum), Fr * 3 * D, 3 * D, hip.ptr(ddir0),
+                       hip.ptr(work), nb, hip.stream())
+        torch.cuda.synchronize()
+        assert hip.lib().dll.srnn_gru_xcd_error(hip.ptr(work)) == 0
+        return dgh, dgi, dgh_lp, dgi_lp, bsum, ddir0
+
+    dgh, dgi, dgh_lp_a, _, _, ddir_a = run(True)
+    _, _, dgh_lp, dgi_lp, bsum, ddir_b = run(False)
+    torch.testing.assert_close(dgh_lp, dgh_lp_a, atol=0, rtol=0)
+    torch.testing.assert_close(dgi_lp, dgi.to(T), atol=0, rtol=0)
+    torch.testing.assert_close(ddir_b, ddir_a, atol=0, rtol=0)
+    ref = torch.cat([dgh.sum(1), dgi[..., 2 * D:].sum(1)], 1)
+    torch.testing.assert_close(bsum, ref, atol=1e-5 * ref.abs().max().item(), rtol=1e-5)
