@@ -332,14 +332,21 @@ __global__ __launch_bounds__(256) void gemm_small_k2_kernel(
     {   // B: thread t loads column n0 + t, all k
         float* bt = reinterpret_cast<float*>(bsT);
         const int n = n0 + tid;
+        // loads from clamped addresses, zeroed after the load: a "load or zero" select per
+        // element would make the compiler wait for each load in turn (one L2 round trip each)
         const T* bp = B + (int64_t)min(n, N - 1) * ldb;
-#pragma unroll 8
-        for (int k = 0; k < KMAX; ++k)
-            bt[k * 256 + tid] = (k < K && n < N) ? to_f(bp[k]) : 0.f;
+        const bool nok = n < N;
+#pragma unroll 16
+        for (int k = 0; k < KMAX; ++k) {
+            const float v = to_f(bp[min(k, K - 1)]);
+            bt[k * 256 + tid] = (k < K && nok) ? v : 0.f;
+        }
         float* at = reinterpret_cast<float*>(as);
-        for (int i = tid; i < 32 * KMAX; i += 256) {
-            const int r = i / KMAX, k = i % KMAX;
-            at[i] = (k < K && m0 + r < M) ? to_f(A[(int64_t)(m0 + r) * lda + k]) : 0.f;
+#pragma unroll
+        for (int i0 = 0; i0 < 32 * KMAX; i0 += 256) {
+            const int i = i0 + tid, r = i / KMAX, k = i % KMAX;
+            const float v = to_f(A[(int64_t)min(m0 + r, M - 1) * lda + min(k, K - 1)]);
+            at[i] = (k < K && m0 + r < M) ? v : 0.f;
         }
     }
     __syncthreads();

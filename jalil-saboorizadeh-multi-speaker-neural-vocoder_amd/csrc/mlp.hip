@@ -127,12 +127,171 @@ __global__ __launch_bounds__(256) void mlp_l1_xcd_kernel(const T* __restrict__ t
     }
 }
 
+// LDS-resident variant for the bf16 training shape (FS0 = 16, Q = 256): workgroup (cg, rc)
+// keeps the table slice Tab[:, :, 16 cg .. 16 cg + 16) -- 16 x 256 x 16 bf16 = 128 KiB -- in
+// LDS for its whole chunk of batch rows, so every gather is a ds_read_b128 instead of an L2
+// round trip (the L2 gather of mlp_l1_xcd_kernel moves 16 x 2 B per output element through
+// the L2 -> CU path).  A row is two lanes (8 columns each); its 16 byte indices come from a
+// double-buffered LDS copy of the batch row's index stream (aligned dword reads + alignbyte).
+// Accumulation: v_dot2c_f32_bf16 against (1, 0) / (0, 1) adds one bf16 to an fp32 sum
+// with a single rounding -- the same result as convert + add, in one instruction instead
+// of two.  The (1, 0) operand must live in a VGPR: hipcc (ROCm 7.2) folds the constant
+// 0x00003f80 into the inline constant 1.0, which the instruction reads as (0, 1)
+// (tools/dot2_probe).  The summation order (upper, then taps 0..15) is mlp_l1_xcd_kernel's,
+// so both produce identical bits.
+typedef __bf16 l1_bf16x2 __attribute__((ext_vector_type(2)));
+constexpr int L1L_NT = 1024;
+
+__device__ __forceinline__ void l1l_add8(const uint4 v, float (&a)[8], l1_bf16x2 lo1,
+                                         l1_bf16x2 hi1) {
+    const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const l1_bf16x2 p = __builtin_bit_cast(l1_bf16x2, w[i]);
+        a[2 * i] = __builtin_amdgcn_fdot2_f32_bf16(p, lo1, a[2 * i], false);
+        a[2 * i + 1] = __builtin_amdgcn_fdot2_f32_bf16(p, hi1, a[2 * i + 1], false);
+    }
+}
+
+__global__ __launch_bounds__(L1L_NT, 1) void mlp_l1_lds_kernel(
+    const bf16* __restrict__ tab, const int64_t* __restrict__ x, int64_t ldx, int xoff, int B,
+    int Tlen, int bpc, const bf16* __restrict__ upper, int64_t ldu, bf16* __restrict__ out,
+    int64_t ldo, int D) {
+    constexpr int FS = 16, Q = 256;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    char* tl = smem;                                        // [FS * Q][16] bf16 = 128 KiB
+    unsigned char* ib = reinterpret_cast<unsigned char*>(smem + FS * Q * 32);
+    const int W = Tlen + FS - 1, WP = (W + 4 + 15) & ~15;   // + 4: the last dword read
+    const int tid = threadIdx.x;
+    // blocks of one XCD (blockIdx % 8 under round-robin dispatch) cover 8 adjacent column
+    // groups, so the 32-B pieces of a 128-B line of `upper` / `out` meet in one L2
+    const int ncg = D / 16, xcd = blockIdx.x % 8, loc = blockIdx.x / 8;
+    int cg, rc;
+    if (ncg % 8 == 0) {
+        const int per = ncg / 8;
+        cg = xcd * per + loc % per;
+        rc = loc / per;
+    } else {
+        cg = blockIdx.x % ncg;
+        rc = blockIdx.x / ncg;
+    }
+    const int b0 = rc * bpc, b1 = min(B, b0 + bpc);
+    if (b0 >= b1) return;
+    const int c0 = cg * 16;
+    for (int i = tid; i < FS * Q * 2; i += L1L_NT) {       // the table slice, 16 B per thread
+        const int row = i >> 1, h = i & 1;
+        *reinterpret_cast<uint4*>(tl + i * 16) =
+            *reinterpret_cast<const uint4*>(tab + (int64_t)row * D + c0 + h * 8);
+    }
+    // the next batch row's indices and `upper` rows are loaded into registers one batch
+    // row ahead (loads in flight across the current row's gathers), written / used after
+    constexpr int RPT = 4;                                   // rows per thread per batch row
+    const int nrt = (Tlen + L1L_NT / 2 - 1) / (L1L_NT / 2);
+    const int h = tid & 1, t0 = tid >> 1;
+    int64_t xn[2];
+    auto load_x = [&](int b) {
+        const int64_t* xr = x + (int64_t)b * ldx + xoff;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int p = tid + j * L1L_NT;
+            xn[j] = xr[min(p, W - 1)];
+        }
+    };
+    auto put_x = [&](unsigned char* dst) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int p = tid + j * L1L_NT;
+            if (p < WP) dst[p] = p < W ? (unsigned char)xn[j] : 0;
+        }
+    };
+    uint4 un[RPT];
+    auto load_u = [&](int b) {
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            const int t = min(t0 + i * (L1L_NT / 2), Tlen - 1);
+            if (i < nrt)
+                un[i] = *reinterpret_cast<const uint4*>(upper + ((int64_t)b * Tlen + t) * ldu + c0 + h * 8);
+        }
+    };
+    unsigned one_lo = 0x00003f80u, one_hi = 0x3f800000u;   // (1, 0), (0, 1) in VGPRs
+    asm volatile("" : "+v"(one_lo), "+v"(one_hi));
+    const l1_bf16x2 lo1 = __builtin_bit_cast(l1_bf16x2, one_lo);
+    const l1_bf16x2 hi1 = __builtin_bit_cast(l1_bf16x2, one_hi);
+    load_x(b0);
+    load_u(b0);
+    put_x(ib);
+    __syncthreads();
+    for (int b = b0; b < b1; ++b) {
+        const unsigned char* cur = ib + ((b - b0) & 1) * WP;
+        const bool more = b + 1 < b1;
+        if (more) load_x(b + 1);
+        uint4 uc[RPT];
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) uc[i] = un[i];
+        if (more) load_u(b + 1);
+#pragma unroll
+        for (int i = 0; i < RPT; ++i) {
+            const int t = t0 + i * (L1L_NT / 2);
+            if (i >= nrt || t >= Tlen) break;
+            const int64_t r = (int64_t)b * Tlen + t;
+            float a[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] = 0.f;
+            l1l_add8(uc[i], a, lo1, hi1);
+            const int tb = t & ~3, sh = t & 3;
+            const unsigned* iw = reinterpret_cast<const unsigned*>(cur + tb);
+            unsigned w5[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) w5[j] = iw[j];
+            unsigned q4[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) q4[j] = __builtin_amdgcn_alignbyte(w5[j + 1], w5[j], sh);
+            uint4 tv[FS];
+#pragma unroll
+            for (int k = 0; k < FS; ++k) {
+                const unsigned q = (q4[k >> 2] >> (8 * (k & 3))) & 0xffu;
+                tv[k] = *reinterpret_cast<const uint4*>(tl + ((k * Q + q) * 2 + h) * 16);
+            }
+#pragma unroll
+            for (int k = 0; k < FS; ++k) l1l_add8(tv[k], a, lo1, hi1);
+            l1_store8(out + r * ldo + c0 + h * 8, a);
+        }
+        if (more) put_x(ib + ((b + 1 - b0) & 1) * WP);
+        __syncthreads();                                    // next buffer staged, cur free
+    }
+}
+
 template <typename T, typename TU>
 static int mlp_l1_launch(const T* tab, const int64_t* x, int64_t ldx, int xoff, const int* base,
                          int B, int Tlen, const TU* upper, int64_t ldu, T* out, int64_t ldo,
                          int D, int FS0, int Q, hipStream_t s) {
     const int64_t nrows = (int64_t)B * Tlen;
     const int ue = (int)sizeof(TU);
+    if constexpr (sizeof(T) == 2 && sizeof(TU) == 2) {
+        const int W = Tlen + FS0 - 1, WP = (W + 4 + 15) & ~15;
+        const int ncg = D / 16;
+        const int lds = 16 * 256 * 32 + 2 * WP;
+        if (!base && FS0 == 16 && Q == 256 && D % 16 == 0 && ncg <= 256 && lds <= 160 * 1024 &&
+            Tlen <= 4 * (L1L_NT / 2) && WP <= 2 * L1L_NT &&
+            nrows >= 4096 && ldu % 8 == 0 && (uintptr_t)upper % 16 == 0 && ldo % 8 == 0 &&
+            (uintptr_t)out % 16 == 0 && (uintptr_t)tab % 16 == 0 && env_flag("SRNN_L1_LDS", 1)) {
+            const int nrc = std::max(1, std::min(B, 256 / ncg));
+            const int bpc = (B + nrc - 1) / nrc;
+            const int nrc2 = (B + bpc - 1) / bpc;
+            static bool attr = false;
+            if (!attr) {
+                SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)mlp_l1_lds_kernel,
+                                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   160 * 1024));
+                attr = true;
+            }
+            hipLaunchKernelGGL(mlp_l1_lds_kernel, dim3(ncg * nrc2), dim3(L1L_NT), lds, s,
+                               (const bf16*)tab, x, ldx, xoff, B, Tlen, bpc, (const bf16*)upper,
+                               ldu, (bf16*)out, ldo, D);
+            SRNN_LAUNCH_CHECK();
+            return 0;
+        }
+    }
     if (!base && D % 128 == 0 && nrows >= 4096 && (ldu * ue) % 16 == 0 &&
         (uintptr_t)upper % 16 == 0 && (ldo * (int)sizeof(T)) % 16 == 0 &&
         (uintptr_t)out % 16 == 0 && (uintptr_t)tab % 16 == 0) {

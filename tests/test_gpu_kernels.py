@@ -552,6 +552,32 @@ def test_permute3(hip, perm, shape):
     torch.testing.assert_close(acc, want, atol=0, rtol=0)
 
 
+@pytest.mark.parametrize('B,Tl,D', [(128, 1024, 1024), (4, 2048, 1024), (6, 1000, 512),
+                                    (3, 4096, 272)])
+def test_mlp_l1_lds_matches_l2_gather(hip, B, Tl, D, monkeypatch):
+    """bf16 training gather: the LDS-resident table kernel == the L2-gather kernels bit for
+    bit (same summation order, single-rounding adds)."""
+    FS0, Q = 16, 256
+    g = torch.Generator().manual_seed(B + Tl + D)
+    tab = (torch.randn(FS0, Q, D, generator=g) * 0.3).to(DEV, torch.bfloat16)
+    x = torch.randint(0, Q, (B, Tl + FS0 + 3), generator=g).to(DEV)
+    upper = (torch.randn(B * Tl, D, generator=g) * 0.5).to(DEV, torch.bfloat16)
+    outs = []
+    for flag in ('1', '0'):
+        monkeypatch.setenv('SRNN_L1_LDS', flag)
+        out = torch.empty(B * Tl, D, device=DEV, dtype=torch.bfloat16)
+        hip.lib().call('srnn_mlp_l1', hip.BF16, hip.ptr(tab), hip.ptr(x), x.shape[1], 2, B, Tl,
+                       hip.BF16, hip.ptr(upper), D, hip.ptr(out), D, D, FS0, Q, hip.stream())
+        outs.append(out)
+    torch.testing.assert_close(outs[0], outs[1], atol=0, rtol=0)
+    idx = torch.stack([x[:, 2 + k:2 + k + Tl] for k in range(FS0)], -1).reshape(B * Tl, FS0)
+    ref = upper.float().clone()
+    for k in range(FS0):
+        ref += tab[k].float()[idx[:, k]]
+    torch.testing.assert_close(outs[0].float(), ref.clamp_min(0).to(torch.bfloat16).float(),
+                               atol=2e-2, rtol=1e-2)
+
+
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('rows,cols', [(131072, 256), (8192, 1024), (100, 37), (1, 1030), (0, 8),
                                        (5000, 16384), (131072, 1), (5000, 3), (7, 2)])
