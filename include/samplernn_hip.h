@@ -139,6 +139,13 @@ int srnn_mlp_l1(int dtype, const void* tab, const int64_t* x, int64_t ldx, int x
 int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x, int64_t ldx,
                   int xoff, int B, int Tlen, void* dtab, int out_dtype, int D, int FS0, int Q,
                   void* work, size_t work_bytes, void* stream);
+/* Same, and (colsum != NULL) the bottom tier's upsampling bias gradient from the same pass:
+ * colsum[j * D + c] = sum over batch rows and t = j (mod FS0) of da[b, t, c] (fp32, FS0 x D);
+ * *colsum_done (host int) = 1 when it was written (the direct position-major path), else 0
+ * and the caller sums the columns itself.                                                   */
+int srnn_mlp_dtab2(int dtype, const void* da, int64_t ldda, const int64_t* x, int64_t ldx,
+                   int xoff, int B, int Tlen, void* dtab_out, int out_dtype, int D, int FS0, int Q,
+                   void* work, size_t work_bytes, float* colsum, int* colsum_done, void* stream);
 /* (deterministic: 2^-40 fixed-point int64 accumulation; work >= Q*FS0*D*8 bytes)        */
 /* log_softmax (model.py:324-325) + NLL rows (nn.py:66-70) + dlogits (softmax-onehot)*g  */
 /* dz = dlogp - exp(logp) * rowsum(dlogp)   (log_softmax backward, rows of Q)          */

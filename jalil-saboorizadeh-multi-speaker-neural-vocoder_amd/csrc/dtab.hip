@@ -121,14 +121,23 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_fx_kernel(
 // row is loaded and converted ONCE (not once per tap) and each step is one address add,
 // a conditional register swap and one ds_add_u64.  A wave walks whole batch rows in
 // 16-position batches; the next batch's values are loaded while the current one runs.
+// The batch row's indices are staged as bytes in a per-wave LDS strip (vector loads), and
+// a batch's 16 indices are ONE broadcast ds_read_b128 issued a batch ahead and waited for
+// with a counted lgkmcnt past the batch's 16 atomics: scalar index loads would cost ~6
+// SALU instructions each on the CU's one scalar unit, and would share the LGKM counter
+// with the atomics (every index wait draining them).
 // DIRECT (one row block: the workgroup sees every row of its columns): the accumulator is
 // final, so the flush converts and stores straight into the output (no zeroed int64
-// buffer, no global atomics, no conversion pass).
+// buffer, no global atomics, no conversion pass); `colsum` (optional, DIRECT only) also
+// receives sum_b sum_{t = j mod 16} da[b, t, c] at [j * D + c] -- the bias gradient of the
+// bottom tier's upsampling (nn.py:33-43) -- from the same loaded rows, in fixed point.
+typedef unsigned dt_u32x4 __attribute__((ext_vector_type(4)));
+
 template <typename T, typename TO, bool DIRECT>
 __global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
     const T* __restrict__ da, int64_t ldda, const int64_t* __restrict__ x, int64_t ldx, int xoff,
     int Tlen, int B, int nb, int nrb, unsigned long long* __restrict__ fx, TO* __restrict__ out,
-    int D, int Q) {
+    float* __restrict__ colsum, int D, int Q) {
     constexpr int CW = 4, FS = 16;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [Q][CW][FS]
@@ -148,8 +157,11 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
     const int b0 = rb * nb;
     const int nbb = min(nb, B - b0);
     const int W = Tlen + FS - 1;                   // positions per batch row
+    const int WPB = (W + 31) & ~15;                // strip bytes: every batch's 16-B read fits
     const int nacc = Q * FS * CW;
-    for (int i = tid; i < nacc; i += DTAB_NT) acc[i] = 0ull;
+    unsigned long long* csum = acc + nacc;         // [CW][FS] column sums (fixed point)
+    unsigned char* strip = reinterpret_cast<unsigned char*>(csum + CW * FS) + wave * WPB;
+    for (int i = tid; i < nacc + CW * FS; i += DTAB_NT) acc[i] = 0ull;
     __syncthreads();
     const int c = lane >> 4, li = lane & 15;       // column, row residue
     const bool cok = c0 + c < D;
@@ -157,31 +169,40 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
     const int coff = c * FS;
     const int nbatch = (W + 15) / 16;
     const unsigned acc_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)acc;
+    const unsigned strip_base =
+        (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)strip;
+    unsigned long long colacc = 0;
     for (int b = wave; b < nbb; b += DTAB_NT / 64) {
         const T* drow = dcol + (int64_t)(b0 + b) * Tlen * ldda;
-        const int64_t* srow = x + (int64_t)(b0 + b) * ldx + xoff;   // wave-uniform
+        const int64_t* srow = x + (int64_t)(b0 + b) * ldx + xoff;
         auto load = [&](int pbase) -> long long {
             const int t = pbase + li;
             return (cok && t < Tlen) ? fx40(to_f(drow[(int64_t)t * ldda])) : 0ll;
         };
-        // the 16 indices of a batch (scalar loads, clamped to the row), one batch ahead
-        auto load_q = [&](int pbase, int (&q)[16]) {
-#pragma unroll
-            for (int j = 0; j < 16; ++j) q[j] = (int)srow[min(pbase + j, W - 1)];
-        };
+        // stage the row's indices (this wave's strip; its own later reads are ordered)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // strip reads of the last row
+        for (int p = lane; p < WPB; p += 64) {
+            const int64_t q = srow[min(p, W - 1)];
+            strip[p] = p < W ? (unsigned char)q : 0;
+        }
         long long cur = 0;                         // row p_base + li - 16 (none yet)
         long long nxt = load(0);
-        int qn[16];
-        load_q(0, qn);
+        dt_u32x4 qn;
+        asm volatile("s_waitcnt lgkmcnt(0)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(qn) : "v"(strip_base) : "memory");
+        __builtin_amdgcn_sched_barrier(0);
         for (int bt = 0; bt < nbatch; ++bt) {
             const int pbase = bt * 16;
             const long long nv = nxt;
-            int qc[16];
-#pragma unroll
-            for (int j = 0; j < 16; ++j) qc[j] = qn[j];
+            colacc += (unsigned long long)nv;
+            const dt_u32x4 qc = qn;
             if (bt + 1 < nbatch) {
                 nxt = load(pbase + 16);
-                load_q(pbase + 16, qn);
+                // next batch's indices: issued before this batch's 16 atomics, waited for
+                // after them with lgkmcnt(15) (LDS operations of a wave complete in order; 15 =
+                // the counter's maximum: the first atomic is waited for too)
+                asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(qn)
+                             : "v"(strip_base + (unsigned)pbase) : "memory");
             }
             const int jmax = min(16, W - pbase);
             // all 16 addresses and operands in their own registers first, then 16
@@ -191,7 +212,8 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
             unsigned long long va[16];
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                ad[j] = acc_base + (unsigned)((qc[j] * CW * FS + coff + ((j - li) & 15)) * 8);
+                const unsigned q = (qc[j >> 2] >> (8 * (j & 3))) & 0xffu;
+                ad[j] = acc_base + ((q * (CW * FS) + (unsigned)(coff + ((j - li) & 15))) << 3);
                 va[j] = (unsigned long long)(li <= j ? nv : cur);   // row enters at tap 0
             }
             if (jmax == 16) {
@@ -204,15 +226,19 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
                              "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8]), "v"(ad[9]),
                              "v"(ad[10]), "v"(ad[11]), "v"(ad[12]), "v"(ad[13]), "v"(ad[14]),
                              "v"(ad[15]));
+                asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
             } else {
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
                     if (j < jmax) asm volatile("ds_add_u64 %0, %1" ::"v"(ad[j]), "v"(va[j]) : "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             }
+            __builtin_amdgcn_sched_barrier(0);
             cur = nv;
         }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");    // inline-asm atomics
+    if (DIRECT && colsum) atomicAdd(&csum[c * FS + li], colacc);
     __syncthreads();
     for (int i = tid; i < nacc; i += DTAB_NT) {
         // i walks the output order (q, k, c): 4 adjacent threads store 4 adjacent columns
@@ -223,6 +249,12 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
         const int64_t o = ((int64_t)q * FS + k) * D + c0 + cc;
         if (DIRECT) out[o] = from_f<TO>((float)((double)(long long)v * (1.0 / DTAB_SCALE)));
         else if (v != 0ull) atomicAdd(&fx[o], v);
+    }
+    if (DIRECT && colsum && tid < CW * FS) {
+        const int cc = tid / FS, j = tid % FS;
+        if (c0 + cc < D)
+            colsum[(int64_t)j * D + c0 + cc] =
+                (float)((double)(long long)csum[cc * FS + j] * (1.0 / DTAB_SCALE));
     }
 }
 
@@ -265,11 +297,16 @@ static bool getenv_off(const char* name) {
     return e && e[0] == '0';
 }
 
+static int pos_lds_bytes(int Q, int Tlen) {
+    const int W = Tlen + 15, WPB = (W + 31) & ~15;
+    return Q * 16 * 4 * 8 + 4 * 16 * 8 + (DTAB_NT / 64) * WPB;
+}
+
 template <typename T, typename TO, bool DIRECT>
 static int launch_pos(const void* da, int64_t ldda, const int64_t* x, int64_t ldx, int xoff, int B,
-                      int Tlen, unsigned long long* fx, void* out, int D, int Q, int nb, int nrb,
-                      hipStream_t s) {
-    const int lds = Q * 16 * 4 * 8;
+                      int Tlen, unsigned long long* fx, void* out, float* colsum, int D, int Q,
+                      int nb, int nrb, hipStream_t s) {
+    const int lds = pos_lds_bytes(Q, Tlen);
     const int nslices = cdiv(D, 4);
     auto k = dtab_pos_kernel<T, TO, DIRECT>;
     static bool attr = false;
@@ -279,7 +316,7 @@ static int launch_pos(const void* da, int64_t ldda, const int64_t* x, int64_t ld
         attr = true;
     }
     hipLaunchKernelGGL(k, dim3(nslices * nrb), dim3(DTAB_NT), lds, s, (const T*)da, ldda, x, ldx,
-                       xoff, Tlen, B, nb, nrb, fx, (TO*)out, D, Q);
+                       xoff, Tlen, B, nb, nrb, fx, (TO*)out, colsum, D, Q);
     SRNN_LAUNCH_CHECK();
     return 0;
 }
@@ -287,40 +324,47 @@ static int launch_pos(const void* da, int64_t ldda, const int64_t* x, int64_t ld
 // position-major path (FS0 == 16); returns 1 if it wrote dtab_out directly
 template <typename T>
 static int dtab_pos(const void* da, int64_t ldda, const int64_t* x, int64_t ldx, int xoff, int B,
-                    int Tlen, unsigned long long* fx, void* out, int out_dtype, int D, int Q,
-                    bool* direct, hipStream_t s) {
+                    int Tlen, unsigned long long* fx, void* out, int out_dtype, float* colsum,
+                    int D, int Q, bool* direct, hipStream_t s) {
     const int nslices = cdiv(D, 4);
     if (nslices >= 192) {          // every workgroup takes all rows of its 4 columns
         *direct = true;
         return out_dtype == SRNN_F32
-                   ? launch_pos<T, float, true>(da, ldda, x, ldx, xoff, B, Tlen, fx, out, D, Q, B, 1, s)
-                   : launch_pos<T, bf16, true>(da, ldda, x, ldx, xoff, B, Tlen, fx, out, D, Q, B, 1, s);
+                   ? launch_pos<T, float, true>(da, ldda, x, ldx, xoff, B, Tlen, fx, out, colsum, D, Q, B, 1, s)
+                   : launch_pos<T, bf16, true>(da, ldda, x, ldx, xoff, B, Tlen, fx, out, colsum, D, Q, B, 1, s);
     }
     *direct = false;
     const int nblk = std::max(1, 1024 / nslices);
     const int nb = std::max(1, cdiv(B, nblk));
-    return launch_pos<T, float, false>(da, ldda, x, ldx, xoff, B, Tlen, fx, out, D, Q, nb,
+    return launch_pos<T, float, false>(da, ldda, x, ldx, xoff, B, Tlen, fx, out, nullptr, D, Q, nb,
                                        cdiv(B, nb), s);
 }
 
-// dtab_out (Q, FS0, D) in out_dtype; work: >= Q*FS0*D*8 bytes of device scratch
-extern "C" int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x,
-                             int64_t ldx, int xoff, int B, int Tlen, void* dtab_out,
-                             int out_dtype, int D, int FS0, int Q, void* work, size_t work_bytes,
-                             void* stream) {
+// dtab_out (Q, FS0, D) in out_dtype; work: >= Q*FS0*D*8 bytes of device scratch.
+// colsum (optional, (FS0 * D) fp32): sum over batch rows of da rows t = j (mod FS0) at
+// [j * D + c]; *colsum_done (host) = 1 when it was written (the direct position-major path)
+extern "C" int srnn_mlp_dtab2(int dtype, const void* da, int64_t ldda, const int64_t* x,
+                              int64_t ldx, int xoff, int B, int Tlen, void* dtab_out,
+                              int out_dtype, int D, int FS0, int Q, void* work, size_t work_bytes,
+                              float* colsum, int* colsum_done, void* stream) {
     SRNN_REQUIRE(Q <= 256, "dtab: q_levels must be <= 256 (byte indices)");
     const int64_t n = (int64_t)Q * FS0 * D;
     SRNN_REQUIRE(work && work_bytes >= (size_t)n * 8, "dtab: workspace too small");
     hipStream_t s = (hipStream_t)stream;
     unsigned long long* fx = (unsigned long long*)work;
-    if (FS0 == 16 && Q * 16 * 4 * 8 <= 160 * 1024 && (int64_t)B * Tlen > 0 &&
+    if (colsum_done) *colsum_done = 0;
+    if (FS0 == 16 && pos_lds_bytes(Q, Tlen) <= 160 * 1024 && (int64_t)B * Tlen > 0 &&
         !getenv_off("SRNN_DTAB_POS")) {
         bool direct = false;
         if (cdiv(D, 4) < 192) SRNN_CHECK_HIP(hipMemsetAsync(fx, 0, (size_t)n * 8, s));
         const int rc = dtype == SRNN_F32
-            ? dtab_pos<float>(da, ldda, x, ldx, xoff, B, Tlen, fx, dtab_out, out_dtype, D, Q, &direct, s)
-            : dtab_pos<bf16>(da, ldda, x, ldx, xoff, B, Tlen, fx, dtab_out, out_dtype, D, Q, &direct, s);
-        if (rc || direct) return rc;
+            ? dtab_pos<float>(da, ldda, x, ldx, xoff, B, Tlen, fx, dtab_out, out_dtype, colsum, D, Q, &direct, s)
+            : dtab_pos<bf16>(da, ldda, x, ldx, xoff, B, Tlen, fx, dtab_out, out_dtype, colsum, D, Q, &direct, s);
+        if (rc) return rc;
+        if (direct) {
+            if (colsum && colsum_done) *colsum_done = 1;
+            return 0;
+        }
         goto convert;
     }
     SRNN_CHECK_HIP(hipMemsetAsync(fx, 0, (size_t)n * 8, s));
@@ -350,4 +394,12 @@ convert:
                            (bf16*)dtab_out, n);
     SRNN_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x,
+                             int64_t ldx, int xoff, int B, int Tlen, void* dtab_out,
+                             int out_dtype, int D, int FS0, int Q, void* work, size_t work_bytes,
+                             void* stream) {
+    return srnn_mlp_dtab2(dtype, da, ldda, x, ldx, xoff, B, Tlen, dtab_out, out_dtype, D, FS0, Q,
+                          work, work_bytes, nullptr, nullptr, stream);
 }

@@ -29,6 +29,7 @@ import utils
 import samplernn_hip as H
 
 verbose = False
+_STATS = {'fused_colsum': 0}     # (tests) how often a fused side result was consumed
 
 
 def _default_dtype():
@@ -329,7 +330,13 @@ class _TierFn(torch.autograd.Function):
         # weight gradient transposed, [i][j*D + o]: one row per input channel for the
         # per-channel weight-norm backward (no permute of the 16 x D x D gradient)
         dWupT = H.gemm(outsT[-1].reshape(M, D), dYT, transA=True)         # (D, k*D)
-        db_up = H.colsum(dY2, M, k * D)
+        # bias gradient: summed by the MLP's dTab pass when dY is its untouched d(upper)
+        cs = getattr(dY, '_srnn_colsum', None)
+        if cs is not None and cs[1] == dY._version and cs[2] == k and cs[0].numel() == k * D:
+            db_up = cs[0]
+            _STATS['fused_colsum'] += 1
+        else:
+            db_up = H.colsum(dY2, M, k * D)
         dX = H.gemm(dYT, W_up.reshape(k * D, D))                          # (M, D)
         g_up = nn.convt_grad_to_params(mod.upsampling.conv_t, dWupT)
         g_up_b = H.permute3(db_up.reshape(1, k, D), (0, 2, 1)).reshape(D, k)
@@ -550,8 +557,13 @@ class _MlpFn(torch.autograd.Function):
         # folded embedding . conv backward: dTab[q][k][:] += da1[t] for x_{t+k} = q
         dtabT = torch.empty((Q, FS0 * D), device=dev, dtype=T)
         work = torch.empty(Q * FS0 * D, device=dev, dtype=torch.int64)
-        H.lib().call('srnn_mlp_dtab', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.shape[1], 0, B, Tl,
-                     H.ptr(dtabT), H.dcode(T), D, FS0, Q, H.ptr(work), work.numel() * 8, st())
+        # the same pass sums da1 over rows t = j (mod FS0): the bottom tier's upsampling bias
+        # gradient (its output is this layer's `upper`), handed over on the returned gradient
+        colsum = torch.empty(FS0 * D, device=dev, dtype=torch.float32)
+        done = ctypes.c_int(0)
+        H.lib().call('srnn_mlp_dtab2', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.shape[1], 0, B,
+                     Tl, H.ptr(dtabT), H.dcode(T), D, FS0, Q, H.ptr(work), work.numel() * 8,
+                     H.ptr(colsum), ctypes.byref(done), st())
         dE = H.gemm(dtabT, Wp.reshape(FS0 * D, Q))                       # (Q, Q)
         dWp = torch.empty((FS0, D, Q), device=dev, dtype=torch.float32)
         H.gemm(dtabT, ET, transA=True, out=dWp, M=D, N=Q, K=Q, lda=FS0 * D, ldb=Q, ldc=Q,
@@ -561,7 +573,10 @@ class _MlpFn(torch.autograd.Function):
         grads += nn.weight_grad_to_params(mlp.input, dW_in)
         grads += nn.weight_grad_to_params(mlp.hidden, dW_hid.reshape(D, D, 1)) + [db_hid]
         grads += nn.weight_grad_to_params(mlp.output, dW_out.reshape(Q, D, 1)) + [db_out]
-        return (None, None, da1.reshape(B, Tl, D)) + tuple(grads)
+        d_upper = da1.reshape(B, Tl, D)
+        if done.value:
+            d_upper._srnn_colsum = (colsum, d_upper._version, FS0)
+        return (None, None, d_upper) + tuple(grads)
 
 
 class Runner:

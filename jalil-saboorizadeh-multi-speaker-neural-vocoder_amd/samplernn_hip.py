@@ -42,6 +42,8 @@ _SIGS = {
                           _P, _L, _P, _P],
     'srnn_mlp_l1': [_I, _P, _P, _L, _I, _I, _I, _I, _P, _L, _P, _L, _I, _I, _I, _P],
     'srnn_mlp_dtab': [_I, _P, _L, _P, _L, _I, _I, _I, _P, _I, _I, _I, _I, _P, _SZ, _P],
+    'srnn_mlp_dtab2': [_I, _P, _L, _P, _L, _I, _I, _I, _P, _I, _I, _I, _I, _P, _SZ, _P,
+                       ctypes.POINTER(_I), _P],
     'srnn_logsoftmax_nll': [_P, _L, _P, _L, _I, _L, _I, _P, _P, _L, _P, _I, _L, _F, _P],
     'srnn_logsoftmax_bwd': [_P, _L, _P, _L, _L, _I, _P, _I, _L, _P],
     'srnn_nll_fwd': [_P, _L, _P, _L, _I, _L, _P, _P],

@@ -537,6 +537,77 @@ def test_mlp_dtab_scatter(hip, dtype, B, Tl, D, FS0, Q):
     torch.testing.assert_close(outs[0].double(), ref, atol=1e-9 + 1e-12 * B * Tl, rtol=1e-6)
 
 
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('B,Tl,D', [(5, 64, 1024), (128, 1024, 1024), (3, 37, 72), (2, 100, 768)])
+def test_mlp_dtab2_colsum(hip, dtype, B, Tl, D):
+    """srnn_mlp_dtab2: the same dTab as srnn_mlp_dtab, plus (direct path, D >= 768) the
+    residue column sums colsum[j * D + c] = sum_{b, t = j mod 16} da[b, t, c]."""
+    import ctypes
+    FS0, Q = 16, 256
+    g = torch.Generator().manual_seed(B + Tl + D)
+    x = torch.randint(0, Q, (B, Tl + FS0 - 1), generator=g).to(DEV)
+    da = (torch.randn(B * Tl, D, generator=g) * 1e-3).to(DEV, dtype)
+    work = torch.empty(Q * FS0 * D, device=DEV, dtype=torch.int64)
+    ref_tab = torch.empty(Q, FS0, D, device=DEV)
+    hip.lib().call('srnn_mlp_dtab', hip.dcode(dtype), hip.ptr(da), D, hip.ptr(x), x.shape[1], 0, B,
+                   Tl, hip.ptr(ref_tab), hip.F32, D, FS0, Q, hip.ptr(work), work.numel() * 8,
+                   hip.stream())
+    tab = torch.empty(Q, FS0, D, device=DEV)
+    colsum = torch.full((FS0 * D,), float('nan'), device=DEV)
+    done = ctypes.c_int(-1)
+    hip.lib().call('srnn_mlp_dtab2', hip.dcode(dtype), hip.ptr(da), D, hip.ptr(x), x.shape[1], 0,
+                   B, Tl, hip.ptr(tab), hip.F32, D, FS0, Q, hip.ptr(work), work.numel() * 8,
+                   hip.ptr(colsum), ctypes.byref(done), hip.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(tab, ref_tab)
+    assert done.value == (1 if D >= 768 else 0)
+    if done.value:
+        ref = da.double().reshape(B, Tl, D)
+        pad = (-Tl) % FS0
+        ref = torch.cat([ref, ref.new_zeros(B, pad, D)], 1).reshape(B, -1, FS0, D).sum((0, 1))
+        torch.testing.assert_close(colsum.double().reshape(FS0, D), ref, atol=1e-9, rtol=1e-6)
+
+
+def test_fused_upsampling_bias_grad_in_step(hip):
+    """A bf16 TBPTT step at D = 1024 takes the bottom tier's upsampling bias gradient from the
+    MLP's dTab pass (no separate column sum), and it equals the column sum of d(upper)."""
+    import model as M
+    import nn as snn
+    torch.manual_seed(3)
+    m = M.SampleRNN([16, 4], 1, 1024, True, 256, True, False, 43, 6)
+    m.compute_dtype = torch.bfloat16
+    pred = M.Predictor(m).to(DEV)
+    B, T, L = 2, 128, 64
+    g = torch.Generator().manual_seed(4)
+    inp = torch.randint(0, 256, (B, L + T - 1), generator=g).to(DEV)
+    tgt = torch.randint(0, 256, (B, T), generator=g).to(DEV)
+    cond = torch.rand(B, T // L, 43, generator=g).to(DEV)
+    spk = torch.tensor([[1], [4]], device=DEV)
+    before = M._STATS['fused_colsum']
+    lp = pred(inp, True, cond, spk)
+    snn.sequence_nll_loss_bits(lp, tgt).backward()
+    assert M._STATS['fused_colsum'] == before + 1
+    bot = m.frame_level_rnns[0]
+    grad_fused = bot.upsampling.bias.grad.clone()
+    # same step with the column sum computed by the tier (attribute stripped by a clone)
+    for p in pred.parameters():
+        p.grad = None
+    pred.reset_hidden_states()
+    lp = pred(inp, True, cond, spk)
+    loss = snn.sequence_nll_loss_bits(lp, tgt)
+    orig = M._MlpFn.backward
+
+    def strip(ctx, dlogp):
+        out = orig(ctx, dlogp)
+        return out[:2] + (out[2].clone(),) + out[3:]
+    M._MlpFn.backward = staticmethod(strip)
+    try:
+        loss.backward()
+    finally:
+        M._MlpFn.backward = staticmethod(orig)
+    torch.testing.assert_close(bot.upsampling.bias.grad, grad_fused, atol=1e-7, rtol=1e-5)
+
+
 @pytest.mark.parametrize('perm', [(0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1),
                                   (2, 1, 0)])
 @pytest.mark.parametrize('shape', [(3, 37, 70), (16, 64, 33), (1, 1, 5)])
