@@ -191,43 +191,85 @@ __device__ __forceinline__ float block_sum(float v, float* sh) {
     return t;
 }
 
-__global__ void wn_fwd_kernel(const float* __restrict__ g, const float* __restrict__ v,
-                              float* __restrict__ w, float* __restrict__ norm, int64_t R) {
+// Every weight-norm kernel walks a row of R floats in the same per-thread order -- float4
+// chunks c = tid, tid + 256, ... (elements 4c .. 4c + 3) when the row is 16-B aligned and
+// R % 4 == 0, else single elements r = tid, tid + 256, ... -- four chunks loaded ahead, and
+// reduces with block_sum: the fused conv_t kernels below reproduce wn_fwd / wn_bwd bit for bit.
+__device__ __forceinline__ bool wn_vec(const float* row, int64_t R) {
+    return R % 4 == 0 && (uintptr_t)row % 16 == 0;
+}
+
+// f(r, v[r]) for r of this thread, in the common order
+template <typename F>
+__device__ __forceinline__ void wn_walk(const float* __restrict__ row, int64_t R, bool vec, F f) {
+    const int tid = threadIdx.x;
+    if (vec) {
+        const int64_t R4 = R / 4;
+        const floatx4* r4 = reinterpret_cast<const floatx4*>(row);
+        int64_t c = tid;
+        for (; c + 768 < R4; c += 1024) {
+            floatx4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = r4[c + 256 * u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) f(4 * (c + 256 * u) + e, x[u][e]);
+        }
+        for (; c < R4; c += 256) {
+            const floatx4 x = r4[c];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) f(4 * c + e, x[e]);
+        }
+    } else {
+        for (int64_t r = tid; r < R; r += 256) f(r, row[r]);
+    }
+}
+
+__global__ __launch_bounds__(256) void wn_fwd_kernel(const float* __restrict__ g,
+                                                     const float* __restrict__ v,
+                                                     float* __restrict__ w,
+                                                     float* __restrict__ norm, int64_t R) {
     __shared__ float sh[16];
     const int64_t o = blockIdx.x;
     const float* vr = v + o * R;
+    const bool vec = wn_vec(vr, R) && (uintptr_t)w % 16 == 0;
     float s = 0.f;
-    for (int64_t r = threadIdx.x; r < R; r += blockDim.x) s += vr[r] * vr[r];
+    wn_walk(vr, R, vec, [&](int64_t, float x) { s += x * x; });
     s = block_sum(s, sh);
     const float nrm = sqrtf(s);
     const float scale = g[o] / nrm;
     if (norm && threadIdx.x == 0) norm[o] = nrm;
-    for (int64_t r = threadIdx.x; r < R; r += blockDim.x) w[o * R + r] = vr[r] * scale;
+    wn_walk(vr, R, vec, [&](int64_t r, float x) { w[o * R + r] = x * scale; });
 }
 
 // dg[o] = sum_r dw v / n ;  dv = (g/n) (dw - (dg/n) v)
-__global__ void wn_bwd_kernel(const float* __restrict__ g, const float* __restrict__ v,
-                              const float* __restrict__ dw, float* __restrict__ dg,
-                              float* __restrict__ dv, int64_t R, int accumulate) {
+__global__ __launch_bounds__(256) void wn_bwd_kernel(const float* __restrict__ g,
+                                                     const float* __restrict__ v,
+                                                     const float* __restrict__ dw,
+                                                     float* __restrict__ dg,
+                                                     float* __restrict__ dv, int64_t R,
+                                                     int accumulate) {
     __shared__ float sh[16];
     const int64_t o = blockIdx.x;
     const float* vr = v + o * R;
     const float* dr = dw + o * R;
+    const bool vec = wn_vec(vr, R);
     float s = 0.f, d = 0.f;
-    for (int64_t r = threadIdx.x; r < R; r += blockDim.x) {
-        s += vr[r] * vr[r];
-        d += dr[r] * vr[r];
-    }
+    wn_walk(vr, R, vec, [&](int64_t r, float x) {
+        s += x * x;
+        d += dr[r] * x;
+    });
     s = block_sum(s, sh);
     d = block_sum(d, sh);
     const float n = sqrtf(s);
     const float dgo = d / n;
     const float gn = g[o] / n;
     if (threadIdx.x == 0) dg[o] = accumulate ? dg[o] + dgo : dgo;
-    for (int64_t r = threadIdx.x; r < R; r += blockDim.x) {
-        float val = gn * (dr[r] - dgo / n * vr[r]);
+    wn_walk(vr, R, vec, [&](int64_t r, float x) {
+        const float val = gn * (dr[r] - dgo / n * x);
         dv[o * R + r] = accumulate ? dv[o * R + r] + val : val;
-    }
+    });
 }
 
 extern "C" int srnn_weight_norm_fwd(const float* g, const float* v, float* w, float* norm, int O,
@@ -255,13 +297,14 @@ extern "C" int srnn_weight_norm_bwd(const float* g, const float* v, const float*
 // block per channel computes dg and dv in v's own layout (srnn_convt_wn_bwd): the same
 // per-thread element order and block reduction as wn_bwd_kernel, so the results are the
 // ones weight_norm_bwd would give for the permuted gradient.
-__global__ void wn_scale_kernel(const float* __restrict__ g, const float* __restrict__ v,
-                                float* __restrict__ scale, int64_t R) {
+__global__ __launch_bounds__(256) void wn_scale_kernel(const float* __restrict__ g,
+                                                       const float* __restrict__ v,
+                                                       float* __restrict__ scale, int64_t R) {
     __shared__ float sh[16];
     const int64_t o = blockIdx.x;
     const float* vr = v + o * R;
     float s = 0.f;
-    for (int64_t r = threadIdx.x; r < R; r += blockDim.x) s += vr[r] * vr[r];
+    wn_walk(vr, R, wn_vec(vr, R), [&](int64_t, float x) { s += x * x; });
     s = block_sum(s, sh);
     if (threadIdx.x == 0) scale[o] = g[o] / sqrtf(s);
 }
@@ -358,23 +401,23 @@ __global__ __launch_bounds__(256) void convt_wn_bwd_kernel(const float* __restri
     }
     __syncthreads();
     const float* vr = v + i * R;
-    float s = 0.f, d = 0.f;
-    for (int64_t r = threadIdx.x; r < R; r += 256) {
+    const bool vec = wn_vec(vr, R);
+    auto dw_at = [&](int64_t r) {
         const int o = (int)(r / k), j = (int)(r - (int64_t)o * k);
-        const float vv = vr[r];
-        s += vv * vv;
-        d += dl[j * pitch + o] * vv;
-    }
+        return dl[j * pitch + o];
+    };
+    float s = 0.f, d = 0.f;
+    wn_walk(vr, R, vec, [&](int64_t r, float x) {
+        s += x * x;
+        d += dw_at(r) * x;
+    });
     s = block_sum(s, sh);
     d = block_sum(d, sh);
     const float n = sqrtf(s);
     const float dgo = d / n;
     const float gn = (HAS_G ? g[i] : 1.f) / n;
     if (threadIdx.x == 0) dg[i] = dgo;
-    for (int64_t r = threadIdx.x; r < R; r += 256) {
-        const int o = (int)(r / k), j = (int)(r - (int64_t)o * k);
-        dv[i * R + r] = gn * (dl[j * pitch + o] - dgo / n * vr[r]);
-    }
+    wn_walk(vr, R, vec, [&](int64_t r, float x) { dv[i * R + r] = gn * (dw_at(r) - dgo / n * x); });
 }
 
 extern "C" int srnn_convt_wn_bwd(const float* g, const float* v, const float* dwt, float* dg,
