@@ -274,8 +274,18 @@ __global__ __launch_bounds__(256) void g3_splitk_sum_kernel(const float* __restr
     if (q * 4 >= MN) return;
     const int64_t e = q * 4;
     const int m = (int)(e / N), n = (int)(e % N);
-    floatx4 s = *reinterpret_cast<const floatx4*>(part + e);
-    for (int z = 1; z < ks; ++z) s += *reinterpret_cast<const floatx4*>(part + z * MN + e);
+    const floatx4* p = reinterpret_cast<const floatx4*>(part + e);
+    const int64_t zs = MN / 4;
+    floatx4 s = p[0];
+    int z = 1;
+    for (; z + 4 <= ks; z += 4) {            // 4 slices in flight, summed in z order
+        floatx4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = p[(z + u) * zs];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; z < ks; ++z) s += p[z * zs];
     *reinterpret_cast<floatx4*>(C + (int64_t)m * ldc + n) = s;
 }
 

@@ -207,8 +207,18 @@ __global__ __launch_bounds__(256) void gemm_small_nt_sum_kernel(const float* __r
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (int64_t)M * N) return;
     const int n = (int)(i / M), m = (int)(i % M);
+    const int64_t zs = (int64_t)N * M;
+    const float* p = P + (int64_t)n * M + m;
     float s = 0.f;
-    for (int z = 0; z < nks; ++z) s += P[((int64_t)z * N + n) * M + m];
+    int z = 0;
+    for (; z + 8 <= nks; z += 8) {          // 8 loads in flight, summed in z order
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = p[(z + u) * zs];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; z < nks; ++z) s += p[z * zs];
     C[(int64_t)m * ldc + n] = alpha * s;
 }
 

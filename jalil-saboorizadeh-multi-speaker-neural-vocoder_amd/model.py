@@ -205,9 +205,14 @@ class _TierFn(torch.autograd.Function):
         ie_b = next(it)
         W_ie = H.cast(nn.weight_of(mod.input_expand).reshape(D, nfs), T)
         prevT = H.cast(prev.reshape(B * Fr, nfs), T)
+        lp = T != torch.float32
+        # In the low-precision mode only the compute-dtype copy of the first GRU layer's input
+        # is ever read, so the last projection writes it directly (no fp32 x0, no cast); the
+        # fp32 (parity) mode keeps the reference's summation order.
         x0 = H.linear(prevT, W_ie, bias=ie_b,
                       cin=None if upper is None else upper.reshape(B * Fr, D),
-                      beta=0.0 if upper is None else 1.0)
+                      beta=0.0 if upper is None else 1.0,
+                      out_dtype=T if lp and not mod.is_cond else torch.float32)
         condT = spk_embT = W_c = W_s = None
         if mod.is_cond:
             take_w(mod.cond_expand)
@@ -218,7 +223,6 @@ class _TierFn(torch.autograd.Function):
             C = cond.shape[-1]
             W_c = H.cast(nn.weight_of(mod.cond_expand).reshape(D, C), T)
             condT = H.cast(cond.reshape(B * Fr, C).float().contiguous(), T)
-            H.linear(condT, W_c, bias=c_b, cin=x0, beta=1.0, out=x0)
             S = E_s.shape[1]
             spk_flat = spk.reshape(B).contiguous()
             spk_emb = torch.empty((B, S), device=dev, dtype=torch.float32)
@@ -227,8 +231,14 @@ class _TierFn(torch.autograd.Function):
             spk_embT = H.cast(spk_emb, T)
             W_s = H.cast(nn.weight_of(mod.spk_expand).reshape(D, S), T)
             spk_proj = H.linear(spk_embT, W_s, bias=s_b)
-            H.lib().call('srnn_add_bcast_rows', H.ptr(x0), H.ptr(spk_proj), B, Fr, D, D,
-                         H.stream())
+            if lp:
+                H.lib().call('srnn_add_bcast_rows', H.ptr(x0), H.ptr(spk_proj), B, Fr, D, D,
+                             H.stream())
+                x0 = H.linear(condT, W_c, bias=c_b, cin=x0, beta=1.0, out_dtype=T)
+            else:
+                H.linear(condT, W_c, bias=c_b, cin=x0, beta=1.0, out=x0)
+                H.lib().call('srnn_add_bcast_rows', H.ptr(x0), H.ptr(spk_proj), B, Fr, D, D,
+                             H.stream())
         else:
             spk_flat = None
         reset = hidden is None
@@ -236,7 +246,6 @@ class _TierFn(torch.autograd.Function):
             h_in = h0.detach().reshape(L, 1, D).expand(L, B, D).contiguous()
         else:
             h_in = hidden.float().contiguous()
-        lp = T != torch.float32
         Wih, Whh, bih, bhh = [], [], [], []
         xs, outs, outsT, gates = [], [], [], []
         X = x0
