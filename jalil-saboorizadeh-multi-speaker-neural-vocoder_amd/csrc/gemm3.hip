@@ -221,6 +221,52 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
                     mk[i][j] = *reinterpret_cast<const u16x4*>(
                         mask + (int64_t)(rbase + (4 * h + i) * 16) * g.ldmask + cbase + j * 16);
         }
+        if constexpr (sizeof(TO) == 2 && !CIN) {
+            // bf16 out: fragments j, j + 1 of a row combined by two v_permlane16_swap per
+            // pair, so every lane stores 16 B (8 columns) -- half the store instructions of
+            // the 8-B-per-fragment form (the epilogue tail is store-issue-bound)
+            const int grp = lane >> 4;
+            const int coff = 16 * (grp & 1) + 8 * (grp >> 1) - 4 * grp;   // lane's 16-B column
+#pragma unroll
+            for (int ii = 0; ii < 4; ++ii) {
+                const int i = 4 * h + ii;
+                const int row = rbase + i * 16;
+#pragma unroll
+                for (int jp = 0; jp < 2; ++jp) {
+                    unsigned pk[2][2];
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const int j = 2 * jp + t;
+                        float v[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) v[e] = g.alpha * acc[i][j][e] + bcol[j][e] + brow[i];
+                        acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+                        if (g.relu) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+                        }
+                        if (mask) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                v[e] = __uint_as_float((unsigned)mk[ii][j][e] << 16) > 0.f ? v[e] : 0.f;
+                        }
+#pragma unroll
+                        for (int e = 0; e < 2; ++e)
+                            pk[t][e] = (unsigned)__bfloat16_as_ushort(__float2bfloat16(v[2 * e])) |
+                                       ((unsigned)__bfloat16_as_ushort(__float2bfloat16(v[2 * e + 1])) << 16);
+                    }
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const auto r = __builtin_amdgcn_permlane16_swap(pk[0][e], pk[1][e], false, false);
+                        pk[0][e] = r[0];
+                        pk[1][e] = r[1];
+                    }
+                    *reinterpret_cast<uint4*>(Cp + (int64_t)row * g.ldc + cbase + 32 * jp + coff) =
+                        make_uint4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
+                }
+            }
+            continue;
+        }
 #pragma unroll
         for (int ii = 0; ii < 4; ++ii) {
             const int i = 4 * h + ii;

@@ -859,26 +859,55 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
     float* __restrict__ V = a.v[t];
     bf16* __restrict__ PL = a.plp[t];
     const int64_t j0 = (int64_t)(blockIdx.x - a.boff[t]) * CH;
-    for (int i = threadIdx.x; i < CH; i += 256) {
-        const int64_t j = j0 + i;
-        if (j >= n) return;
-        // (a null gradient is an all-zero one: a parameter backward did not reach this
-        //  step, e.g. the learned h0 on a carried chunk -- torch-0.4 zero_grad semantics)
-        float gi = 0.f;
-        if (G) {
-            gi = fminf(fmaxf(G[j], lo), hi);
-            G[j] = gi;
+    // (a null gradient is an all-zero one: a parameter backward did not reach this
+    //  step, e.g. the learned h0 on a carried chunk -- torch-0.4 zero_grad semantics)
+    auto upd = [&](float g, float& p, float& m, float& v) {
+        const float gi = fminf(fmaxf(g, lo), hi);
+        m = m + w1 * (gi - m);
+        v = v * b2;
+        v = v + omb2 * gi * gi;
+        const float denom = sqrtf(v) / bc2s + eps;
+        p = p + (-step_size) * m / denom;
+        return gi;
+    };
+    // two 4-element chunks per thread (16-B accesses; every tensor is its own allocation,
+    // so chunk starts are 16-B aligned); the ragged end element by element
+#pragma unroll
+    for (int c = 0; c < CH / 1024; ++c) {
+        const int64_t j = j0 + c * 1024 + 4 * threadIdx.x;
+        if (j + 4 <= n) {
+            floatx4 g4 = G ? *reinterpret_cast<const floatx4*>(G + j) : floatx4{0.f, 0.f, 0.f, 0.f};
+            floatx4 p4 = *reinterpret_cast<const floatx4*>(P + j);
+            floatx4 m4 = *reinterpret_cast<const floatx4*>(Mm + j);
+            floatx4 v4 = *reinterpret_cast<const floatx4*>(V + j);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float pe = p4[e], me = m4[e], ve = v4[e];
+                g4[e] = upd(g4[e], pe, me, ve);
+                p4[e] = pe; m4[e] = me; v4[e] = ve;
+            }
+            if (G) *reinterpret_cast<floatx4*>(G + j) = g4;
+            *reinterpret_cast<floatx4*>(Mm + j) = m4;
+            *reinterpret_cast<floatx4*>(V + j) = v4;
+            *reinterpret_cast<floatx4*>(P + j) = p4;
+            if (PL) {
+                const unsigned lo2 = (unsigned)__bfloat16_as_ushort(__float2bfloat16(p4[0])) |
+                                     ((unsigned)__bfloat16_as_ushort(__float2bfloat16(p4[1])) << 16);
+                const unsigned hi2 = (unsigned)__bfloat16_as_ushort(__float2bfloat16(p4[2])) |
+                                     ((unsigned)__bfloat16_as_ushort(__float2bfloat16(p4[3])) << 16);
+                *reinterpret_cast<uint2*>(PL + j) = make_uint2(lo2, hi2);
+            }
+        } else {
+            for (int64_t k = j; k < n && k < j + 4; ++k) {
+                float pe = P[k], me = Mm[k], ve = V[k];
+                const float gi = upd(G ? G[k] : 0.f, pe, me, ve);
+                if (G) G[k] = gi;
+                Mm[k] = me;
+                V[k] = ve;
+                P[k] = pe;
+                if (PL) PL[k] = __float2bfloat16(pe);
+            }
         }
-        float mi = Mm[j];
-        mi = mi + w1 * (gi - mi);
-        float vi = V[j] * b2;
-        vi = vi + omb2 * gi * gi;
-        const float denom = sqrtf(vi) / bc2s + eps;
-        const float pi = P[j] + (-step_size) * mi / denom;
-        Mm[j] = mi;
-        V[j] = vi;
-        P[j] = pi;
-        if (PL) PL[j] = __float2bfloat16(pi);
     }
 }
 

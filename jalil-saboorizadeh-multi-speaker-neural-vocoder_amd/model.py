@@ -182,6 +182,14 @@ class FrameLevelRNN(torch.nn.Module):
         return out, h
 
 
+def _wcast(mod, T):
+    """Effective weight of a conv module in the compute dtype: the cached copy of the plain
+    parameter (samplernn_hip.cast_param), or a cast of the weight-normed weight."""
+    if hasattr(mod, 'weight_g'):
+        return H.cast(nn.weight_of(mod), T)
+    return H.cast_param(mod.weight, T)
+
+
 def _dt(mod):
     root = mod.__dict__.get('_root')
     return root.compute_dtype if root is not None else torch.float32
@@ -203,7 +211,7 @@ class _TierFn(torch.autograd.Function):
 
         ie_p = take_w(mod.input_expand)
         ie_b = next(it)
-        W_ie = H.cast(nn.weight_of(mod.input_expand).reshape(D, nfs), T)
+        W_ie = _wcast(mod.input_expand, T).reshape(D, nfs)
         prevT = H.cast(prev.reshape(B * Fr, nfs), T)
         lp = T != torch.float32
         # In the low-precision mode only the compute-dtype copy of the first GRU layer's input
@@ -221,7 +229,7 @@ class _TierFn(torch.autograd.Function):
             take_w(mod.spk_expand)
             s_b = next(it)
             C = cond.shape[-1]
-            W_c = H.cast(nn.weight_of(mod.cond_expand).reshape(D, C), T)
+            W_c = _wcast(mod.cond_expand, T).reshape(D, C)
             condT = H.cast(cond.reshape(B * Fr, C).float().contiguous(), T)
             S = E_s.shape[1]
             spk_flat = spk.reshape(B).contiguous()
@@ -229,7 +237,7 @@ class _TierFn(torch.autograd.Function):
             H.lib().call('srnn_gather_rows', H.ptr(E_s), S, H.ptr(spk_flat), B, S, H.ptr(spk_emb),
                          H.F32, S, H.stream())
             spk_embT = H.cast(spk_emb, T)
-            W_s = H.cast(nn.weight_of(mod.spk_expand).reshape(D, S), T)
+            W_s = _wcast(mod.spk_expand, T).reshape(D, S)
             spk_proj = H.linear(spk_embT, W_s, bias=s_b)
             if lp:
                 H.lib().call('srnn_add_bcast_rows', H.ptr(x0), H.ptr(spk_proj), B, Fr, D, D,
@@ -251,8 +259,8 @@ class _TierFn(torch.autograd.Function):
         X = x0
         for l in range(L):
             wih, whh, b_ih, b_hh = next(it), next(it), next(it), next(it)
-            Wih.append(H.cast(wih, T))
-            Whh.append(H.cast(whh, T))
+            Wih.append(H.cast_param(wih, T))
+            Whh.append(H.cast_param(whh, T))
             bih.append(b_ih)
             bhh.append(b_hh)
             XT = H.cast(X, T)
@@ -509,7 +517,7 @@ def _build_tab(mlp, T):
     Q, D, FS0 = mlp.q_levels, mlp.dim, mlp.frame_size
     W_in = nn.weight_of(mlp.input)                                       # (D, Q, FS0)
     Wp = H.permute3(W_in, (2, 0, 1), dtype=T)                            # (FS0, D, Q)
-    ET = H.cast(mlp.embedding.weight, T)
+    ET = H.cast_param(mlp.embedding.weight, T)
     tab = torch.empty((FS0, Q, D), device=ET.device, dtype=T)
     H.gemm(ET, Wp, transB=True, out=tab, M=Q, N=D, K=Q, lda=Q, ldb=Q, ldc=D, batch=FS0, sA=0,
            sB=D * Q, sC=Q * D)
@@ -529,8 +537,8 @@ class _MlpFn(torch.autograd.Function):
         upper = upper.contiguous()
         H.lib().call('srnn_mlp_l1', H.dcode(T), H.ptr(tab), H.ptr(x), x.shape[1], 0, B, Tl,
                      H.dcode(upper), H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
-        W_hid = H.cast(nn.weight_of(mlp.hidden).reshape(D, D), T)
-        W_out = H.cast(nn.weight_of(mlp.output).reshape(Q, D), T)
+        W_hid = _wcast(mlp.hidden, T).reshape(D, D)
+        W_out = _wcast(mlp.output, T).reshape(Q, D)
         a2 = H.linear(a1, W_hid, bias=mlp.hidden.bias, relu=True, out_dtype=T)
         z = H.linear(a2, W_out, bias=mlp.output.bias)                    # (B*T, Q) fp32
         logp = torch.empty((B * Tl, Q), device=dev, dtype=torch.float32)

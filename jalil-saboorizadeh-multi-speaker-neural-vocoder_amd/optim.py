@@ -45,9 +45,13 @@ def _fused_adam_step(optimizer, lo, hi):
             n = len(items)
             arr = lambda ts: (ctypes.c_void_p * n)(  # noqa: E731
                 *[t.data_ptr() if t is not None else None for t in ts])
+            # parameters with a cached bf16 copy (samplernn_hip.cast_param) get it rewritten
+            # by the same kernel, so the next forward needs no cast
+            shadows = [H.shadow_of(p) for p, _ in items]
             H.lib().call('srnn_adam_clip_multi', n, arr([p for p, _ in items]),
                          arr([p.grad for p, _ in items]), arr([s['exp_avg'] for _, s in items]),
-                         arr([s['exp_avg_sq'] for _, s in items]), None,
+                         arr([s['exp_avg_sq'] for _, s in items]),
+                         arr(shadows) if any(t is not None for t in shadows) else None,
                          (ctypes.c_int64 * n)(*[p.numel() for p, _ in items]), float(lo),
                          float(hi), float(group['lr']), float(b1), float(b2),
                          float(group['eps']), step, H.stream())

@@ -350,6 +350,39 @@ def cast(x, dtype):
     return out
 
 
+# Compute-dtype (bf16) copies of parameters, kept across steps: id(param) -> (weakref, copy,
+# data_ptr, _version).  A copy is valid while the parameter's storage and version are
+# unchanged; torch in-place updates (load_state_dict, manual edits) bump the version, and the
+# fused clip+Adam (optim.py), which writes the parameter through a raw pointer, rewrites the
+# copy in the same kernel (srnn_adam_clip_multi's p_bf16), so the copy stays valid.
+_SHADOW = {}
+
+
+def cast_param(p, dtype):
+    """`p` (an fp32 parameter) in `dtype`: the cached copy when still valid, else a fresh cast
+    that becomes the cached copy."""
+    if p.dtype == dtype:
+        return p
+    import weakref
+    key = id(p)
+    e = _SHADOW.get(key)
+    if e is not None and e[0]() is p and e[1].dtype == dtype and e[2] == p.data_ptr() and \
+            e[3] == p._version:
+        return e[1]
+    c = cast(p.detach(), dtype)
+    _SHADOW[key] = (weakref.ref(p), c, p.data_ptr(), p._version)
+    return c
+
+
+def shadow_of(p):
+    """The valid bf16 copy of parameter p, or None (the fused Adam step refreshes it)."""
+    e = _SHADOW.get(id(p))
+    if e is not None and e[0]() is p and e[2] == p.data_ptr() and e[3] == p._version and \
+            e[1].dtype == torch.bfloat16:
+        return e[1]
+    return None
+
+
 def permute3(src, perm, dtype=torch.float32, out=None, accumulate=False):
     """out = src.permute(perm).contiguous() (src fp32, 3-D) via the HIP permute kernel."""
     need_cuda(src)

@@ -858,3 +858,46 @@ def test_gru_xcd_bwd2_lowp_outputs(hip, B, D, Fr):
     torch.testing.assert_close(ddir_b, ddir_a, atol=0, rtol=0)
     ref = torch.cat([dgh.sum(1), dgi[..., 2 * D:].sum(1)], 1)
     torch.testing.assert_close(bsum, ref, atol=1e-5 * ref.abs().max().item(), rtol=1e-5)
+
+
+def test_bf16_parameter_copies_follow_adam(hip):
+    """The cached bf16 parameter copies (samplernn_hip.cast_param) stay equal to a fresh cast
+    of the fp32 parameters across fused clip+Adam steps (the Adam kernel rewrites them), and
+    a torch in-place edit of a parameter invalidates its copy."""
+    import model as M
+    import nn as snn
+    import optim
+    torch.manual_seed(5)
+    m = M.SampleRNN([16, 4], 1, 256, True, 256, True, False, 43, 6)
+    m.compute_dtype = torch.bfloat16
+    pred = M.Predictor(m).to(DEV)
+    opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3))
+    B, T, L = 2, 128, 64
+    g = torch.Generator().manual_seed(6)
+    for step in range(3):
+        inp = torch.randint(0, 256, (B, L + T - 1), generator=g).to(DEV)
+        tgt = torch.randint(0, 256, (B, T), generator=g).to(DEV)
+        cond = torch.rand(B, T // L, 43, generator=g).to(DEV)
+        spk = torch.tensor([[1], [4]], device=DEV)
+        opt.zero_grad()
+
+        def closure():
+            loss = snn.sequence_nll_loss_bits(pred(inp, step == 0, cond, spk), tgt)
+            loss.backward()
+            return loss
+        opt.step(closure)
+    torch.cuda.synchronize()
+    n = 0
+    for p in pred.parameters():
+        c = hip.shadow_of(p)
+        if c is not None:
+            n += 1
+            torch.testing.assert_close(c, p.detach().to(torch.bfloat16), atol=0, rtol=0)
+    assert n >= 6
+    w = m.sample_level_mlp.hidden.weight
+    assert hip.shadow_of(w) is not None
+    with torch.no_grad():
+        w.mul_(0.5)
+    assert hip.shadow_of(w) is None
+    torch.testing.assert_close(hip.cast_param(w, torch.bfloat16), w.detach().to(torch.bfloat16),
+                               atol=0, rtol=0)
