@@ -304,11 +304,18 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 // The Cin branch is resolved once per tile: a uniform branch inside the store loop makes
 // the compiler join its wait states with an s_waitcnt vmcnt(0) per fragment, which waits
 // for every store issued before it (32 serialised store round trips per tile).
+// Returns the number of stores each wave issued (SW path): the main loops' counted DMA
+// waits leave exactly that many younger stores in flight, so the count must be exact -- a
+// larger allowance would let a stage's DMA pieces still be outstanding at the read.
 template <typename TO, bool SW>
-__device__ __forceinline__ void g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
-                                            int n0, int wm, int wn, int lane, int kb) {
-    if (SW && g.beta != 0.f) g3_epilogue_t<TO, SW, true>(g, acc, m0, n0, wm, wn, lane, kb);
-    else g3_epilogue_t<TO, SW, false>(g, acc, m0, n0, wm, wn, lane, kb);
+__device__ __forceinline__ int g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
+                                           int n0, int wm, int wn, int lane, int kb) {
+    if (SW && g.beta != 0.f) {
+        g3_epilogue_t<TO, SW, true>(g, acc, m0, n0, wm, wn, lane, kb);
+        return 32;
+    }
+    g3_epilogue_t<TO, SW, false>(g, acc, m0, n0, wm, wn, lane, kb);
+    return sizeof(TO) == 2 ? 16 : 32;
 }
 
 // C[m][n] = sum_z part[z][m][n], z in order (4 columns per thread)
@@ -433,15 +440,14 @@ __global__ __launch_bounds__(512, 1) void gemm3_kernel(Gemm3Args g) {
     };
     // compute cursor: unit ic, stage ktc
     int ic = 0, ktc = 0;
-    bool epi = false;
+    int epi = 0;                               // stores of the just-finished tile's epilogue
     auto finish_stage = [&]() {
         if (++ktc == nk) {
             int m0, n0, kb;
             unit(ic, m0, n0, kb);
-            g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
+            epi = g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
             ktc = 0;
             ++ic;
-            epi = true;
         }
     };
     // Steady state: every stage issues the DMA pieces of stage s+NS-1 into the slot freed
@@ -452,9 +458,10 @@ __global__ __launch_bounds__(512, 1) void gemm3_kernel(Gemm3Args g) {
     for (; s + g3::NS - 1 < S; ++s) {
         // the 32 epilogue stores of a just-finished tile are younger than the pieces
         // waited for here: leave them in flight
-        if (SW && epi) g3_wait_vm<(g3::NS - 2) * PER + 32>();
+        if (SW && epi == 16) g3_wait_vm<(g3::NS - 2) * PER + 16>();
+        else if (SW && epi) g3_wait_vm<(g3::NS - 2) * PER + 32>();
         else g3_wait_vm<(g3::NS - 2) * PER>();
-        epi = false;
+        epi = 0;
         __builtin_amdgcn_s_barrier();
         char* img = smem + ws * g3::SLOT;
         next_ws();
@@ -615,7 +622,7 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
 
     bf16x8 a[8], b[4];
     int ic = 0, ktc = 0;
-    bool epi = false;
+    int epi = 0;                               // stores of the just-finished tile's epilogue
     auto read_unit = [&](const char* img, int u) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) b[j] = g3p_frag<KCB>(img + g3p::OPB, wn * 64 + j * 16, u, lane);
@@ -632,10 +639,9 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
         if (++ktc == nk) {
             int m0, n0, kb;
             unit(ic, m0, n0, kb);
-            if (!(g.diag & 8)) g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
+            epi = (g.diag & 8) ? 0 : g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
             ktc = 0;
             ++ic;
-            epi = true;
         }
     };
     // Stage s+1 is issued right after the barrier that opens stage s, into the slot
@@ -644,9 +650,10 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     for (; s + 1 < S; ++s) {
         const char* img = smem + (s & 1) * g3p::SLOT;
         char* nimg = smem + ((s + 1) & 1) * g3p::SLOT;
-        if (SW && epi) g3_wait_vm<32>();
+        if (SW && epi == 16) g3_wait_vm<16>();
+        else if (SW && epi) g3_wait_vm<32>();
         else g3_wait_vm<0>();
-        epi = false;
+        epi = 0;
         __builtin_amdgcn_s_barrier();
         const int64_t oa = koffA(kti), ob = koffB(kti);
         const bf16* pa0 = srcA[0] + oa;
