@@ -152,7 +152,7 @@ def kernel_roofline_gemm(dev, M, N, K, dtype, reps=20):
     w = torch.randn(N, K, device=dev).to(dtype)
     bias = torch.zeros(N, device=dev)
     out = torch.empty(M, N, device=dev, dtype=dtype)
-    for _ in range(3):
+    for _ in range(10):
         H.linear(a, w, bias=bias, relu=True, out=out)
     s = torch.cuda.current_stream()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -165,7 +165,7 @@ def kernel_roofline_gemm(dev, M, N, K, dtype, reps=20):
     return ms
 
 
-def pmc_traffic(kernel, path=os.path.join(ROOT, 'profiles', 'r01_pmc_gemm.txt')):
+def pmc_traffic(kernel, path=os.path.join(ROOT, 'profiles', 'r02_pmc_gemm.txt')):
     """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
     (tools/roofline_kernel.py under --pmc FETCH_SIZE, then --pmc WRITE_SIZE): FETCH_SIZE kB x 2
     (gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md HBM section) + WRITE_SIZE kB."""
@@ -244,6 +244,21 @@ def main():
     del pred, m
     torch.cuda.empty_cache()
 
+    # dominant kernel of the TBPTT step (timed right after the step, before the generation legs): the MLP hidden layer GEMM (B*T x D x D, bf16)
+    tdt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+    M_, N_, K_ = rows * 1024, 1024, 1024
+    kms = kernel_roofline_gemm(dev, M_, N_, K_, tdt)
+    flops = 2.0 * M_ * N_ * K_
+    ach = flops / (kms * 1e-3) / 1e12
+    peak = MI355X_BF16_TFLOPS if args.dtype == 'bf16' else MI355X_FP32_TFLOPS
+    roof = {'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
+            'frac': round(ach / peak, 4),
+            'traffic': pmc_traffic('gemm3p_kernel') if (args.dtype == 'bf16' and rows == 128)
+            else None,
+            'traffic_algorithmic': 2 * (M_ * K_ + N_ * K_ + M_ * N_),
+            'kernel': 'gemm_kernel (MLP hidden layer %dx%dx%d %s, relu epilogue), %.3f ms/launch'
+                      % (M_, N_, K_, args.dtype, kms)}
+
     def gen_line(dname, frame_sizes=(16, 4), cond_dim=43, n_cond=None, tag='3-tier dim1024 '
                  'FS=[16,4]'):
         gdt = torch.bfloat16 if dname == 'bf16' else torch.float32
@@ -286,21 +301,6 @@ def main():
             # GPUs = 128 per GPU (replicas), 188 cond rows x 256 = 48,128 samples each
             gen_e = gen_line(args.gen_dtype, (16, 4, 4), 86, 188,
                              '4-tier dim1024 FS=[16,4,4] look-ahead')
-
-    # dominant kernel of the TBPTT step: the MLP hidden layer GEMM (B*T x D x D, bf16)
-    tdt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
-    M_, N_, K_ = rows * 1024, 1024, 1024
-    kms = kernel_roofline_gemm(dev, M_, N_, K_, tdt)
-    flops = 2.0 * M_ * N_ * K_
-    ach = flops / (kms * 1e-3) / 1e12
-    peak = MI355X_BF16_TFLOPS if args.dtype == 'bf16' else MI355X_FP32_TFLOPS
-    roof = {'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
-            'frac': round(ach / peak, 4),
-            'traffic': pmc_traffic('gemm3p_kernel') if (args.dtype == 'bf16' and rows == 128)
-            else None,
-            'traffic_algorithmic': 2 * (M_ * K_ + N_ * K_ + M_ * N_),
-            'kernel': 'gemm_kernel (MLP hidden layer %dx%dx%d %s, relu epilogue), %.3f ms/launch'
-                      % (M_, N_, K_, args.dtype, kms)}
 
     cpu = None
     if D.rank() == 0 and N == 1 and not args.no_cpu:
