@@ -56,6 +56,26 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __ex
 // exact-ish transcendental forms used where parity with torch CPU matters
 __device__ __forceinline__ float sigmoid_acc(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// ---- cross-lane moves without LDS ------------------------------------------------------
+// (__shfl* is a ds_bpermute: an LDS round trip of ~100+ cycles; these are VALU ops)
+template <int CTRL> __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xf, 0xf, true);
+}
+// value of lane + 1 within the lane's 16-lane row (DPP row_shl:1; 0 at a row's last lane)
+__device__ __forceinline__ uint32_t lane_next16(uint32_t v) { return dpp_u32<0x101>(v); }
+// pair exchange across lanes i, i ^ 16 (v_permlane16_swap) and i, i ^ 32 (v_permlane32_swap):
+// lo = the value of the pair's lower lane, hi = its upper lane's, in both lanes
+__device__ __forceinline__ void xpair16(uint32_t v, uint32_t& lo, uint32_t& hi) {
+    const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    lo = r[0];
+    hi = r[1];
+}
+__device__ __forceinline__ void xpair32(uint32_t v, uint32_t& lo, uint32_t& hi) {
+    const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    lo = r[0];
+    hi = r[1];
+}
+
 // ---- MFMA wrappers -------------------------------------------------------------------
 // One "k-unit" = 64 bytes of k per row: 16 fp32 (4 x v_mfma_f32_16x16x4_f32) or
 // 32 bf16 (1 x v_mfma_f32_16x16x32_bf16).  Each lane supplies the 16 bytes at offset

@@ -30,6 +30,7 @@
 // * Spins are bounded: a lost hand-off sets the error word and the loop runs out instead of
 //   hanging.
 #include <algorithm>
+#include <type_traits>
 
 #include "samplernn_hip_internal.hpp"
 #include "sampler.hpp"
@@ -43,6 +44,8 @@ constexpr int Q = 256;
 constexpr int HIST = 32;               // sample history ring per row (FS0 <= 32)
 }  // namespace gm
 
+
+#define GM_DIAG_WAVE0 (512 + 3 * 1024)
 
 template <typename T> struct GmT;
 template <> struct GmT<bf16> {
@@ -85,17 +88,19 @@ __device__ __forceinline__ uint32_t gm_bf16_bits(float v) {
 
 // A-operand fragments of one wave for one hand-off buffer (granules of row `row`, starting
 // at granule `rowg`): for unit j (global unit u = wave + NW*j) the lane's 16 data bytes are
-// 4 granules = two 16-B loads.  Spins until every tag == tag.
-template <typename T, int UPW>
+// 4 granules = two 16-B loads.  Spins until every tag == tag.  `work` (independent of the
+// hand-off) runs once between the first poll's issue and its check, so it fills the
+// hand-off's latency (the first check is straight-line code after it: its vmcnt leaves
+// work's own loads in flight).
+template <typename T, int UPW, typename W>
 __device__ __forceinline__ void gm_fetch_a(__amdgpu_buffer_rsrc_t src, uint32_t rowg, bool rv,
                                            int wave, int lane, int NU, int D, uint32_t tag,
-                                           uint32_t (&w)[UPW][4], int* err) {
+                                           uint32_t (&w)[UPW][4], int* err, W&& work) {
     constexpr int GV = GmT<T>::GV, UK = GmT<T>::UK, EPL = UK / 4;
-    int spins = 0;
-    for (;;) {
-        // every load unconditional (clamped k), so all 2 x UPW are in flight at once; a
-        // branch per unit would put a vmcnt(0) between them
-        uint4 x[UPW][2];
+    uint4 x[UPW][2];
+    // every load unconditional (clamped k), so all 2 x UPW are in flight at once; a branch
+    // per unit would put a vmcnt(0) between them
+    auto issue = [&]() {
 #pragma unroll
         for (int j = 0; j < UPW; ++j) {
             const int u = wave + gm::NW * j;
@@ -104,6 +109,8 @@ __device__ __forceinline__ void gm_fetch_a(__amdgpu_buffer_rsrc_t src, uint32_t 
             x[j][0] = hx_get2(src, off);
             x[j][1] = hx_get2(src, off + 16);
         }
+    };
+    auto check = [&]() -> bool {
         bool ok = true;
 #pragma unroll
         for (int j = 0; j < UPW; ++j) {
@@ -114,8 +121,16 @@ __device__ __forceinline__ void gm_fetch_a(__amdgpu_buffer_rsrc_t src, uint32_t 
             ok &= !v || ((x[j][0].y == tag) & (x[j][0].w == tag) & (x[j][1].y == tag) &
                          (x[j][1].w == tag));
         }
-        if (__all(ok)) return;
+        return __all(ok);
+    };
+    issue();
+    work();
+    if (check()) return;
+    int spins = 0;
+    for (;;) {
         if (hx_spin_fail(spins, err, lane)) return;
+        issue();
+        if (check()) return;
     }
 }
 
@@ -126,28 +141,36 @@ __device__ __forceinline__ void gm_fetch_a(__amdgpu_buffer_rsrc_t src, uint32_t 
 // and z.  A consumer therefore only ever sees tag i-1 (keep polling) or tag i (done).
 //
 // Thread tid owns a1/a2 element (r, c) = (tid / CW, tid % CW) of its workgroup (R*CW <= 512).
-template <typename T, int UPW, int NT, int NZT, int MAXT>
+template <typename T> __device__ __forceinline__ T gm_tap_load(__amdgpu_buffer_rsrc_t r, uint32_t off);
+template <> __device__ __forceinline__ bf16 gm_tap_load<bf16>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __ushort_as_bfloat16(__builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0));
+}
+template <> __device__ __forceinline__ float gm_tap_load<float>(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+// FS0C: FS0 as a compile-time constant (0: runtime a.FS0).  DC: the whole launch shape as
+// constants -- D = DC, R = 8, CW = 64, NZ = Q / (D / 64) (0: runtime); the per-unit validity
+// masks of the runtime shape would otherwise be scalar-register spills in the loop.
+template <typename T, int UPW, int NT, int NZT, int MAXT, int FS0C, int DC>
 __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     using F = typename GmT<T>::frag;
     constexpr int GV = GmT<T>::GV, UK = GmT<T>::UK, EPL = UK / 4;
     constexpr int Q = gm::Q;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int D = a.D, R = a.R, CW = a.CW, NZ = a.NZ, FS0 = a.FS0, B = a.B;
-    // ---- group / member of this workgroup
-    // Static map: group = block % G (one XCD under round-robin dealing, speed only) with sc1
-    // hand-offs.  XCD census (a.census): every workgroup reads its XCC id and takes a slot on
-    // its XCD; once all arrived, if every XCD holds whole groups (count % P == 0) the groups
-    // are formed per XCD and hand-offs stay in that XCD's L2 (local mode).  All workgroups
-    // read the same final counts, so they all take the same decision.
+    const int D = DC ? DC : a.D, R = DC ? 8 : a.R, CW = DC ? 64 : a.CW;
+    const int NZ = DC ? gm::Q / (DC / 64) : a.NZ, B = a.B;
+    const int FS0 = FS0C ? FS0C : a.FS0;
+    // ---- group / member of this workgroup: static map, group g = block % G, member
+    // p = block / G (one XCD per group under round-robin dealing); the placement check
+    // (a.census, handoff.hpp) confirms it, and then the hand-offs stay in that XCD's L2.
     // (the 16-B word block at the very end of the dynamic LDS; no static __shared__: it would
     //  shift the 16-B alignment of the dynamic base)
-    int* gsh = (int*)(smem + ((((size_t)gm::Q * a.CW * sizeof(T) + 15) & ~(size_t)15) +
-                              (size_t)min(gm::NW, (a.D + UK - 1) / UK) *
-                                  max(a.CW / 16, a.NZ / 16) * 64 * sizeof(floatx4) +
-                              (size_t)a.R * gm::HIST * 4));
-    // member p is fixed by the block index (the weights below depend only on p and load
-    // while the census runs); the census only assigns the row group g
+    int* gsh = (int*)(smem + ((((size_t)gm::Q * CW * sizeof(T) + 15) & ~(size_t)15) +
+                              (size_t)min(gm::NW, (D + UK - 1) / UK) *
+                                  max(CW / 16, NZ / 16) * 64 * sizeof(floatx4) +
+                              (size_t)R * gm::HIST * 4));
     const int p = blockIdx.x / a.G;
     const int c0 = p * CW, z0 = p * NZ;
     const int NU = (D + UK - 1) / UK;
@@ -162,6 +185,11 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     if (dgb) dgb[0] = __builtin_amdgcn_s_memrealtime();
     int nd = 0;
 #define GM_STAMP() do { if (dg && nd < 511) dg[nd++] = __builtin_amdgcn_s_memrealtime(); } while (0)
+    // per-wave stamps of blocks 0 and G (group 0), steps 2..4 (timing diagnostics only)
+    unsigned long long* dgw = (a.diag && lane == 0 && (blockIdx.x == 0 || blockIdx.x == a.G))
+                                  ? a.diag + GM_DIAG_WAVE0 + ((blockIdx.x ? 8 : 0) + wave) * 64
+                                  : nullptr;
+#define GM_W(k) do { if (dgw && s >= 2 && s < 5) dgw[(s - 2) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
     GM_STAMP();
     // LDS: [tab15 Q x CW][red KW x ntm x 64 floatx4][hist R x HIST]
     T* tab15 = (T*)smem;
@@ -175,37 +203,19 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     F wh[UPW][NT], wo[UPW][NZT];
     // (loads from clamped addresses with no branches, so all of them are in flight at once;
     //  fragments outside the shape are zeroed afterwards)
-    int g;
+    const int g = blockIdx.x % a.G;
     bool local;
     {
-        // census arrival first (thread 0)
         int* cen = nullptr;
-        int slot = 0;
-        unsigned xcc = 0;
         if (a.census) {
             const int n = (*a.base + a.off - a.L) / FS0;          // launch index in this call
             cen = a.census + (n & 1) * HX_KEYED_WORDS;
-            if (tid == 0) slot = hx_census_arrive(cen, p, xcc);
+            if (tid == 0) hx_group_arrive(cen + g * a.P + p);
             else if (blockIdx.x == 0 && wave == 1) {
                 // zero the next launch's array (last used two launches ago)
                 int* nxt = a.census + ((n + 1) & 1) * HX_KEYED_WORDS;
                 for (int j = lane; j < HX_KEYED_WORDS; j += 64)
                     __hip_atomic_store(nxt + j, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        // ---- row group: static (block % G) or the XCD census.  Wave 0 settles it before
-        //      issuing its own loads (a wave's loads return in order, so a census poll queued
-        //      behind them would wait for the weights); the other waves' loads already fly.
-        if (wave == 0) {
-            int gg = blockIdx.x % a.G;
-            slot = __shfl(slot, 0);
-            xcc = (unsigned)__builtin_amdgcn_readfirstlane((int)xcc);
-            const int loc = cen && hx_census_finish(cen, a.P, slot, xcc, a.err, gg) ? 1 : 0;
-            if (!loc) gg = blockIdx.x % a.G;
-            if (tid == 0) {
-                gsh[0] = gg; gsh[2] = loc;
-                GM_STAMP();
-                if (dgb) dgb[1] = __builtin_amdgcn_s_memrealtime();
             }
         }
         uint4 lw[UPW][NT], lz[UPW][NZT];
@@ -236,8 +246,16 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             buf[it] = *reinterpret_cast<const uint4*>(
                 tab + ((int64_t)(FS0 - 1) * Q + q) * D + c0 + c);
         }
+        // placement check (wave 0, after its own loads are in flight)
+        if (wave == 0) {
+            const int loc = cen && hx_group_local(cen + g * a.P, a.P, a.err) ? 1 : 0;
+            if (tid == 0) {
+                gsh[2] = loc;
+                GM_STAMP();
+                if (dgb) dgb[1] = __builtin_amdgcn_s_memrealtime();
+            }
+        }
         __syncthreads();
-        g = gsh[0];
         local = gsh[2] != 0;
         if (dg) dg[511] = local ? 1 : 2;
 #pragma unroll
@@ -276,6 +294,8 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     }
     // this thread's a1/a2 element
     const bool own = tid < R * CW;
+    // every wave's elements lie in the row that wave samples (r = wave)
+    const bool row_wave = CW == 64 && R <= gm::NW;
     const int er = own ? tid / CW : 0, ec = own ? tid % CW : 0;
     const int eb = min(g * R + er, B - 1);
     const float bh = own ? a.b_hid[c0 + ec] : 0.f;
@@ -287,16 +307,23 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     // work (the next hand-off wait) in between so the gathers' latency hides behind it.
     // The loads are unconditional (clamped tap index; unused taps re-read tap 0 and are
     // dropped by a select), so the compiler keeps them all in flight in one basic block.
+    // (32-bit buffer offsets computed in VGPRs from the index: no per-tap 64-bit base
+    //  address to keep live in scalar registers)
     T tv[MAXT];
     float upv = 0.f, part = 0.f;
+    const __amdgpu_buffer_rsrc_t rtab =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<T*>(tab), (short)0, 0x7fffffff, 0x00020000);
+    const uint32_t colb = (uint32_t)(c0 + ec) * (uint32_t)sizeof(T);
     auto issue_part = [&](int i) {
         int xs[MAXT];
 #pragma unroll
         for (int k = 0; k < MAXT; ++k)
             xs[k] = hist[er * gm::HIST + ((i - FS0 + (k < FS0 - 1 ? k : 0)) & (gm::HIST - 1))];
 #pragma unroll
-        for (int k = 0; k < MAXT; ++k)
-            tv[k] = tab[((int64_t)(k < FS0 - 1 ? k : 0) * Q + xs[k]) * D + c0 + ec];
+        for (int k = 0; k < MAXT; ++k) {
+            const uint32_t row = (uint32_t)xs[k] + (uint32_t)((k < FS0 - 1 ? k : 0) * Q);
+            tv[k] = gm_tap_load<T>(rtab, row * (uint32_t)D * (uint32_t)sizeof(T) + colb);
+        }
         upv = a.up0[(int64_t)eb * a.ldup + (int64_t)(i % FS0) * D + c0 + ec];
     };
     auto finish_part = [&]() {
@@ -305,17 +332,15 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         for (int k = 0; k < MAXT; ++k) v += k < FS0 - 1 ? to_f(tv[k]) : 0.f;
         part = own ? v : 0.f;
     };
-    // publish a1(i) = relu(part + Tab[FS0-1][x_{i-1}]) as granules tagged i
-    auto publish_a1 = [&](int i) {
+    // publish a1(i) = relu(part + Tab[FS0-1][x_{i-1}]) as granules tagged i (x = x_{i-1} of
+    // this thread's row)
+    auto publish_a1 = [&](int i, int x) {
         u64* dst = a.xa1 + (size_t)g * R * DG;
         float v = 0.f;
-        if (own) {
-            const int x = hist[er * gm::HIST + ((i - 1) & (gm::HIST - 1))];
-            v = fmaxf(part + to_f(tab15[x * CW + ec]), 0.f);
-        }
+        if (own) v = fmaxf(part + to_f(tab15[x * CW + ec]), 0.f);
         if (GV == 2) {
             const uint32_t mine = gm_bf16_bits(v);
-            const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
+            const uint32_t nb = lane_next16(mine);
             if (own && (ec & 1) == 0) hx_put(dst + (size_t)er * DG + (c0 + ec) / 2, i, mine | (nb << 16), local);
         } else if (own) {
             hx_put(dst + (size_t)er * DG + c0 + ec, i, gm_bits(v), local);
@@ -326,9 +351,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     if (dgb) dgb[2] = __builtin_amdgcn_s_memrealtime();
     issue_part(i0);
     finish_part();
-    publish_a1(i0);
-    if (a.nsteps > 1) issue_part(i0 + 1);
-    bool pending = a.nsteps > 1;
+    publish_a1(i0, hist[er * gm::HIST + ((i0 - 1) & (gm::HIST - 1))]);
 
     const int row = lane & 15;
     const bool rv = row < R;
@@ -336,15 +359,19 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     for (int s = 0; s < a.nsteps; ++s) {
         const int i = i0 + s;
         const uint32_t tag = (uint32_t)i;
+        GM_W(0);
         // ---------------- a2 = relu(W_hid a1 + b_hid), this workgroup's CW columns
         {
             floatx4 acc[NT];
 #pragma unroll
             for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            // the next sample's table gathers go in flight under the a1 hand-off
+            auto work = [&]() { if (s + 1 < a.nsteps) issue_part(i + 1); };
+            if (wave >= KW) work();
             if (wave < KW) {
                 uint32_t w[UPW][4];
-                gm_fetch_a<T, UPW>(rx1, rowg, rv, wave, lane, NU, D, tag, w, a.err);
-                GM_STAMP();
+                gm_fetch_a<T, UPW>(rx1, rowg, rv, wave, lane, NU, D, tag, w, a.err, work);
+                GM_W(1);
 #pragma unroll
                 for (int j = 0; j < UPW; ++j) {
                     const F af = gm_frag<F>(w[j][0], w[j][1], w[j][2], w[j][3]);
@@ -355,9 +382,10 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 for (int t = 0; t < NT; ++t)
                     if (t < nt) red[(wave * ntm + t) * 64 + lane] = acc[t];
             }
-            if (pending) { finish_part(); pending = false; }   // gathers landed meanwhile
-            GM_STAMP();
+            GM_W(2);
+            GM_W(3);
             __syncthreads();
+            GM_W(4);
             u64* dst = a.xa2 + (size_t)g * R * DG;
             float v = 0.f;
             if (own) {
@@ -372,23 +400,28 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             }
             if (GV == 2) {
                 const uint32_t mine = gm_bf16_bits(v);
-                const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
+                const uint32_t nb = lane_next16(mine);
                 if (own && (ec & 1) == 0)
                     hx_put(dst + (size_t)er * DG + (c0 + ec) / 2, tag, mine | (nb << 16), local);
             } else if (own) {
                 hx_put(dst + (size_t)er * DG + c0 + ec, tag, gm_bits(v), local);
             }
+            GM_W(5);
             __syncthreads();                   // red is reused by the next phase
         }
-        GM_STAMP();
+        GM_W(6);
         // ---------------- z = W_out a2 + b_out, this workgroup's NZ logits
         {
             floatx4 acc[NZT];
 #pragma unroll
             for (int t = 0; t < NZT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            // ... and are summed under the a2 hand-off
+            auto work = [&]() { if (s + 1 < a.nsteps) finish_part(); };
+            if (wave >= KW) work();
             if (wave < KW) {
                 uint32_t w[UPW][4];
-                gm_fetch_a<T, UPW>(rx2, rowg, rv, wave, lane, NU, D, tag, w, a.err);
+                gm_fetch_a<T, UPW>(rx2, rowg, rv, wave, lane, NU, D, tag, w, a.err, work);
+                GM_W(7);
 #pragma unroll
                 for (int j = 0; j < UPW; ++j) {
                     const F af = gm_frag<F>(w[j][0], w[j][1], w[j][2], w[j][3]);
@@ -400,7 +433,9 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 for (int t = 0; t < NZT; ++t)
                     if (t < nzt) red[(wave * ntm + t) * 64 + lane] = acc[t];
             }
+            GM_W(8);
             __syncthreads();
+            GM_W(9);
             for (int e = tid; e < R * NZ; e += gm::NTHR) {
                 const int r = e / NZ, c = e % NZ;
                 const int t = c >> 4, ln = (r >> 2) * 16 + (c & 15), ii = r & 3;
@@ -414,61 +449,84 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 hx_put(a.xz + ((size_t)g * R + r) * Q + z0 + c, tag,
                        gm_bits(v + (e < gm::NTHR ? bo : a.b_out[z0 + c])), local);
             }
+            GM_W(10);
             __syncthreads();
         }
-        GM_STAMP();
+        GM_W(11);
         // ---------------- sample x_i for every row of the group (one wave per row)
+        int xw = 0;
         for (int r = wave; r < R; r += gm::NW) {
             const int b = g * R + r;
             const bool valid = b < B;
-            const floatx4 qn = valid ? sample_noise(a.noise, a.seed, B, b, i - a.L, lane)
-                                     : floatx4{1.f, 1.f, 1.f, 1.f};
             const uint32_t zoff = (uint32_t)((((size_t)g * R + r) * Q + 4 * lane) * 8);
             floatx4 v;
-            int spins = 0;
-            for (;;) {
-                const uint4 x0 = hx_get2(rxz, zoff), x1 = hx_get2(rxz, zoff + 16);
+            uint4 x0, x1;
+            auto zcheck = [&]() -> bool {
                 v = floatx4{__uint_as_float(x0.x), __uint_as_float(x0.z), __uint_as_float(x1.x),
                             __uint_as_float(x1.z)};
-                const bool ok = (x0.y == tag) & (x0.w == tag) & (x1.y == tag) & (x1.w == tag);
-                if (__all(ok)) break;
-                if (hx_spin_fail(spins, a.err, lane)) break;
+                return __all((x0.y == tag) & (x0.w == tag) & (x1.y == tag) & (x1.w == tag));
+            };
+            x0 = hx_get2(rxz, zoff);
+            x1 = hx_get2(rxz, zoff + 16);
+            // the row's noise is drawn under the z hand-off (first poll in flight)
+            const floatx4 lq = valid ? log_noise(sample_noise(a.noise, a.seed, B, b, i - a.L, lane))
+                                     : floatx4{0.f, 0.f, 0.f, 0.f};
+            if (!zcheck()) {
+                int spins = 0;
+                for (;;) {
+                    if (hx_spin_fail(spins, a.err, lane)) break;
+                    x0 = hx_get2(rxz, zoff);
+                    x1 = hx_get2(rxz, zoff + 16);
+                    if (zcheck()) break;
+                }
             }
+            if (r == wave) GM_W(12);
             float* lrow = (p == 0 && valid && a.logp)
                               ? a.logp + ((int64_t)(i - a.L) * B + b) * Q : nullptr;
-            const int x = sample_row(v, qn, lrow, lane);
+            const int x = sample_row(v, lq, lrow, lane);
             if (lane == 0) {
                 hist[r * gm::HIST + (i & (gm::HIST - 1))] = x;
                 if (p == 0 && valid) a.seq[(int64_t)b * a.ldseq + i] = x;
             }
+            if (r == wave) xw = x;
         }
-        __syncthreads();
-        GM_STAMP();
+        GM_W(13);
         // ---------------- next sample's a1; the one after's gathers go in flight
-        if (s + 1 < a.nsteps) {
-            publish_a1(i + 1);
-            if (s + 2 < a.nsteps) { issue_part(i + 2); pending = true; }
-        }
+        // (row-per-wave layout: this wave sampled its own elements' row, so a1(i+1) leaves
+        //  before the barrier; otherwise the row's index comes from the history after it)
+        if (row_wave && s + 1 < a.nsteps) publish_a1(i + 1, xw);
+        GM_W(14);
+        __syncthreads();
+        GM_W(15);
+        if (!row_wave && s + 1 < a.nsteps)
+            publish_a1(i + 1, hist[er * gm::HIST + (i & (gm::HIST - 1))]);
         GM_STAMP();
     }
 #undef GM_STAMP
+#undef GM_W
 }
 
 // ------------------------------------------------------------------ host side
 namespace {
 typedef void (*GmKernel)(GenMlpArgs);
 
-template <typename T, int MAXT>
+template <typename T, int MAXT, int FS0C>
 GmKernel pick_t(int upw, int nzt) {
-    if (upw <= 1 && nzt <= 16) return gen_mlp_kernel<T, 1, 4, 16, MAXT>;
-    if (upw <= 2 && nzt <= 4) return gen_mlp_kernel<T, 2, 4, 4, MAXT>;
-    if (upw <= 4 && nzt <= 2) return gen_mlp_kernel<T, 4, 4, 2, MAXT>;
+    if (upw <= 1 && nzt <= 16) return gen_mlp_kernel<T, 1, 4, 16, MAXT, FS0C, 0>;
+    if (upw <= 2 && nzt <= 4) return gen_mlp_kernel<T, 2, 4, 4, MAXT, FS0C, 0>;
+    if (upw <= 4 && nzt <= 2) return gen_mlp_kernel<T, 4, 4, 2, MAXT, FS0C, 0>;
     return nullptr;     // fp32 at D > 512 would spill its resident weights: per-step path
 }
 // MAXT = older taps gathered per sample (FS0 - 1 <= MAXT)
 template <typename T>
-GmKernel pick(int upw, int nzt, int fs0) {
-    return fs0 - 1 <= 15 ? pick_t<T, 15>(upw, nzt) : pick_t<T, 31>(upw, nzt);
+GmKernel pick(int upw, int nzt, int fs0, int D, int R) {
+    // (FS0 = 16, the bottom frame of every published config, gets its own build: a
+    //  constant FS0 folds the tap bookkeeping that would otherwise live in scalar registers;
+    //  dim 1024 in bf16 -- the published model -- has its whole launch shape compiled in)
+    if (std::is_same<T, bf16>::value && fs0 == 16 && D == 1024 && R == 8)
+        return gen_mlp_kernel<T, 4, 4, 2, 15, 16, 1024>;
+    if (fs0 == 16) return pick_t<T, 15, 16>(upw, nzt);
+    return fs0 - 1 <= 15 ? pick_t<T, 15, 0>(upw, nzt) : pick_t<T, 31, 0>(upw, nzt);
 }
 
 int device_cus() {
@@ -500,8 +558,8 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     for (int r : {8})          // one a1 element per thread: R * CW <= 512
         if ((int64_t)cdiv(B, r) * P <= ncu) { R = r; break; }
     if (!R) return 0;
-    const GmKernel k = dtype == SRNN_BF16 ? pick<bf16>(upw, NZ / 16, FS0)
-                                          : pick<float>(upw, NZ / 16, FS0);
+    const GmKernel k = dtype == SRNN_BF16 ? pick<bf16>(upw, NZ / 16, FS0, D, R)
+                                          : pick<float>(upw, NZ / 16, FS0, D, R);
     if (!k) return 0;
     const int es = dtype == SRNN_BF16 ? 2 : 4;
     const int KW = NU < gm::NW ? NU : gm::NW;
@@ -528,7 +586,7 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
 }
 
 #define GM_DIAG_BLOCKS 1024
-#define GM_DIAG_WORDS (512 + 3 * GM_DIAG_BLOCKS)
+#define GM_DIAG_WORDS (GM_DIAG_WAVE0 + 16 * 64)
 unsigned long long*& gm_diag_buf() {
     static unsigned long long* p = nullptr;
     return p;
@@ -553,6 +611,23 @@ extern "C" int srnn_gen_diag_dump(void) {
     }
     fprintf(stderr, "gen_mlp diag %d blocks: last start +%.2f us, last group +%.2f us, "
             "last prologue +%.2f us\n", nb, smax / 100.0, cmax / 100.0, pmax / 100.0);
+    // per-wave stamps (blocks 0 and G, steps 2..4), us relative to wave 0 of block 0 at the
+    // step's start
+    for (int st = 0; st < 3; ++st) {
+        const unsigned long long t0w = h[GM_DIAG_WAVE0 + st * 16];
+        if (!t0w) break;
+        fprintf(stderr, "gen_mlp wave stamps, step %d (block 0 waves 0-7 | block G waves 0-7):\n", st + 2);
+        for (int k = 0; k < 16; ++k) {
+            fprintf(stderr, "  k=%2d", k);
+            for (int w = 0; w < 16; ++w) {
+                const unsigned long long v = h[GM_DIAG_WAVE0 + w * 64 + st * 16 + k];
+                if (w == 8) fprintf(stderr, " |");
+                if (v) fprintf(stderr, " %5.2f", ((double)v - (double)t0w) / 100.0);
+                else fprintf(stderr, "     -");
+            }
+            fprintf(stderr, "\n");
+        }
+    }
     return 0;
 }
 
@@ -563,7 +638,7 @@ int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
     a.P = pl->P;
     a.CW = pl->CW;
     a.NZ = pl->NZ;
-    if (!pl->local) a.census = nullptr;
+    if (!pl->local || pl->G * pl->P > HX_KEYED_WORDS) a.census = nullptr;
     {
         // SRNN_GEN_DIAG=1: phase timestamps of the first launch into a device buffer that
         // srnn_gen_diag_dump prints (timing diagnostics only)

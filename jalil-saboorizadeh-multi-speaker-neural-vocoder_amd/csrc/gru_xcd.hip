@@ -8,7 +8,7 @@
 // the Infinity Fabric.  Here:
 //   * a group = 16 rows (one MFMA M tile) x all D units, split over P = D / 32 workgroups of
 //     32 units (B = 128, D = 1024: 8 groups x 32 = 256 workgroups, one group per XCD when the
-//     per-launch census (handoff.hpp) confirms the placement);
+//     per-launch placement check (handoff.hpp) confirms it);
 //   * each of the 8 waves holds its K-slice of the workgroup's 96 W_hh rows (3 gates x 32
 //     units) as MFMA B fragments in VGPRs for the whole sequence (96 VGPRs at D = 1024);
 //   * per step every workgroup reads the group's h_{t-1} as 8-byte {2 x bf16, tag} granules
@@ -26,6 +26,8 @@ constexpr int RG = 16;                 // rows per group
 constexpr int CU = 32;                 // units per workgroup
 constexpr int NT = 6;                  // n tiles: 3 gates x 2 x 16 units
 constexpr int UK = 32;                 // k per bf16 MFMA unit
+// work header: [0] error word, ints [16, HDR / 4) the placement-check slots ([G][P])
+constexpr int HDR = 2048;
 }  // namespace gx
 
 // Failure reporting: the per-call error word lives in a work buffer the next call re-zeroes,
@@ -44,7 +46,7 @@ struct GruXArgs {
     float* out; bf16* out_lp; int64_t ldo; int64_t so;
     float* gates; int64_t ldg; int64_t sg;          // r | z | n | gh_n per row and step
     u64* xh;                                        // 2 x G x RG x D/2 granules
-    int* census;                                    // 9 zeroed words, or null (static map)
+    int* census;                                    // [G][P] zeroed slots, or null (global mode)
     int* err;
     int* sticky;                                    // persist.hip flag
     int spin_limit;
@@ -63,20 +65,15 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     const int NU = D / UK, KW = NW < NU ? NW : NU;
     floatx4* red = (floatx4*)smem;                              // [KW][NT][64]
     int* gsh = (int*)(smem + (size_t)KW * NT * 64 * sizeof(floatx4));
-    if (tid == 0) {
-        int g = blockIdx.x % a.G, p = blockIdx.x / a.G, loc = 0;
-        if (a.census) loc = hx_census(a.census, a.P, a.err, g, p) ? 1 : 0;
-        gsh[0] = g; gsh[1] = p; gsh[2] = loc;
-    }
-    __syncthreads();
-    const int g = gsh[0], p = gsh[1];
-    const bool local = gsh[2] != 0;
+    // static map (handoff.hpp): group g = block % G, member p = block / G; the placement
+    // check runs while the weights load
+    const int g = blockIdx.x % a.G, p = blockIdx.x / a.G;
+    if (a.census && tid == 0) hx_group_arrive(a.census + g * a.P + p);
     const int u0 = p * CU;
     const int DG = D / 2;
     unsigned long long* dg = (a.diag && blockIdx.x == 0 && tid == 0) ? a.diag : nullptr;
     int nd = 0;
 #define GX_STAMP() do { if (dg && nd < 255) dg[nd++] = __builtin_amdgcn_s_memrealtime(); } while (0)
-    if (dg) dg[255] = local ? 1 : 2;
     // ---- resident W_hh fragments: unit j of this wave = k-range [(wave + NW j) * 32, +32)
     bf16x8 wf[UPW][NT];
     {
@@ -101,6 +98,13 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
             }
         }
     }
+    if (wave == 0) {
+        const int loc = a.census && hx_group_local(a.census + g * a.P, a.P, a.err) ? 1 : 0;
+        if (tid == 0) gsh[2] = loc;
+    }
+    __syncthreads();
+    const bool local = gsh[2] != 0;
+    if (dg) dg[255] = local ? 1 : 2;
     // ---- this thread's state element: row r of the group, unit u0 + uu
     const int r = tid >> 5, uu = tid & 31;
     const int b = min(g * RG + r, B - 1);
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     const size_t bufw = (size_t)a.G * RG * DG;                  // granules per buffer
     auto publish = [&](int s, float h) {        // h_s -> buffer (s + 1) & 1, tag s + 2
         const uint32_t mine = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(h));
-        const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
+        const uint32_t nb = lane_next16(mine);
         if ((uu & 1) == 0 && !(a.withhold && blockIdx.x == 0))
             hx_put(a.xh + ((s + 1) & 1) * bufw + (size_t)(g * RG + r) * DG + unit / 2,
                    (uint32_t)(s + 2), mine | (nb << 16), local);
@@ -249,14 +253,10 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
     constexpr int NTB = 2;                                      // 32 units = 2 n tiles
     floatx4* red = (floatx4*)smem;                              // [KW][2][64]
     int* gsh = (int*)(smem + (size_t)KW * NTB * 64 * sizeof(floatx4));
-    if (tid == 0) {
-        int g = blockIdx.x % a.G, p = blockIdx.x / a.G, loc = 0;
-        if (a.census) loc = hx_census(a.census, a.P, a.err, g, p) ? 1 : 0;
-        gsh[0] = g; gsh[1] = p; gsh[2] = loc;
-    }
-    __syncthreads();
-    const int g = gsh[0], p = gsh[1];
-    const bool local = gsh[2] != 0;
+    // static map (handoff.hpp): group g = block % G, member p = block / G; the placement
+    // check runs while the weights load
+    const int g = blockIdx.x % a.G, p = blockIdx.x / a.G;
+    if (a.census && tid == 0) hx_group_arrive(a.census + g * a.P + p);
     const int u0 = p * CU;
     const int KG = K3 / 2;                                      // granules per row
     bf16x8 wf[UPW][NTB];
@@ -282,6 +282,12 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
             }
         }
     }
+    if (wave == 0) {
+        const int loc = a.census && hx_group_local(a.census + g * a.P, a.P, a.err) ? 1 : 0;
+        if (tid == 0) gsh[2] = loc;
+    }
+    __syncthreads();
+    const bool local = gsh[2] != 0;
     const int r = tid >> 5, uu = tid & 31;
     const int b = min(g * RG + r, B - 1);
     const bool wr = g * RG + r < B;
@@ -365,7 +371,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
 #pragma unroll
             for (int gt = 0; gt < 3; ++gt) {
                 const uint32_t mine = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(vals[gt]));
-                const uint32_t nb = (uint32_t)__shfl_down((int)mine, 1);
+                const uint32_t nb = lane_next16(mine);
                 if ((uu & 1) == 0 && !(a.withhold && blockIdx.x == 0))
                     hx_put(dst + (gt * D + unit) / 2, (uint32_t)(a.Fr - t), mine | (nb << 16), local);
             }
@@ -438,7 +444,7 @@ extern "C" size_t srnn_gru_xcd_work_bytes(int dtype, int B, int D) {
     const int G = cdiv(B, gx::RG), P = D / gx::CU;
     const int ncu = gx_cus();
     if (ncu <= 0 || G * P > ncu) return 0;
-    return 256 + (size_t)2 * G * gx::RG * (D / 2) * 8;
+    return gx::HDR + (size_t)2 * G * gx::RG * (D / 2) * 8;
 }
 
 extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
@@ -464,7 +470,7 @@ extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi
     a.spin_limit = srnn_persist_spin_limit(hx::SPIN_LIMIT);
     a.withhold = env_flag("SRNN_PERSIST_FORCE_FAIL", 0);
     a.census = env_flag("SRNN_GEN_LOCAL", 1) ? (int*)work + 16 : nullptr;
-    a.xh = (u64*)((char*)work + 256);
+    a.xh = (u64*)((char*)work + gx::HDR);
     a.B = B; a.D = D; a.Fr = Fr;
     a.diag = nullptr;
     a.poll_sleep = env_flag("SRNN_POLL_SLEEP", 1);
@@ -504,7 +510,7 @@ extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi
 extern "C" size_t srnn_gru_xcd_bwd_work_bytes(int dtype, int B, int D) {
     if (!srnn_gru_xcd_work_bytes(dtype, B, D)) return 0;
     const int G = cdiv(B, gx::RG);
-    return 256 + (size_t)2 * G * gx::RG * (3 * D / 2) * 8;
+    return gx::HDR + (size_t)2 * G * gx::RG * (3 * D / 2) * 8;
 }
 
 extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* dy, int64_t lddy,
@@ -534,7 +540,7 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
     a.spin_limit = srnn_persist_spin_limit(hx::SPIN_LIMIT);
     a.withhold = env_flag("SRNN_PERSIST_FORCE_FAIL", 0);
     a.census = env_flag("SRNN_GEN_LOCAL", 1) ? (int*)work + 16 : nullptr;
-    a.xg = (u64*)((char*)work + 256);
+    a.xg = (u64*)((char*)work + gx::HDR);
     a.B = B; a.D = D; a.Fr = Fr;
     a.G = cdiv(B, gx::RG);
     a.P = D / gx::CU;

@@ -526,8 +526,8 @@ __global__ __launch_bounds__(256) void sample_kernel(
     const int i = *base + off;        // absolute sample index being generated
     const int step = i - L;
     const floatx4 v = *reinterpret_cast<const floatx4*>(z + (int64_t)b * ldz + 4 * lane);
-    const floatx4 q = sample_noise(noise, seed, B, b, step, lane);
-    const int bi = sample_row(v, q, logp_out ? logp_out + ((int64_t)step * B + b) * 256 : nullptr,
+    const floatx4 lq = log_noise(sample_noise(noise, seed, B, b, step, lane));
+    const int bi = sample_row(v, lq, logp_out ? logp_out + ((int64_t)step * B + b) * 256 : nullptr,
                               lane);
     if (lane == 0) seq[(int64_t)b * ldseq + i] = bi;
 }

@@ -4,21 +4,64 @@
 //
 // Reference: Generator.__call__ (model.py:514-517) samples
 //     x_t = exp(log_softmax(z)).multinomial(1)
-// which torch>=2 on CPU implements as argmax(p / q), q ~ Exp(1) (first index on ties).
+// which torch>=2 on CPU implements as argmax(p / q), q ~ Exp(1) (first index on ties);
+// here argmax(z - log q), the same index up to fp rounding of near-ties.
 // q comes either from a device buffer (bit-replay of the reference RNG stream) or from a
 // counter-based Philox4x32-10 (counter = (lane, row, step, 0), key = seed).
 #pragma once
 #include "common.hpp"
 
+// All-lane reductions over the wave without LDS: xor-1, xor-2 (DPP quad_perm), the
+// 8-lane half mirror and the 16-lane mirror (DPP), then the lane pairs i, i ^ 16 and i, i ^ 32
+// (permlane swaps).  Every step combines the same two operands in both lanes of a pair
+// (a + b == b + a bitwise), so all 64 lanes end with the identical value.
+template <typename Op>
+__device__ __forceinline__ float wave_allreduce(float v, Op op) {
+    v = op(v, __uint_as_float(dpp_u32<0xB1>(__float_as_uint(v))));    // quad_perm [1,0,3,2]
+    v = op(v, __uint_as_float(dpp_u32<0x4E>(__float_as_uint(v))));    // quad_perm [2,3,0,1]
+    v = op(v, __uint_as_float(dpp_u32<0x141>(__float_as_uint(v))));   // row_half_mirror
+    v = op(v, __uint_as_float(dpp_u32<0x140>(__float_as_uint(v))));   // row_mirror
+    uint32_t lo, hi;
+    xpair16(__float_as_uint(v), lo, hi);
+    v = op(__uint_as_float(lo), __uint_as_float(hi));
+    xpair32(__float_as_uint(v), lo, hi);
+    return op(__uint_as_float(lo), __uint_as_float(hi));
+}
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    return v;
+    return wave_allreduce(v, [](float a, float b) { return fmaxf(a, b); });
 }
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
+    return wave_allreduce(v, [](float a, float b) { return a + b; });
+}
+
+// (best, index) argmax over the wave, first index on ties (torch argmax); same step
+// sequence as wave_allreduce
+__device__ __forceinline__ void amax_take(float& best, int& bi, float ob, int oi) {
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+}
+template <int CTRL>
+__device__ __forceinline__ void amax_dpp(float& best, int& bi) {
+    const float ob = __uint_as_float(dpp_u32<CTRL>(__float_as_uint(best)));
+    const int oi = (int)dpp_u32<CTRL>((uint32_t)bi);
+    amax_take(best, bi, ob, oi);
+}
+__device__ __forceinline__ int wave_argmax(float best, int bi) {
+    amax_dpp<0xB1>(best, bi);
+    amax_dpp<0x4E>(best, bi);
+    amax_dpp<0x141>(best, bi);
+    amax_dpp<0x140>(best, bi);
+    uint32_t lo, hi, ilo, ihi;
+    xpair16(__float_as_uint(best), lo, hi);
+    xpair16((uint32_t)bi, ilo, ihi);
+    best = __uint_as_float(lo);
+    bi = (int)ilo;
+    amax_take(best, bi, __uint_as_float(hi), (int)ihi);
+    xpair32(__float_as_uint(best), lo, hi);
+    xpair32((uint32_t)bi, ilo, ihi);
+    best = __uint_as_float(lo);
+    bi = (int)ilo;
+    amax_take(best, bi, __uint_as_float(hi), (int)ihi);
+    return bi;
 }
 
 // Philox4x32-10 (Salmon et al. 2011)
@@ -51,32 +94,36 @@ __device__ __forceinline__ floatx4 sample_noise(const float* noise, uint64_t see
                    exp1_from_u32(rnd.w)};
 }
 
-// One wave, one row of Q = 256 logits (lane holds q = 4 lane + j).  Returns the sampled index
-// (wave-uniform); writes the row's log-probs to logp_row (if non-null).
-__device__ __forceinline__ int sample_row(const floatx4& v, const floatx4& q, float* logp_row,
+// log q of a lane's 4 noise values (computed ahead of the logits: off the critical path)
+__device__ __forceinline__ floatx4 log_noise(const floatx4& q) {
+    return floatx4{logf(q[0]), logf(q[1]), logf(q[2]), logf(q[3])};
+}
+
+// One wave, one row of Q = 256 logits (lane holds q = 4 lane + j), lq = log_noise(q).
+// Returns the sampled index (wave-uniform); writes the row's log-probs to logp_row (if
+// non-null).  The draw argmax_j softmax(z)_j / q_j (model.py:514) is taken in log space as
+// argmax_j (z_j - log q_j): the softmax normaliser is common to all j, so the index needs no
+// reduction but the argmax (first index on ties); log-probs, when asked for, come after.
+__device__ __forceinline__ int sample_row(const floatx4& v, const floatx4& lq, float* logp_row,
                                           int lane) {
-    float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
-    m = wave_max(m);
-    float s = 0.f;
+    float best = v[0] - lq[0];
+    int bi = 4 * lane;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) s += expf(v[j] - m);
-    s = wave_sum(s);
-    const float ls = logf(s);
-    float best = -1.0f;
-    int bi = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const float lp = (v[j] - m) - ls;
-        if (logp_row) logp_row[4 * lane + j] = lp;
-        const float r = expf(lp) / q[j];
-        if (r > best) { best = r; bi = 4 * lane + j; }
+    for (int j = 1; j < 4; ++j) {
+        const float t = v[j] - lq[j];
+        if (t > best) { best = t; bi = 4 * lane + j; }
     }
-    // wave argmax, first index on ties (torch argmax)
+    bi = __builtin_amdgcn_readfirstlane(wave_argmax(best, bi));
+    if (logp_row) {
+        float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+        m = wave_max(m);
+        float s = 0.f;
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const float ob = __shfl_xor(best, o);
-        const int oi = __shfl_xor(bi, o);
-        if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+        for (int j = 0; j < 4; ++j) s += expf(v[j] - m);
+        s = wave_sum(s);
+        const float ls = logf(s);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) logp_row[4 * lane + j] = (v[j] - m) - ls;
     }
-    return __builtin_amdgcn_readfirstlane(bi);
+    return bi;
 }
