@@ -361,7 +361,7 @@ def test_gemm_bf16_out_batched_mask(hip):
 
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('with_x', [False, True])
-@pytest.mark.parametrize('D', [80, 256])     # 256: deep-ring kernel path
+@pytest.mark.parametrize('D', [80, 256, 1024])   # 256, 1024: deep-ring kernel path
 def test_gru_cell(hip, dtype, with_x, D):
     B = 67
     x = _rand(B, D, seed=1).to(DEV)
