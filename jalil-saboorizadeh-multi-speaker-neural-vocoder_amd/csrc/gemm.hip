@@ -21,6 +21,7 @@ struct GemmArgs {
     int vecA, vecB;
     const void* mask;  // optional relu-backward mask (input dtype): out = 0 where mask <= 0
     int64_t ldmask;
+    unsigned long long* diag;   // skinny path timing diagnostics (workgroup 0, wave 0), or null
 };
 
 template <typename T, typename TO, int BM, int BN, int KS, int WM, int WN, int WK, bool KCA,
@@ -82,9 +83,13 @@ __global__ __launch_bounds__(256) void skinny_kernel(GemmArgs g) {
     for (int i = 0; i < R::FM; ++i)
 #pragma unroll
         for (int j = 0; j < R::FN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+    unsigned long long* st = (g.diag && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+                                 ? g.diag : nullptr;
+    if (st) st[0] = __builtin_amdgcn_s_memrealtime();
     ring_core<T, BM, BN, WM, WN, WK, NS>((const T*)g.A, g.lda, RowClamp{m0, g.M}, (const T*)g.B,
-                                         g.ldb, RowClamp{n0, g.N}, g.K, smem, acc);
+                                         g.ldb, RowClamp{n0, g.N}, g.K, smem, acc, st);
     ring_reduce<T, BM, BN, WM, WN, WK, NS>(smem, acc);
+    if (st) st[31] = __builtin_amdgcn_s_memrealtime();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
     if (wk != 0) return;
@@ -109,6 +114,33 @@ __global__ __launch_bounds__(256) void skinny_kernel(GemmArgs g) {
                 Cp[(int64_t)row * g.ldc + col] = from_f<TO>(v);
             }
         }
+    if (st) st[32] = __builtin_amdgcn_s_memrealtime();
+}
+
+// SRNN_SKINNY_DIAG=1: stage timestamps of workgroup 0 of every skinny launch into a device
+// buffer (the last launch wins) that srnn_skinny_diag_dump prints (timing diagnostics only)
+static unsigned long long* skinny_diag() {
+    static unsigned long long* d = nullptr;
+    static int armed = -1;
+    if (armed < 0) {
+        armed = env_flag("SRNN_SKINNY_DIAG", 0);
+        if (armed && hipMalloc(&d, 64 * 8) != hipSuccess) d = nullptr;
+        if (d) (void)hipMemset(d, 0, 64 * 8);
+    }
+    return d;
+}
+
+extern "C" int srnn_skinny_diag_dump(void) {
+    unsigned long long h[64];
+    unsigned long long* d = skinny_diag();
+    if (!d || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost) != hipSuccess)
+        return 1;
+    fprintf(stderr, "skinny diag (us from workgroup 0 start):");
+    for (int k = 1; k <= 32; ++k)
+        if (h[k]) fprintf(stderr, " %d:%.2f", k, (double)(h[k] - h[0]) / 100.0);
+    fprintf(stderr, "\n");
+    return 0;
 }
 
 // all M (<= 128) rows in one tile, so every weight row streams through the chip ONCE (the
@@ -249,6 +281,7 @@ int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int 
     g.M = M; g.N = N; g.K = K; g.alpha = alpha; g.beta = beta;
     g.bias_mode = bias ? bias_mode : 0; g.relu = relu;
     g.mask = mask; g.ldmask = ldmask;
+    g.diag = skinny_diag();
     auto aligned = [&](const void* p, int64_t ld, int64_t st) {
         return ((uintptr_t)p % 16 == 0) && (ld % E == 0) && (batch == 1 || st % E == 0);
     };

@@ -243,7 +243,7 @@ struct GruXBwdArgs {
     int B, D, Fr, G, P;
 };
 
-template <int UPW>
+template <int UPW, bool FULL>     // FULL: NU == UPW * NW (every unit of every wave in range)
 __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a) {
     using namespace gx;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -319,11 +319,19 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
                                                   (size_t)(g * RG + lrow) * KG) * 8);
                 uint4 x[UPW][2];
                 int spins = 0;
+                // unit j's granules sit at lane offset + j * NW units (every unit of the wave
+                // in range: NU == UPW * NW, e.g. D = 1024); the lane offset is made opaque per
+                // step so the compiler does not keep UPW hoisted offsets live (at UPW = 12 they
+                // were spilled to scratch and reloaded serially every step)
+                uint32_t lb = (uint32_t)((wave * UK + (lane >> 4) * 8) / 2) * 8u;
+                asm volatile("" : "+v"(lb));
                 for (;;) {
 #pragma unroll
                     for (int j = 0; j < UPW; ++j) {
                         const int u = min(wave + NW * j, NU - 1);
-                        const uint32_t off = base + (uint32_t)((u * UK + (lane >> 4) * 8) / 2) * 8u;
+                        const uint32_t off =
+                            FULL ? base + lb + (uint32_t)(j * NW * UK / 2 * 8)
+                                 : base + (uint32_t)((u * UK + (lane >> 4) * 8) / 2) * 8u;
                         x[j][0] = hx_get2(rx, off);
                         x[j][1] = hx_get2(rx, off + 16);
                     }
@@ -548,8 +556,10 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
     const int KW = NU < gx::NW ? NU : gx::NW;
     const size_t lds = (size_t)KW * 2 * 64 * 16 + 16;
     const int upw = cdiv(NU, gx::NW);
-    void (*k)(GruXBwdArgs) = upw <= 3 ? gru_xcd_bwd_kernel<3>
-                             : upw <= 6 ? gru_xcd_bwd_kernel<6> : gru_xcd_bwd_kernel<12>;
+    void (*k)(GruXBwdArgs) =
+        upw <= 3 ? (NU == 3 * gx::NW ? gru_xcd_bwd_kernel<3, true> : gru_xcd_bwd_kernel<3, false>)
+        : upw <= 6 ? (NU == 6 * gx::NW ? gru_xcd_bwd_kernel<6, true> : gru_xcd_bwd_kernel<6, false>)
+        : (NU == 12 * gx::NW ? gru_xcd_bwd_kernel<12, true> : gru_xcd_bwd_kernel<12, false>);
     hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;

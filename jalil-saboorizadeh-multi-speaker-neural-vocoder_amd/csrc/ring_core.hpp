@@ -86,7 +86,8 @@ template <typename T, int BM, int BN, int WM, int WN, int WK, int NS, class MapA
 __device__ __forceinline__ void ring_core(
     const T* __restrict__ A, int64_t lda, MapA mapA, const T* __restrict__ B, int64_t ldb,
     MapB mapB, int K, char* smem,
-    floatx4 (&acc)[Ring<T, BM, BN, WM, WN, WK, NS>::FM][Ring<T, BM, BN, WM, WN, WK, NS>::FN]) {
+    floatx4 (&acc)[Ring<T, BM, BN, WM, WN, WK, NS>::FM][Ring<T, BM, BN, WM, WN, WK, NS>::FN],
+    unsigned long long* stamp = nullptr) {
     typedef Ring<T, BM, BN, WM, WN, WK, NS> R;
     typedef typename Mma<T>::frag F;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -103,6 +104,7 @@ __device__ __forceinline__ void ring_core(
     const int lr = lane & 15, lh = lane >> 4;
     for (int kt = 0; kt < nk; ++kt) {
         rc_wait_sel<R::IA + R::IB, NS - 2>(nk - 1 - kt);
+        if (stamp && kt < 30) stamp[1 + kt] = __builtin_amdgcn_s_memrealtime();
         __builtin_amdgcn_s_barrier();
         if (kt + NS - 1 < nk) issue(kt + NS - 1);
         const char* ia = smem + (kt % NS) * R::SLOT;
