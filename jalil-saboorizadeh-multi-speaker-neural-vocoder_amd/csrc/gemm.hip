@@ -22,6 +22,7 @@ struct GemmArgs {
     const void* mask;  // optional relu-backward mask (input dtype): out = 0 where mask <= 0
     int64_t ldmask;
     unsigned long long* diag;   // skinny path timing diagnostics (workgroup 0, wave 0), or null
+    int vecC;          // skinny path: C (and Cin / bias / mask) allow 4-column vector access
 };
 
 template <typename T, typename TO, int BM, int BN, int KS, int WM, int WN, int WK, bool KCA,
@@ -92,9 +93,57 @@ __global__ __launch_bounds__(256) void skinny_kernel(GemmArgs g) {
     if (st) st[31] = __builtin_amdgcn_s_memrealtime();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = wave % WM, wn = (wave / WM) % WN, wk = wave / (WM * WN);
-    if (wk != 0) return;
     TO* Cp = reinterpret_cast<TO*>(g.C);
     const T* mask = reinterpret_cast<const T*>(g.mask);
+    if (g.vecC) {
+        // Staged epilogue: the tile goes through LDS (the ring is free) so the stores are
+        // whole row segments, 4 columns per lane (16 B fp32 / 8 B bf16), instead of 4-byte
+        // scalars scattered over 4 rows per instruction (5.8 of 14.8 us at 128 x 16384 x 1024)
+        constexpr int P = BN + 4;                   // LDS pitch (floats): 4 rows apart -> +16 banks
+        static_assert(BM * P * 4 <= R::LDS, "staged epilogue tile must fit the ring");
+        float* Tl = reinterpret_cast<float*>(smem);
+        if (wk == 0) {
+#pragma unroll
+            for (int fm = 0; fm < R::FM; ++fm)
+#pragma unroll
+                for (int fn = 0; fn < R::FN; ++fn)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        Tl[(wm * R::FM * 16 + fm * 16 + (lane >> 4) * 4 + i) * P + wn * R::FN * 16 +
+                           fn * 16 + (lane & 15)] = g.alpha * acc[fm][fn][i];
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < BM * BN / 4; e += 256) {
+            const int r = e / (BN / 4), c = (e % (BN / 4)) * 4;
+            const int row = m0 + r, col = n0 + c;
+            if (row >= g.M || col >= g.N) continue;     // N % 4 == 0: a quad is in or out
+            floatx4 v = *reinterpret_cast<const floatx4*>(Tl + r * P + c);
+            if (g.beta != 0.f) {
+                const floatx4 ci = *reinterpret_cast<const floatx4*>(g.Cin + (int64_t)row * g.ldcin + col);
+                v += g.beta * ci;
+            }
+            if (g.bias_mode == 1) v += *reinterpret_cast<const floatx4*>(g.bias + col);
+            else if (g.bias_mode == 2) v += g.bias[row];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (g.relu) v[j] = fmaxf(v[j], 0.f);
+                if (mask && !(to_f(mask[(int64_t)row * g.ldmask + col + j]) > 0.f)) v[j] = 0.f;
+            }
+            TO* cp = Cp + (int64_t)row * g.ldc + col;
+            if constexpr (sizeof(TO) == 4) {
+                *reinterpret_cast<floatx4*>(cp) = v;
+            } else {
+                const uint32_t lo = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(v[0])) |
+                                    ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(v[1])) << 16);
+                const uint32_t hi = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(v[2])) |
+                                    ((uint32_t)__bfloat16_as_ushort(__float2bfloat16(v[3])) << 16);
+                *reinterpret_cast<uint2*>(cp) = make_uint2(lo, hi);
+            }
+        }
+        if (st) st[32] = __builtin_amdgcn_s_memrealtime();
+        return;
+    }
+    if (wk != 0) return;
 #pragma unroll
     for (int fm = 0; fm < R::FM; ++fm)
 #pragma unroll
@@ -282,6 +331,17 @@ int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int 
     g.bias_mode = bias ? bias_mode : 0; g.relu = relu;
     g.mask = mask; g.ldmask = ldmask;
     g.diag = skinny_diag();
+    {
+        // 4-column vector epilogue (skinny path): every row of C (and Cin, mask) starts on a
+        // 4-element boundary and N is whole quads
+        const int eo = out_dtype == SRNN_F32 ? 4 : 2;
+        auto al = [](const void* p, int64_t ld, int b) {
+            return p == nullptr || (((uintptr_t)p % b == 0) && (ld % 4 == 0));
+        };
+        g.vecC = N % 4 == 0 && al(C, ldc, 4 * eo) && (beta == 0.f || al(Cin, ldcin, 16)) &&
+                 (bias == nullptr || bias_mode != 1 || (uintptr_t)bias % 16 == 0) &&
+                 al(mask, ldmask, 4 * es) && batch == 1 && env_flag("SRNN_SKINNY_VEC", 1);
+    }
     auto aligned = [&](const void* p, int64_t ld, int64_t st) {
         return ((uintptr_t)p % 16 == 0) && (ld % E == 0) && (batch == 1 || st % E == 0);
     };
