@@ -126,92 +126,103 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     // input projections are loaded one step ahead: issued at the end of step t-1, they land
     // during step t's hand-off wait instead of stalling its epilogue
     const float* gp0 = a.gi + (int64_t)b * a.ldgi;
-    float gir = gp0[unit], giz = gp0[D + unit], gin = gp0[2 * D + unit];
-    for (int t = 0; t < a.Fr; ++t) {
-        floatx4 acc[NT];
-#pragma unroll
-        for (int i = 0; i < NT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-        if (wave < KW) {
-            const uint32_t tag = (uint32_t)(t + 1);
-            const uint32_t base = (uint32_t)(((size_t)(t & 1) * bufw +
-                                              (size_t)(g * RG + lrow) * DG) * 8);
-            uint32_t w[UPW][4];
-            int spins = 0;
-            for (;;) {
-                // every load unconditional (clamped unit), so all 2 x UPW are in flight at
-                // once; a branch per unit would put a vmcnt(0) between them
-                uint4 x[UPW][2];
-#pragma unroll
-                for (int j = 0; j < UPW; ++j) {
-                    const int u = min(wave + NW * j, NU - 1);
-                    const uint32_t off = base + (uint32_t)((u * UK + (lane >> 4) * 8) / 2) * 8u;
-                    x[j][0] = hx_get2(rx, off);
-                    x[j][1] = hx_get2(rx, off + 16);
+    // input projections: step t + 1's are issued as soon as step t's hand-off has landed
+    // (vmcnt is in order: issued after the publish they made the next hand-off check wait for
+    // their latency too), into the other of two register sets used alternately (loop unrolled
+    // by two: a copy into the current set would wait for the loads at once)
+    struct Gi { float r, z, n; };
+    Gi ga{gp0[unit], gp0[D + unit], gp0[2 * D + unit]}, gb{0.f, 0.f, 0.f};
+    auto fetch_gi = [&](int t, Gi& nx) {
+        const float* gp = a.gi + (int64_t)b * a.ldgi + (int64_t)min(t + 1, a.Fr - 1) * a.sgi;
+        nx.r = gp[unit]; nx.z = gp[D + unit]; nx.n = gp[2 * D + unit];
+    };
+    auto step = [&](int t, const Gi& cu, Gi& nx) {
+            floatx4 acc[NT];
+    #pragma unroll
+            for (int i = 0; i < NT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+            if (wave >= KW) fetch_gi(t, nx);
+            if (wave < KW) {
+                const uint32_t tag = (uint32_t)(t + 1);
+                const uint32_t base = (uint32_t)(((size_t)(t & 1) * bufw +
+                                                  (size_t)(g * RG + lrow) * DG) * 8);
+                uint32_t w[UPW][4];
+                int spins = 0;
+                for (;;) {
+                    // every load unconditional (clamped unit), so all 2 x UPW are in flight at
+                    // once; a branch per unit would put a vmcnt(0) between them
+                    uint4 x[UPW][2];
+    #pragma unroll
+                    for (int j = 0; j < UPW; ++j) {
+                        const int u = min(wave + NW * j, NU - 1);
+                        const uint32_t off = base + (uint32_t)((u * UK + (lane >> 4) * 8) / 2) * 8u;
+                        x[j][0] = hx_get2(rx, off);
+                        x[j][1] = hx_get2(rx, off + 16);
+                    }
+                    bool ok = true;
+    #pragma unroll
+                    for (int j = 0; j < UPW; ++j) {
+                        const bool v = wave + NW * j < NU;
+                        w[j][0] = v ? x[j][0].x : 0u; w[j][1] = v ? x[j][0].z : 0u;
+                        w[j][2] = v ? x[j][1].x : 0u; w[j][3] = v ? x[j][1].z : 0u;
+                        ok &= !v || ((x[j][0].y == tag) & (x[j][0].w == tag) & (x[j][1].y == tag) &
+                                     (x[j][1].w == tag));
+                    }
+                    if (__all(ok)) break;
+                    if (hx_spin_fail(spins, a.err, lane, a.poll_sleep, a.spin_limit)) break;
                 }
-                bool ok = true;
-#pragma unroll
+                fetch_gi(t, nx);
+                GX_STAMP();
+    #pragma unroll
                 for (int j = 0; j < UPW; ++j) {
-                    const bool v = wave + NW * j < NU;
-                    w[j][0] = v ? x[j][0].x : 0u; w[j][1] = v ? x[j][0].z : 0u;
-                    w[j][2] = v ? x[j][1].x : 0u; w[j][3] = v ? x[j][1].z : 0u;
-                    ok &= !v || ((x[j][0].y == tag) & (x[j][0].w == tag) & (x[j][1].y == tag) &
-                                 (x[j][1].w == tag));
+                    const uint4 v = make_uint4(w[j][0], w[j][1], w[j][2], w[j][3]);
+                    bf16x8 af;
+                    __builtin_memcpy(&af, &v, 16);
+    #pragma unroll
+                    for (int i = 0; i < NT; ++i) Mma<bf16>::run(acc[i], af, wf[j][i]);
                 }
-                if (__all(ok)) break;
-                if (hx_spin_fail(spins, a.err, lane, a.poll_sleep, a.spin_limit)) break;
+    #pragma unroll
+                for (int i = 0; i < NT; ++i) red[(wave * NT + i) * 64 + lane] = acc[i];
             }
             GX_STAMP();
-#pragma unroll
-            for (int j = 0; j < UPW; ++j) {
-                const uint4 v = make_uint4(w[j][0], w[j][1], w[j][2], w[j][3]);
-                bf16x8 af;
-                __builtin_memcpy(&af, &v, 16);
-#pragma unroll
-                for (int i = 0; i < NT; ++i) Mma<bf16>::run(acc[i], af, wf[j][i]);
+            __syncthreads();
+            GX_STAMP();
+            float gh[3];
+            {
+                const int ln = (r >> 2) * 16 + (uu & 15), ii = r & 3;
+    #pragma unroll
+                for (int gt = 0; gt < 3; ++gt) {
+                    const int tile = 2 * gt + (uu >> 4);
+                    float v = 0.f;
+                    float pr[NW];
+                    #pragma unroll
+                    for (int kw = 0; kw < NW; ++kw)
+                        pr[kw] = red[(min(kw, KW - 1) * NT + tile) * 64 + ln][ii];
+                    #pragma unroll
+                    for (int kw = 0; kw < NW; ++kw) v += kw < KW ? pr[kw] : 0.f;
+                    gh[gt] = v;
+                }
             }
-#pragma unroll
-            for (int i = 0; i < NT; ++i) red[(wave * NT + i) * 64 + lane] = acc[i];
-        }
-        GX_STAMP();
-        __syncthreads();
-        GX_STAMP();
-        float gh[3];
-        {
-            const int ln = (r >> 2) * 16 + (uu & 15), ii = r & 3;
-#pragma unroll
-            for (int gt = 0; gt < 3; ++gt) {
-                const int tile = 2 * gt + (uu >> 4);
-                float v = 0.f;
-                float pr[NW];
-                #pragma unroll
-                for (int kw = 0; kw < NW; ++kw)
-                    pr[kw] = red[(min(kw, KW - 1) * NT + tile) * 64 + ln][ii];
-                #pragma unroll
-                for (int kw = 0; kw < NW; ++kw) v += kw < KW ? pr[kw] : 0.f;
-                gh[gt] = v;
+            const float ghr = gh[0] + bhr, ghz = gh[1] + bhz, ghn = gh[2] + bhn;
+            const float rr = 1.0f / (1.0f + expf(-(ghr + cu.r)));
+            const float zz = 1.0f / (1.0f + expf(-(ghz + cu.z)));
+            const float nn = tanhf(cu.n + ghn * rr);
+            const float hn = (hprev - nn) * zz + nn;
+            hprev = hn;
+            publish(t, hn);
+            GX_STAMP();
+            if (wr) {
+                const int64_t o = (int64_t)b * a.ldo + (int64_t)t * a.so + unit;
+                a.out[o] = hn;
+                a.out_lp[o] = __float2bfloat16(hn);
+                float* gt = a.gates + (int64_t)b * a.ldg + (int64_t)t * a.sg;
+                gt[unit] = rr; gt[D + unit] = zz; gt[2 * D + unit] = nn; gt[3 * D + unit] = ghn;
             }
-        }
-        const float ghr = gh[0] + bhr, ghz = gh[1] + bhz, ghn = gh[2] + bhn;
-        const float rr = 1.0f / (1.0f + expf(-(ghr + gir)));
-        const float zz = 1.0f / (1.0f + expf(-(ghz + giz)));
-        const float nn = tanhf(gin + ghn * rr);
-        const float hn = (hprev - nn) * zz + nn;
-        hprev = hn;
-        publish(t, hn);
-        {
-            const float* gp = a.gi + (int64_t)b * a.ldgi + (int64_t)min(t + 1, a.Fr - 1) * a.sgi;
-            gir = gp[unit]; giz = gp[D + unit]; gin = gp[2 * D + unit];
-        }
-        GX_STAMP();
-        if (wr) {
-            const int64_t o = (int64_t)b * a.ldo + (int64_t)t * a.so + unit;
-            a.out[o] = hn;
-            a.out_lp[o] = __float2bfloat16(hn);
-            float* gt = a.gates + (int64_t)b * a.ldg + (int64_t)t * a.sg;
-            gt[unit] = rr; gt[D + unit] = zz; gt[2 * D + unit] = nn; gt[3 * D + unit] = ghn;
-        }
-        __syncthreads();                       // red is rewritten next step
-        GX_STAMP();
+            __syncthreads();                       // red is rewritten next step
+            GX_STAMP();
+    };
+    for (int t = 0; t < a.Fr; t += 2) {
+        step(t, ga, gb);
+        if (t + 1 < a.Fr) step(t + 1, gb, ga);
     }
 #undef GX_STAMP
     gx_note_failure(a.err, a.sticky);
