@@ -468,9 +468,12 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             };
             x0 = hx_get2(rxz, zoff);
             x1 = hx_get2(rxz, zoff + 16);
-            // the row's noise is drawn under the z hand-off (first poll in flight)
-            const floatx4 lq = valid ? log_noise(sample_noise(a.noise, a.seed, B, b, i - a.L, lane))
-                                     : floatx4{0.f, 0.f, 0.f, 0.f};
+            // the row's noise: precomputed by gen_noise_kernel (loaded under the z hand-off)
+            // or drawn here, under the first poll
+            floatx4 lq = floatx4{0.f, 0.f, 0.f, 0.f};
+            if (valid)
+                lq = a.lq ? *reinterpret_cast<const floatx4*>(a.lq + ((int64_t)s * B + b) * Q + 4 * lane)
+                          : log_noise(sample_noise(a.noise, a.seed, B, b, i - a.L, lane));
             if (!zcheck()) {
                 int spins = 0;
                 for (;;) {
@@ -504,6 +507,28 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     }
 #undef GM_STAMP
 #undef GM_W
+}
+
+// log q of the draws of nsteps generation steps, one wave per (step, row)
+__global__ __launch_bounds__(256) void gen_noise_kernel(const float* __restrict__ noise,
+                                                        uint64_t seed, const int* __restrict__ base,
+                                                        int off, int nsteps, int L, int B,
+                                                        float* __restrict__ lq) {
+    const int idx = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (idx >= nsteps * B) return;
+    const int s = idx / B, b = idx - s * B;
+    const int i = *base + off + s;
+    *reinterpret_cast<floatx4*>(lq + ((int64_t)s * B + b) * gm::Q + 4 * lane) =
+        log_noise(sample_noise(noise, seed, B, b, i - L, lane));
+}
+
+int gen_noise_launch(const float* noise, uint64_t seed, const int* base, int off, int nsteps,
+                     int L, int B, float* lq, hipStream_t s) {
+    if (nsteps <= 0 || B <= 0) return 0;
+    hipLaunchKernelGGL(gen_noise_kernel, dim3(cdiv((int64_t)nsteps * B, 4)), dim3(256), 0, s,
+                       noise, seed, base, off, nsteps, L, B, lq);
+    SRNN_LAUNCH_CHECK();
+    return 0;
 }
 
 // ------------------------------------------------------------------ host side

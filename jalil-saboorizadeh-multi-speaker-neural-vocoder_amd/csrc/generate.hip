@@ -150,6 +150,7 @@ struct Bufs {
     unsigned long long* xa2;
     unsigned long long* xz;
     int* gerr;
+    float* lq;               // (FS0, B, Q) log q of the persistent launch's draws
     size_t gm_bytes;
 };
 
@@ -181,6 +182,7 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
     b->base = (int*)take(64);
     b->xa1 = b->xa2 = b->xz = nullptr;
     b->gerr = nullptr;
+    b->lq = nullptr;
     b->gm_bytes = 0;
     if (pl && pl->ok) {
         const size_t start = off;
@@ -188,6 +190,7 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
         b->xa1 = (unsigned long long*)take(pl->xa_words * 8);
         b->xa2 = (unsigned long long*)take(pl->xa_words * 8);
         b->xz = (unsigned long long*)take(pl->xz_words * 8);
+        b->lq = (float*)take((size_t)m->tier[0].frame_size * B * Q * 4);
         b->gm_bytes = off - start;
     }
     return off;
@@ -325,6 +328,11 @@ int run_block(Ctx& c, int periods) {
             a.B = c.B; a.D = m->dim; a.FS0 = m->tier[0].frame_size;
             a.xa1 = c.b.xa1; a.xa2 = c.b.xa2; a.xz = c.b.xz; a.err = c.b.gerr;
             a.census = c.b.gerr + 64;
+            if (c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
+                RET(gen_noise_launch(c.noise, c.seed, c.b.base, off, a.nsteps, c.L, c.B, c.b.lq,
+                                     c.s));
+                a.lq = c.b.lq;
+            }
             RET(gen_mlp_launch(c.pl, a, c.s));
         }
     }
