@@ -14,6 +14,7 @@
 #include "ulaw_tables.h"
 #include "../../include/samplernn_hip.h"
 #include "gen_mlp.hpp"
+#include "sampler.hpp"
 
 int srnn_mlp_l1_impl(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff,
                      const int* base, int B, int Tlen, int upper_dtype, const void* upper,
@@ -67,13 +68,35 @@ __global__ __launch_bounds__(256) void tier_input_kernel(
 // latency-bound: 6 us at in_dim 16, 23 us at 107).  Each (row, output) still accumulates
 // over s in order from 0 with the same fused multiply-adds, then + bias + add: results are
 // bit-identical to tier_input_kernel.
+// The bottom tick's launch also draws the next persistent sample loop's noise (planes
+// blockIdx.z >= 1: log q of steps *base + off + s - L, s < nsteps, one wave per (step, row)),
+// which saves that loop a launch of its own.
+struct NoiseJob {
+    const float* noise;      // (T, B, Q) Exp(1) draws, or null -> Philox(seed)
+    uint64_t seed;
+    int nsteps;              // 0: no noise work
+    float* lq;               // (nsteps, B, Q)
+};
+
 constexpr int TI_RB = 8, TI_OB = 64;
 template <typename T>
 __global__ __launch_bounds__(256) void tier_input_tiled_kernel(
     const int64_t* __restrict__ seq, int64_t ldseq, const int* __restrict__ base, int off,
     int nfs, const float* __restrict__ lut2, const float* __restrict__ cond, int n_cond, int C,
     int L, const T* __restrict__ w_in, int in_dim, const float* __restrict__ bias,
-    const float* __restrict__ add, int64_t ldadd, T* __restrict__ x, int B, int D) {
+    const float* __restrict__ add, int64_t ldadd, T* __restrict__ x, int B, int D,
+    NoiseJob nz) {
+    if (blockIdx.z > 0) {
+        const int idx = (((int)blockIdx.z - 1) * (int)(gridDim.x * gridDim.y) +
+                         (int)(blockIdx.y * gridDim.x + blockIdx.x)) * 4 + (int)(threadIdx.x >> 6);
+        const int lane = threadIdx.x & 63;
+        if (idx >= nz.nsteps * B) return;
+        const int st = idx / B, b = idx - st * B;
+        const int i = *base + off + st;
+        *reinterpret_cast<floatx4*>(nz.lq + ((int64_t)st * B + b) * 256 + 4 * lane) =
+            log_noise(sample_noise(nz.noise, nz.seed, B, b, i - L, lane));
+        return;
+    }
     extern __shared__ float tsh[];
     const int S1 = in_dim | 1;
     float* wsh = tsh;                       // [TI_OB][S1]
@@ -209,6 +232,7 @@ struct Ctx {
     float* logp;
     hipStream_t s;
     const GenMlpPlan* pl;     // persistent sample loop, or null for per-sample kernels
+    bool noise_ahead = false; // the last bottom tick's launch drew the next loop's noise
 };
 
 #define RET(x) do { int _r = (x); if (_r) return _r; } while (0)
@@ -246,17 +270,26 @@ int tier_tick(Ctx& c, int k, int off, int par) {
                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
                 attr[ai] = true;
             }
-            const dim3 grid(cdiv(D, TI_OB), cdiv(B, TI_RB));
+            NoiseJob nz{c.noise, c.seed, 0, nullptr};
+            int planes = 1;
+            if (k == 0 && c.pl && c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
+                nz.nsteps = t.frame_size;             // the persistent launch after this tick
+                nz.lq = c.b.lq;
+                const int per = cdiv(D, TI_OB) * cdiv(B, TI_RB);
+                planes = 1 + cdiv(cdiv((int64_t)nz.nsteps * B, 4), per);
+                c.noise_ahead = true;
+            }
+            const dim3 grid(cdiv(D, TI_OB), cdiv(B, TI_RB), planes);
             if (dt == SRNN_F32)
                 hipLaunchKernelGGL((tier_input_tiled_kernel<float>), grid, dim3(256), tlds, c.s,
                                    c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2,
                                    c.cond, c.n_cond, m->cond_dim, c.L, (const float*)t.w_in,
-                                   t.in_dim, bias, add, ldadd, (float*)c.b.x[k], B, D);
+                                   t.in_dim, bias, add, ldadd, (float*)c.b.x[k], B, D, nz);
             else
                 hipLaunchKernelGGL((tier_input_tiled_kernel<bf16>), grid, dim3(256), tlds, c.s,
                                    c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2,
                                    c.cond, c.n_cond, m->cond_dim, c.L, (const bf16*)t.w_in,
-                                   t.in_dim, bias, add, ldadd, (bf16*)c.b.x[k], B, D);
+                                   t.in_dim, bias, add, ldadd, (bf16*)c.b.x[k], B, D, nz);
         } else {
             const size_t lds = (size_t)t.in_dim * sizeof(float);
             if (dt == SRNN_F32)
@@ -329,8 +362,11 @@ int run_block(Ctx& c, int periods) {
             a.xa1 = c.b.xa1; a.xa2 = c.b.xa2; a.xz = c.b.xz; a.err = c.b.gerr;
             a.census = c.b.gerr + 64;
             if (c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
-                RET(gen_noise_launch(c.noise, c.seed, c.b.base, off, a.nsteps, c.L, c.B, c.b.lq,
-                                     c.s));
+                // drawn by the bottom tick's input launch just before, else by a launch here
+                if (!c.noise_ahead)
+                    RET(gen_noise_launch(c.noise, c.seed, c.b.base, off, a.nsteps, c.L, c.B,
+                                         c.b.lq, c.s));
+                c.noise_ahead = false;
                 a.lq = c.b.lq;
             }
             RET(gen_mlp_launch(c.pl, a, c.s));
