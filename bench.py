@@ -180,6 +180,20 @@ def pmc_traffic(kernel, path=os.path.join(ROOT, 'profiles', 'r02_pmc_gemm.txt'))
         return None
 
 
+def gen_traffic(path=os.path.join(ROOT, 'profiles', 'r02_pmc_gen.txt')):
+    """HBM bytes per generation step of the bf16 loop (B = 128, D = 1024, FS = [16, 4]) from the
+    committed rocprofv3 PMC passes (tools/pmc_gen.py: FETCH_SIZE kB x 2 + WRITE_SIZE kB over
+    every dispatch of the loop's kernels / samples generated)."""
+    try:
+        for line in open(path):
+            m = line.split()
+            if len(m) == 2 and m[0] == 'avg_step_bytes':
+                return int(m[1])
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def cpu_baseline(seconds_budget=20.0):
     """The oracle (torch-CPU restatement of the reference) on the host cores: a bounded
     TBPTT sample of the same workload (config B dims, T = 1024, B = 4 rows)."""
@@ -289,7 +303,9 @@ def main():
                              'peak': MI355X_HBM_TBS * 1000, 'unit': 'GB/s',
                              'frac': round(bytes_step * steps_per_s / 1e9 /
                                            (MI355X_HBM_TBS * 1000), 4),
-                             'traffic': None}}
+                             'traffic': gen_traffic() if (dname == 'bf16' and tuple(frame_sizes)
+                                                          == (16, 4) and args.gen_seqs == 128)
+                                        else None}}
 
     gen = gen_fp32 = gen_e = None
     if not args.no_gen:
