@@ -128,3 +128,25 @@ def test_persistent_static_map_mode(hip, monkeypatch):
     s0, l0 = generate(m, B, cond, spk, False, noise=noise)
     assert torch.equal(s1, s0)
     torch.testing.assert_close(l1, l0, atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize('sampler', ['philox', 'replay'])
+def test_noise_ahead_matches_in_loop_draws(hip, monkeypatch, sampler):
+    """The persistent loop's noise (log q) drawn ahead by the bottom tick's input launch is
+    the noise the loop draws itself (SRNN_GEN_NOISE_AHEAD=0): identical index streams and
+    log-probs, bf16 D = 1024 (the compiled-shape loop) and fp32."""
+    for dtype, cfgname, B in ((torch.bfloat16, 'big', 128), (torch.float32, 't3', 24)):
+        cfg = recipe.CONFIGS[cfgname]
+        m, _ = build(cfg, 13, dtype)
+        n_cond = 2
+        cond = recipe.synth_cond((B, n_cond, cfg['cond_dim']), 12)
+        spk = np.arange(B) % cfg['spk_dim']
+        L = int(np.prod(cfg['frame_sizes']))
+        kw = (dict(sampler='philox', seed=1234) if sampler == 'philox' else
+              dict(noise=torch.from_numpy(recipe.synth_noise((n_cond * L, B, 256), 21))))
+        monkeypatch.setenv('SRNN_GEN_NOISE_AHEAD', '1')
+        s1, l1 = generate(m, B, cond, spk, True, **kw)
+        monkeypatch.setenv('SRNN_GEN_NOISE_AHEAD', '0')
+        s0, l0 = generate(m, B, cond, spk, True, **kw)
+        assert torch.equal(s1, s0)
+        assert torch.equal(l1, l0)
