@@ -180,6 +180,66 @@ def pmc_traffic(kernel, path=os.path.join(ROOT, 'profiles', 'r02_pmc_gemm.txt'))
         return None
 
 
+def gru_sweep_roofline(dev, B=128, D=1024, Fr=64, reps=5):
+    """MFMA utilisation of the recurrence's hidden x hidden products (the persistent XCD-grouped
+    sweeps, gru_xcd.hip): the bottom tier's forward and backward sweep at the TBPTT step's shape
+    (bf16, B rows, Fr frames), timed with HIP events on their stream; flop = Fr x 2 x B x 3D x D
+    per sweep (the forward's W_hh h, the backward's W_hh^T dgh).  Latency-bound: one hand-off of
+    h (dgh) between the group's workgroups per step."""
+    import samplernn_hip as H
+    T = torch.bfloat16
+    g = torch.Generator(device=dev).manual_seed(3)
+    whh = (torch.randn(3 * D, D, device=dev, generator=g) * 0.03).to(T)
+    whh_t = whh.t().contiguous()
+    bhh = torch.zeros(3 * D, device=dev)
+    gi = torch.randn(B * Fr, 3 * D, device=dev, generator=g) * 0.5
+    h0 = torch.zeros(B, D, device=dev)
+    out = torch.empty(B, Fr, D, device=dev)
+    outT = torch.empty(B, Fr, D, device=dev, dtype=T)
+    gt = torch.empty(B, Fr, 4 * D, device=dev)
+    nf = H.gru_xcd_work_bytes(T, B, D)
+    nb = H.gru_xcd_bwd_work_bytes(T, B, D)
+    if not nf or not nb:
+        return None
+    wf = torch.empty(nf, device=dev, dtype=torch.uint8)
+    wb = torch.empty(nb, device=dev, dtype=torch.uint8)
+    dy = torch.randn(B, Fr, D, device=dev, generator=g) * 0.1
+    dgh = torch.empty(B, Fr, 3 * D, device=dev, dtype=T)
+    dgi = torch.empty(B, Fr, 3 * D, device=dev, dtype=T)
+    bsum = torch.empty(B, 4 * D, device=dev)
+    ddir0 = torch.empty(B, D, device=dev)
+
+    def fwd():
+        H.lib().call('srnn_gru_xcd_fwd', H.BF16, B, D, Fr, H.ptr(gi), Fr * 3 * D, 3 * D,
+                     H.ptr(h0), H.ptr(whh), H.ptr(bhh), H.ptr(out), H.ptr(outT), Fr * D, D,
+                     H.ptr(gt), Fr * 4 * D, 4 * D, H.ptr(wf), nf, H.stream())
+
+    def bwd():
+        H.lib().call('srnn_gru_xcd_bwd2', H.BF16, B, D, Fr, H.ptr(dy), Fr * D, D, H.ptr(gt),
+                     Fr * 4 * D, 4 * D, H.ptr(out), Fr * D, D, H.ptr(h0), H.ptr(whh_t), None,
+                     H.ptr(dgh), None, H.ptr(dgi), H.ptr(bsum), Fr * 3 * D, 3 * D, H.ptr(ddir0),
+                     H.ptr(wb), nb, H.stream())
+
+    res = {}
+    flop = Fr * 2.0 * B * 3 * D * D
+    for name, fn in (('fwd', fwd), ('bwd', bwd)):
+        for _ in range(2):
+            fn()
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            fn()
+        e1.record(st)
+        e1.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        tf = flop / (ms * 1e-3) / 1e12
+        res[name] = {'us_per_step': round(ms * 1e3 / Fr, 2), 'tflops': round(tf, 1),
+                     'frac': round(tf / MI355X_BF16_TFLOPS, 4)}
+    H.check_persistent_errors()
+    return res
+
+
 def gen_traffic(path=os.path.join(ROOT, 'profiles', 'r02_pmc_gen.txt')):
     """HBM bytes per generation step of the bf16 loop (B = 128, D = 1024, FS = [16, 4]) from the
     committed rocprofv3 PMC passes (tools/pmc_gen.py: FETCH_SIZE kB x 2 + WRITE_SIZE kB over
@@ -272,6 +332,14 @@ def main():
             'traffic_algorithmic': 2 * (M_ * K_ + N_ * K_ + M_ * N_),
             'kernel': 'gemm_kernel (MLP hidden layer %dx%dx%d %s, relu epilogue), %.3f ms/launch'
                       % (M_, N_, K_, args.dtype, kms)}
+    # MFMA utilisation of the GRU recurrence (north star: "MFMA utilisation for the GRU GEMMs")
+    gru = None
+    if args.dtype == 'bf16' and rows == 128:
+        gru = gru_sweep_roofline(dev)
+        if gru:
+            gru.update({'bound': 'latency (one hand-off of h / dgh per step)', 'unit': 'TFLOP/s',
+                        'peak': MI355X_BF16_TFLOPS,
+                        'kernel': 'gru_xcd_fwd/bwd_kernel, bottom tier B=128 D=1024 64 frames'})
 
     def gen_line(dname, frame_sizes=(16, 4), cond_dim=43, n_cond=None, tag='3-tier dim1024 '
                  'FS=[16,4]'):
@@ -334,7 +402,7 @@ def main():
                            'parallelism': 'dp%d' % N},
                 'tbptt_steps_per_s': round(args.steps / dt, 3),
                 'roofline': roof, 'cpu_baseline': cpu, 'gen': gen, 'gen_fp32': gen_fp32,
-                'gen_config_e': gen_e,
+                'gen_config_e': gen_e, 'gru_sweep': gru,
                 'final_loss': round(losses[-1], 4)}
         print(json.dumps(line), flush=True)
     D.barrier()
