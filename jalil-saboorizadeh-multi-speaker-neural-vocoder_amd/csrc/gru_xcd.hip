@@ -140,8 +140,12 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
             floatx4 acc[NT];
     #pragma unroll
             for (int i = 0; i < NT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-            if (wave >= KW) fetch_gi(t, nx);
-            if (wave < KW) {
+            // (UPW >= 2: NU > NW units, every wave polls -- known at compile time, so the
+            //  wait analysis sees the poll's vmcnt(0) on every path and the step's operands
+            //  from the previous step need no further wait)
+            const bool polls = UPW >= 2 || wave < KW;
+            if (!polls) fetch_gi(t, nx);
+            if (polls) {
                 const uint32_t tag = (uint32_t)(t + 1);
                 const uint32_t base = (uint32_t)(((size_t)(t & 1) * bufw +
                                                   (size_t)(g * RG + lrow) * DG) * 8);
@@ -324,7 +328,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
 #pragma unroll
         for (int i = 0; i < NTB; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
         if (has_next) {
-            if (wave < KW) {
+            if (UPW >= 2 || wave < KW) {                        // (as the forward)
                 const uint32_t tag = (uint32_t)(a.Fr - 1 - t);     // dgh_{t+1}
                 const uint32_t base = (uint32_t)((((size_t)((t + 1) & 1)) * bufw +
                                                   (size_t)(g * RG + lrow) * KG) * 8);
