@@ -213,8 +213,13 @@ static int launch_skinny_rows(const GemmArgs& g, hipStream_t s) {
 template <typename T, typename TO>
 static int launch_skinny(const GemmArgs& g, hipStream_t s) {
     if (g.M > 64 && g.M <= 128 && g.N >= 64 * 64 && env_flag("SRNN_SKINNY_ROWS", 1)) {
-        if (g.N >= 64 * 256) return launch_skinny_rows<T, TO, 64, 2, 2, 3>(g, s);
-        return launch_skinny_rows<T, TO, 32, 4, 1, 4>(g, s);
+        // the narrowest tile that keeps it to one round of <= 256 workgroups (the generation
+        // ticks: N = 4 D top upsampling, 12 D folded upper tick, 16 D / 19 D bottom tick)
+        if (cdiv(g.N, 32) <= 256) return launch_skinny_rows<T, TO, 32, 4, 1, 4>(g, s);
+        if (cdiv(g.N, 48) <= 256) return launch_skinny_rows<T, TO, 48, 4, 1, 3>(g, s);
+        if (cdiv(g.N, 64) <= 256 || cdiv(g.N, 80) > 256)
+            return launch_skinny_rows<T, TO, 64, 2, 2, 3>(g, s);
+        return launch_skinny_rows<T, TO, 80, 4, 1, 3>(g, s);
     }
     // 32 x 16 tiles (waves: 2 along M, 2 along K) unless 32 x 32 already gives 512 tiles
     const int64_t t32 = (int64_t)cdiv(g.M, 32) * cdiv(g.N, 32);

@@ -78,6 +78,19 @@ struct NoiseJob {
     float* lq;               // (nsteps, B, Q)
 };
 
+// noise plane z >= 1 of a 256-thread launch: one wave per (step, row)
+__device__ __forceinline__ void noise_plane(const NoiseJob& nz, const int* base, int off, int L,
+                                            int B) {
+    const int idx = (((int)blockIdx.z - 1) * (int)(gridDim.x * gridDim.y) +
+                     (int)(blockIdx.y * gridDim.x + blockIdx.x)) * 4 + (int)(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (idx >= nz.nsteps * B) return;
+    const int st = idx / B, b = idx - st * B;
+    const int i = *base + off + st;
+    *reinterpret_cast<floatx4*>(nz.lq + ((int64_t)st * B + b) * 256 + 4 * lane) =
+        log_noise(sample_noise(nz.noise, nz.seed, B, b, i - L, lane));
+}
+
 constexpr int TI_RB = 8, TI_OB = 64;
 template <typename T>
 __global__ __launch_bounds__(256) void tier_input_tiled_kernel(
@@ -87,14 +100,7 @@ __global__ __launch_bounds__(256) void tier_input_tiled_kernel(
     const float* __restrict__ add, int64_t ldadd, T* __restrict__ x, int B, int D,
     NoiseJob nz) {
     if (blockIdx.z > 0) {
-        const int idx = (((int)blockIdx.z - 1) * (int)(gridDim.x * gridDim.y) +
-                         (int)(blockIdx.y * gridDim.x + blockIdx.x)) * 4 + (int)(threadIdx.x >> 6);
-        const int lane = threadIdx.x & 63;
-        if (idx >= nz.nsteps * B) return;
-        const int st = idx / B, b = idx - st * B;
-        const int i = *base + off + st;
-        *reinterpret_cast<floatx4*>(nz.lq + ((int64_t)st * B + b) * 256 + 4 * lane) =
-            log_noise(sample_noise(nz.noise, nz.seed, B, b, i - L, lane));
+        noise_plane(nz, base, off, L, B);
         return;
     }
     extern __shared__ float tsh[];
@@ -141,6 +147,119 @@ __global__ __launch_bounds__(256) void tier_input_tiled_kernel(
     }
 }
 
+// ---- folded bottom tick (bf16, one GRU layer) ----------------------------------------
+// The bottom tier's tick is x = W_in a + b_in + up_upper[fi]; gi = W_ih x + b_ih; GRU;
+// up = W_up h + b_up (model.py:196-244).  With x linear in its three terms it folds to
+//     gi = Min a + G[fi],  Min = W_ih W_in (3D x nfs),
+//     G[fi] = W_ih up_upper[fi] + W_ih b_in + b_ih = Wfold[fi] h_upper + bfold[fi],
+//     Wfold[fi] = W_ih W_up_upper[fi] (3D x D),  bfold[fi] = W_ih (b_up_upper[fi] + b_in) + b_ih
+// so the upper tier's tick produces G for all its FS_upper positions with ONE skinny GEMM
+// over its h (weights (FS_upper 3D, D), folded once per call) in place of its upsampling
+// GEMM, and Min a is 16 multiply-adds per gate.  gh = W_hh h + b_hh of the NEXT tick only
+// needs this tick's h, so it rides in this tick's upsampling GEMM (weights [W_up; W_hh]:
+// the h operand is streamed once for both).  What stays between the sample loop launches
+// is a gate-update kernel and one GEMM, instead of input kernel + GRU-cell GEMM + GEMM.
+// Rounding differs from the unfolded bf16 path (x and up_upper are never rounded to bf16;
+// the folded weights are), at the same bf16 scale; fp32 models keep the unfolded tick.
+
+// Min[g][s] (row-padded to 16) = sum_o W_ih[g, o] W_in[o, s], and the folded upper-tick bias
+// bfold[j][g] = sum_o W_ih[g, o] (b_in[o] + b_up1[j D + o]) + b_ih[g], j < fs1: one wave per
+// gate row, once per generate call
+constexpr int FOLD_MAX_FS1 = 8;
+template <typename T>
+__global__ __launch_bounds__(256) void fold_input_kernel(const T* __restrict__ wih,
+                                                         const T* __restrict__ win, int nfs,
+                                                         const float* __restrict__ bin,
+                                                         const float* __restrict__ bih,
+                                                         const float* __restrict__ bup1, int fs1,
+                                                         float* __restrict__ Min,
+                                                         float* __restrict__ bfold, int G3, int D) {
+    const int g = blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (g >= G3) return;
+    constexpr int NA = 17 + FOLD_MAX_FS1;
+    float acc[NA];
+#pragma unroll
+    for (int s = 0; s < NA; ++s) acc[s] = 0.f;
+    for (int o = lane; o < D; o += 64) {
+        const float w = to_f(wih[(int64_t)g * D + o]);
+#pragma unroll
+        for (int s = 0; s < 16; ++s)
+            if (s < nfs) acc[s] += w * to_f(win[(int64_t)o * nfs + s]);
+        if (bin) acc[16] += w * bin[o];
+#pragma unroll
+        for (int j = 0; j < FOLD_MAX_FS1; ++j)
+            if (j < fs1 && bup1) acc[17 + j] += w * bup1[(int64_t)j * D + o];
+    }
+#pragma unroll
+    for (int s = 0; s < NA; ++s) acc[s] = wave_sum(acc[s]);
+    if (lane == 0) {
+#pragma unroll
+        for (int s = 0; s < 16; ++s) Min[(int64_t)g * 16 + s] = acc[s];
+        const float c0 = acc[16] + (bih ? bih[g] : 0.f);
+#pragma unroll
+        for (int j = 0; j < FOLD_MAX_FS1; ++j)
+            if (j < fs1) bfold[(int64_t)j * G3 + g] = c0 + acc[17 + j];
+    }
+}
+
+// gate update of the folded bottom tick: block = FG_RB rows x 256 units (+ noise planes)
+constexpr int FG_RB = 2;
+template <typename T>
+__global__ __launch_bounds__(256) void fold_gru_kernel(
+    const int64_t* __restrict__ seq, int64_t ldseq, const int* __restrict__ base, int off,
+    int nfs, const float* __restrict__ lut2, int L, const float* __restrict__ Min,
+    const float* __restrict__ G, int64_t ldg, const float* __restrict__ gh, int64_t ldgh,
+    const float* __restrict__ hp, float* __restrict__ hn, T* __restrict__ hn_lp, int B, int D,
+    NoiseJob nz) {
+    if (blockIdx.z > 0) {
+        noise_plane(nz, base, off, L, B);
+        return;
+    }
+    __shared__ float ash[FG_RB][16];
+    const int u = blockIdx.x * 256 + (int)threadIdx.x, b0 = blockIdx.y * FG_RB;
+    if (threadIdx.x < FG_RB * 16) {
+        const int r = threadIdx.x >> 4, s = threadIdx.x & 15;
+        const int b = min(b0 + r, B - 1);
+        const int i = *base + off;
+        // a[s] = 2 deq(seq[b, i - nfs + s]) rounded to T, as the unfolded input's operand
+        ash[r][s] = s < nfs ? to_f(from_f<T>(lut2[seq[(int64_t)b * ldseq + i - nfs + s]])) : 0.f;
+    }
+    __syncthreads();
+    if (u >= D) return;
+    floatx4 mr[4], mz[4], mn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        mr[j] = *reinterpret_cast<const floatx4*>(Min + (int64_t)u * 16 + 4 * j);
+        mz[j] = *reinterpret_cast<const floatx4*>(Min + (int64_t)(D + u) * 16 + 4 * j);
+        mn[j] = *reinterpret_cast<const floatx4*>(Min + (int64_t)(2 * D + u) * 16 + 4 * j);
+    }
+#pragma unroll
+    for (int r = 0; r < FG_RB; ++r) {
+        const int b = b0 + r;
+        if (b >= B) break;
+        const float* gr = G + (int64_t)b * ldg;
+        const float* hr = gh + (int64_t)b * ldgh;
+        float gir = gr[u], giz = gr[D + u], gin = gr[2 * D + u];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float a = ash[r][4 * j + e];
+                gir += a * mr[j][e];
+                giz += a * mz[j][e];
+                gin += a * mn[j][e];
+            }
+        const float ghr = hr[u], ghz = hr[D + u], ghn = hr[2 * D + u];
+        const float rg = 1.0f / (1.0f + expf(-(ghr + gir)));
+        const float zg = 1.0f / (1.0f + expf(-(ghz + giz)));
+        const float ng = tanhf(gin + ghn * rg);
+        const float h = hp[(int64_t)b * D + u];
+        const float v = (h - ng) * zg + ng;
+        hn[(int64_t)b * D + u] = v;
+        hn_lp[(int64_t)b * D + u] = from_f<T>(v);
+    }
+}
+
 template <typename T>
 __global__ void init_state_kernel(const float* __restrict__ h0, float* __restrict__ h,
                                   T* __restrict__ hlp, int B, int D) {
@@ -175,7 +294,24 @@ struct Bufs {
     int* gerr;
     float* lq;               // (FS0, B, Q) log q of the persistent launch's draws
     size_t gm_bytes;
+    // folded bottom tick (fold_ok): up[0] rows are [up (FS0 D) | gh of the next tick (3D)]
+    bool fold;
+    int64_t ldup0;           // row stride of up[0]
+    void* wcat;              // (FS0 D + 3D, D) [W_up; W_hh] of the bottom tier
+    float* bcat;             // [b_up; b_hh]
+    float* fmin;             // (3D, 16) W_ih W_in, rows zero-padded
+    void* wfold;             // (FS1 3D, D) W_ih0 W_up1[j]
+    float* bfold;            // (FS1 3D)
+    float* fg;               // (B, FS1 3D) G of the current upper frame
 };
+
+bool fold_ok(const SrnnModel* m) {
+    const SrnnTier& t = m->tier[0];
+    return m->dtype == SRNN_BF16 && m->n_tiers >= 2 && m->n_rnn == 1 &&
+           t.in_dim == t.n_frame_samples && t.n_frame_samples <= 16 && t.b_up &&
+           m->tier[1].frame_size <= FOLD_MAX_FS1 &&
+           env_flag("SRNN_GEN_FOLD", 1);
+}
 
 // carve (or size, if ws == nullptr) the workspace
 size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl) {
@@ -196,7 +332,22 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
                 b->h[k][l][p] = (float*)take((size_t)B * D * 4);
                 b->hlp[k][l][p] = lp ? (void*)take((size_t)B * D * es) : (void*)b->h[k][l][p];
             }
-        b->up[k] = (float*)take((size_t)B * t.frame_size * D * 4);
+        b->up[k] = (float*)take((size_t)B * (t.frame_size + 3) * D * 4);
+    }
+    b->fold = fold_ok(m);
+    b->ldup0 = (int64_t)m->tier[0].frame_size * D + (b->fold ? 3 * D : 0);
+    b->wcat = nullptr;
+    b->wfold = nullptr;
+    b->bcat = b->fmin = b->bfold = b->fg = nullptr;
+    if (b->fold) {
+        const int N0 = m->tier[0].frame_size * D + 3 * D;
+        b->wcat = take((size_t)N0 * D * es);
+        b->bcat = (float*)take((size_t)N0 * 4);
+        b->fmin = (float*)take((size_t)3 * D * 16 * 4);
+        const int F1 = m->tier[1].frame_size;
+        b->wfold = take((size_t)F1 * 3 * D * D * es);
+        b->bfold = (float*)take((size_t)F1 * 3 * D * 4);
+        b->fg = (float*)take((size_t)B * F1 * 3 * D * 4);
     }
     b->a1 = take((size_t)B * D * es);
     b->a2 = take((size_t)B * D * es);
@@ -244,6 +395,31 @@ int tier_tick(Ctx& c, int k, int off, int par) {
     const int D = m->dim, B = c.B, dt = m->dtype;
     const bool top = (k == m->n_tiers - 1);
     const bool lp = dt != SRNN_F32;
+    const int cur = par, nxt = par ^ 1;
+    if (k == 0 && c.b.fold) {
+        // folded bottom tick: gate update (gi = Min a + G[fi], gh from the last tick's GEMM),
+        // then [up | gh'] = h [W_up; W_hh]^T + [b_up; b_hh]
+        const SrnnTier& u = m->tier[1];
+        const int fi = (off / t.n_frame_samples) % u.frame_size;
+        NoiseJob nz{c.noise, c.seed, 0, nullptr};
+        const dim3 g2(cdiv(D, 256), cdiv(B, FG_RB));
+        int planes = 1;
+        if (c.pl && c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
+            nz.nsteps = t.frame_size;
+            nz.lq = c.b.lq;
+            planes = 1 + cdiv(cdiv((int64_t)nz.nsteps * B, 4), (int64_t)g2.x * g2.y);
+            c.noise_ahead = true;
+        }
+        const int64_t fs0d = (int64_t)t.frame_size * D;
+        hipLaunchKernelGGL((fold_gru_kernel<bf16>), dim3(g2.x, g2.y, planes), dim3(256), 0, c.s,
+                           c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.L,
+                           c.b.fmin, c.b.fg + (size_t)fi * 3 * D, (int64_t)u.frame_size * 3 * D,
+                           c.b.up[0] + fs0d, c.b.ldup0, c.b.h[0][0][cur], c.b.h[0][0][nxt],
+                           (bf16*)c.b.hlp[0][0][nxt], B, D, nz);
+        SRNN_LAUNCH_CHECK();
+        return linear_fwd(dt, SRNN_F32, B, (int)(fs0d + 3 * D), D, c.b.hlp[0][0][nxt], D,
+                          c.b.wcat, D, c.b.bcat, c.b.up[0], c.b.ldup0, 0, c.s);
+    }
     // 1. x = A_in . W_in^T + (top: row_bias ; lower: b_in + upper-tier conditioning row)
     {
         const float* add;
@@ -306,7 +482,6 @@ int tier_tick(Ctx& c, int k, int off, int par) {
         SRNN_LAUNCH_CHECK();
     }
     // 3. GRU layers
-    const int cur = par, nxt = par ^ 1;
     for (int l = 0; l < m->n_rnn; ++l) {
         const void* xin = l == 0 ? c.b.x[k] : c.b.hlp[k][l - 1][nxt];
         RET(srnn_gru_cell_impl(dt, B, D, D, xin, D, t.w_ih[l], t.b_ih[l], nullptr, 0,
@@ -315,6 +490,12 @@ int tier_tick(Ctx& c, int k, int off, int par) {
                                0, c.s));
     }
     // 4. LearnedUpsampling1d: up = h . W_up^T + b_up   (B, fs*D) fp32
+    if (k == 1 && c.b.fold) {
+        // feeds only the folded bottom tick: G = h . Wfold^T + bfold, (B, FS1 3D) fp32
+        return linear_fwd(dt, SRNN_F32, B, t.frame_size * 3 * D, D,
+                          c.b.hlp[k][m->n_rnn - 1][nxt], D, c.b.wfold, D, c.b.bfold, c.b.fg,
+                          (int64_t)t.frame_size * 3 * D, 0, c.s);
+    }
     RET(linear_fwd(dt, SRNN_F32, B, t.frame_size * D, D, c.b.hlp[k][m->n_rnn - 1][nxt], D, t.w_up,
                    D, t.b_up, c.b.up[k], (int64_t)t.frame_size * D, 0, c.s));
     return 0;
@@ -325,7 +506,7 @@ int mlp_step(Ctx& c, int off) {
     const int D = m->dim, Q = m->q_levels, B = c.B, dt = m->dtype;
     const int FS0 = m->tier[0].frame_size;
     RET(srnn_mlp_l1_impl(dt, m->tab, c.seq, c.ldseq, off - FS0, c.b.base, B, 1, SRNN_F32,
-                         c.b.up[0] + (size_t)(off % FS0) * D, (int64_t)FS0 * D, c.b.a1, D, D, FS0,
+                         c.b.up[0] + (size_t)(off % FS0) * D, c.b.ldup0, c.b.a1, D, D, FS0,
                          Q, c.s));
     RET(linear_fwd(dt, dt, B, D, D, c.b.a1, D, m->w_hid, D, m->b_hid, c.b.a2, D, 1, c.s));
     RET(linear_fwd(dt, SRNN_F32, B, Q, D, c.b.a2, D, m->w_out, D, m->b_out, c.b.logits, Q, 0,
@@ -354,7 +535,7 @@ int run_block(Ctx& c, int periods) {
             memset(&a, 0, sizeof(a));
             a.tab = m->tab; a.w_hid = m->w_hid; a.b_hid = m->b_hid;
             a.w_out = m->w_out; a.b_out = m->b_out;
-            a.up0 = c.b.up[0]; a.ldup = (int64_t)m->tier[0].frame_size * m->dim;
+            a.up0 = c.b.up[0]; a.ldup = c.b.ldup0;
             a.noise = c.noise; a.seed = c.seed;
             a.seq = c.seq; a.ldseq = c.ldseq; a.logp = c.logp;
             a.base = c.b.base; a.off = off; a.nsteps = m->tier[0].frame_size; a.L = c.L;
@@ -477,6 +658,39 @@ extern "C" int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const f
                                        dim3(256), 0, s, h0, c.b.h[k][l][0],
                                        (bf16*)c.b.hlp[k][l][0], B, D);
             }
+        if (!rc && c.b.fold) {
+            // folded bottom tick operands (see fold_gru_kernel), and gh of its first tick
+            const SrnnTier& t0 = m->tier[0];
+            const size_t upw = (size_t)t0.frame_size * D;
+            rc = (hipMemcpyAsync(c.b.wcat, t0.w_up, upw * D * 2, hipMemcpyDeviceToDevice, s) ||
+                  hipMemcpyAsync((char*)c.b.wcat + upw * D * 2, t0.w_hh[0], (size_t)3 * D * D * 2,
+                                 hipMemcpyDeviceToDevice, s) ||
+                  hipMemcpyAsync(c.b.bcat, t0.b_up, upw * 4, hipMemcpyDeviceToDevice, s))
+                     ? 2 : 0;
+            if (!rc)
+                rc = (t0.b_hh[0] ? hipMemcpyAsync(c.b.bcat + upw, t0.b_hh[0], (size_t)3 * D * 4,
+                                                  hipMemcpyDeviceToDevice, s)
+                                 : hipMemsetAsync(c.b.bcat + upw, 0, (size_t)3 * D * 4, s))
+                         ? 2 : 0;
+            if (rc) { srnn_set_error("generate: fold weight copy"); break; }
+            const SrnnTier& t1 = m->tier[1];
+            hipLaunchKernelGGL((fold_input_kernel<bf16>), dim3(cdiv(3 * D, 4)), dim3(256), 0, s,
+                               (const bf16*)t0.w_ih[0], (const bf16*)t0.w_in, t0.n_frame_samples,
+                               t0.b_in, t0.b_ih[0], t1.b_up, t1.frame_size, c.b.fmin, c.b.bfold,
+                               3 * D, D);
+            if (hipGetLastError() != hipSuccess) {
+                srnn_set_error("generate: fold_input launch");
+                rc = 2;
+                break;
+            }
+            // Wfold[j] = W_ih0 (3D x D) . W_up1[j] (D x D, rows j D .. j D + D - 1), bf16 out
+            rc = srnn_gemm_impl(m->dtype, m->dtype, 0, 0, 3 * D, D, D, 1.f, t0.w_ih[0], D, 0,
+                                t1.w_up, D, (int64_t)D * D, 0.f, nullptr, 0, 0, c.b.wfold, D,
+                                (int64_t)3 * D * D, nullptr, 0, 0, t1.frame_size, -1, s);
+            if (rc) break;
+            rc = linear_fwd(m->dtype, SRNN_F32, B, 3 * D, D, c.b.hlp[0][0][0], D, t0.w_hh[0], D,
+                            t0.b_hh[0], c.b.up[0] + upw, c.b.ldup0, 0, s);
+        }
         if (rc) break;
         const bool use_graph = (flags & 1) != 0;
         int done = 0;

@@ -101,6 +101,39 @@ def test_config_e_bf16_d1024(hip):
     assert err.mean().item() < 0.02, err.mean().item()
 
 
+@pytest.mark.parametrize('cfgname,D,B,persistent', [('big', 1024, 128, True),
+                                                    ('t3', 256, 24, False)])
+def test_folded_bottom_tick_bf16(hip, monkeypatch, cfgname, D, B, persistent):
+    """bf16 folded bottom tick (gi = W_ih W_in a + G[fi], gh carried by the previous tick's
+    [W_up; W_hh] GEMM) against the unfolded tick (SRNN_GEN_FOLD=0): same noise, log-probs
+    within bf16 tolerance on every step whose row prefix is still identical, and the folded
+    stream is the teacher-forced fp32 Predictor's within the same bound."""
+    cfg = dict(recipe.CONFIGS[cfgname], dim=D)
+    m, pred = build(cfg, 17, torch.bfloat16)
+    n_cond = 2
+    L = m.lookback
+    cond = recipe.synth_cond((B, n_cond, cfg['cond_dim']), 14)
+    spk = np.arange(B) % cfg['spk_dim']
+    noise = torch.from_numpy(recipe.synth_noise((n_cond * L, B, 256), 15))
+    monkeypatch.setenv('SRNN_GEN_FOLD', '1')
+    s1, l1 = generate(m, B, cond, spk, persistent, noise=noise)
+    monkeypatch.setenv('SRNN_GEN_FOLD', '0')
+    s0, l0 = generate(m, B, cond, spk, persistent, noise=noise)
+    # step t of row b is comparable while both streams agree on samples [L, L + t)
+    same = torch.cumprod((s1[:, L:] == s0[:, L:]).int(), dim=1)
+    ok = torch.cat([torch.ones(B, 1, dtype=torch.int32), same[:, :-1]], dim=1).bool()
+    err = (l1 - l0).abs()[ok]             # l: (B, steps, Q), ok: (B, steps)
+    assert err.max().item() < 0.25, err.max().item()
+    assert err.mean().item() < 0.02, err.mean().item()
+    m.compute_dtype = torch.float32
+    with torch.no_grad():
+        tf = pred(s1[:, :-1], True, torch.from_numpy(cond),
+                  torch.from_numpy(spk).reshape(-1, 1)).cpu()
+    err = (tf - l1).abs()
+    assert err.max().item() < 0.25, err.max().item()
+    assert err.mean().item() < 0.02, err.mean().item()
+
+
 def test_persistent_philox_matches_per_sample_fp32(hip):
     """Device RNG: both paths draw Philox4x32-10(seed) noise with the same counters."""
     cfg = dict(recipe.CONFIGS['t3'], dim=128)

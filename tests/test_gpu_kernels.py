@@ -333,9 +333,11 @@ def test_segsum(hip):
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('M,N,K', [(128, 1024, 1024), (67, 256, 512), (128, 40, 256),
                                    (256, 2048, 256), (128, 16384, 1024), (100, 4096, 1024),
-                                   (65, 16448, 256)])
+                                   (65, 16448, 256), (128, 19456, 1024), (120, 20480, 256),
+                                   (128, 12288, 1024)])
 def test_gemm_skinny_ring(hip, dtype, M, N, K):
-    """Skinny NT deep-ring kernel (tile 4 forces it), with the full epilogue."""
+    """Skinny NT deep-ring kernel (tile 4 forces it), with the full epilogue; N = 19456 and
+    20480 take the 80-wide tiles (the generation tick's [W_up; W_hh] GEMM), 12288 the 48-wide."""
     A, W = _rand(M, K, seed=1), _rand(N, K, seed=2)
     bias, cin, mask = _rand(N, seed=3), _rand(M, N, seed=4), _rand(M, N, seed=5)
     Ad, Wd = A.to(DEV, dtype), W.to(DEV, dtype)

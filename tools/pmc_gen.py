@@ -10,6 +10,7 @@ import sqlite3
 import sys
 
 LOOP = ('gen_mlp_kernel', 'skinny_kernel', 'gru_cell_ring_kernel', 'tier_input_tiled_kernel',
+        'fold_gru_kernel',
         'advance_kernel', 'gen_noise_kernel')
 
 
