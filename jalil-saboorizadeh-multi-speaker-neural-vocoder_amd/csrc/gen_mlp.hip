@@ -300,6 +300,17 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     const int eb = min(g * R + er, B - 1);
     const float bh = own ? a.b_hid[c0 + ec] : 0.f;
     const float bo = tid < R * NZ ? a.b_out[z0 + tid % NZ] : 0.f;
+    // the next tick's gate operands that do not depend on this launch's samples, loaded now
+    // (7 registers across the loop) so the gate update after it waits only for the LUT
+    const int tr = tid / CW, tb = g * R + tr, tu = c0 + (tid - tr * CW);
+    float tg[7];
+    if (a.tk && tr < R && tb < B && tu < D) {
+        const float* gr = a.tk->G + (int64_t)tb * a.tk->ldg;
+        const float* hr = a.tk->gh + (int64_t)tb * a.tk->ldgh;
+        tg[0] = gr[tu]; tg[1] = gr[D + tu]; tg[2] = gr[2 * D + tu];
+        tg[3] = hr[tu]; tg[4] = hr[D + tu]; tg[5] = hr[2 * D + tu];
+        tg[6] = a.tk->hp[(int64_t)tb * D + tu];
+    }
     __syncthreads();
 
     // partial a1 sum of sample i: up0 + the FS0-1 older taps.  issue_part puts every load in
@@ -504,6 +515,46 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         if (!row_wave && s + 1 < a.nsteps)
             publish_a1(i + 1, hist[er * gm::HIST + (i & (gm::HIST - 1))]);
         GM_STAMP();
+    }
+    // ---- the next bottom tick's gate update for this group's rows x this workgroup's
+    // columns (the history now holds the FS0 samples it takes; same arithmetic and order as
+    // fold_gru_kernel: gi = G + sum_s a_s Min[., s], a_s = 2 deq rounded to T)
+    if (a.tk) {
+        const GenMlpArgs::Tick* tk = a.tk;
+        asm volatile("" : "+s"(tk));            // fresh loads of the table after the loop
+        if (tr < R && tb < B && tu < D) {
+            const int inx = i0 + a.nsteps;
+            const float* mr = tk->fmin + (int64_t)tu * 16;
+            const float* mz = tk->fmin + (int64_t)(D + tu) * 16;
+            const float* mn = tk->fmin + (int64_t)(2 * D + tu) * 16;
+            floatx4 wr[4], wz[4], wn[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                wr[j] = *reinterpret_cast<const floatx4*>(mr + 4 * j);
+                wz[j] = *reinterpret_cast<const floatx4*>(mz + 4 * j);
+                wn[j] = *reinterpret_cast<const floatx4*>(mn + 4 * j);
+            }
+            float av[16];
+#pragma unroll
+            for (int s = 0; s < 16; ++s)
+                av[s] = s < FS0 ? to_f(from_f<T>(tk->lut2[hist[tr * gm::HIST +
+                                  ((inx - FS0 + s) & (gm::HIST - 1))]])) : 0.f;
+            float gir = tg[0], giz = tg[1], gin = tg[2];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    gir += av[4 * j + e] * wr[j][e];
+                    giz += av[4 * j + e] * wz[j][e];
+                    gin += av[4 * j + e] * wn[j][e];
+                }
+            const float rg = 1.0f / (1.0f + expf(-(tg[3] + gir)));
+            const float zg = 1.0f / (1.0f + expf(-(tg[4] + giz)));
+            const float ng = tanhf(gin + tg[5] * rg);
+            const float v = (tg[6] - ng) * zg + ng;
+            tk->hn[(int64_t)tb * D + tu] = v;
+            ((T*)tk->hn_lp)[(int64_t)tb * D + tu] = from_f<T>(v);
+        }
     }
 #undef GM_STAMP
 #undef GM_W

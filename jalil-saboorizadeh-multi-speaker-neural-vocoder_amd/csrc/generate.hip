@@ -10,6 +10,8 @@
 // replayed n_cond / 2 times.  Per sample: L1 gather -> hidden GEMM (relu) -> output
 // GEMM -> softmax/sampler; per tier tick: input build -> input GEMM -> GRU cell(s) ->
 // upsampling GEMM.
+#include <vector>
+
 #include "samplernn_hip_internal.hpp"
 #include "ulaw_tables.h"
 #include "../../include/samplernn_hip.h"
@@ -27,6 +29,10 @@ int srnn_gru_cell_impl(int dtype, int B, int D, int Din, const void* x, int64_t 
                        const void* h, int64_t ldh, const float* hf, int64_t ldhf, const void* whh,
                        const float* bhh, float* hout, int64_t ldho, void* hout_lp, int64_t ldhl,
                        float* gates, int64_t ldgt, hipStream_t s);
+int srnn_gru_cell_x_impl(int dtype, int B, int D, const void* x, int64_t ldx, const void* wih,
+                         const float* bih, const float* gh, int64_t ldgh, const float* hf,
+                         int64_t ldhf, float* hout, int64_t ldho, void* hout_lp, int64_t ldhl,
+                         hipStream_t s);
 
 // Fused tier input (build_input + input projection of one tier tick), one row per block:
 //   a[s] = 2*deq(seq[b, i - nfs + s]) (s < nfs) | cond[b, i/L - 1, s - nfs]   (rounded to T,
@@ -217,6 +223,26 @@ __global__ __launch_bounds__(256) void fold_gru_kernel(
     }
     __shared__ float ash[FG_RB][16];
     const int u = blockIdx.x * 256 + (int)threadIdx.x, b0 = blockIdx.y * FG_RB;
+    // every operand that does not depend on the samples is loaded first, so its latency
+    // overlaps the seq -> LUT chain below (clamped addresses, no branches)
+    const int uc = min(u, D - 1);
+    floatx4 mr[4], mz[4], mn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        mr[j] = *reinterpret_cast<const floatx4*>(Min + (int64_t)uc * 16 + 4 * j);
+        mz[j] = *reinterpret_cast<const floatx4*>(Min + (int64_t)(D + uc) * 16 + 4 * j);
+        mn[j] = *reinterpret_cast<const floatx4*>(Min + (int64_t)(2 * D + uc) * 16 + 4 * j);
+    }
+    float gv[FG_RB][6], hv[FG_RB];
+#pragma unroll
+    for (int r = 0; r < FG_RB; ++r) {
+        const int b = min(b0 + r, B - 1);
+        const float* gr = G + (int64_t)b * ldg;
+        const float* hr = gh + (int64_t)b * ldgh;
+        gv[r][0] = gr[uc]; gv[r][1] = gr[D + uc]; gv[r][2] = gr[2 * D + uc];
+        gv[r][3] = hr[uc]; gv[r][4] = hr[D + uc]; gv[r][5] = hr[2 * D + uc];
+        hv[r] = hp[(int64_t)b * D + uc];
+    }
     if (threadIdx.x < FG_RB * 16) {
         const int r = threadIdx.x >> 4, s = threadIdx.x & 15;
         const int b = min(b0 + r, B - 1);
@@ -226,20 +252,11 @@ __global__ __launch_bounds__(256) void fold_gru_kernel(
     }
     __syncthreads();
     if (u >= D) return;
-    floatx4 mr[4], mz[4], mn[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        mr[j] = *reinterpret_cast<const floatx4*>(Min + (int64_t)u * 16 + 4 * j);
-        mz[j] = *reinterpret_cast<const floatx4*>(Min + (int64_t)(D + u) * 16 + 4 * j);
-        mn[j] = *reinterpret_cast<const floatx4*>(Min + (int64_t)(2 * D + u) * 16 + 4 * j);
-    }
 #pragma unroll
     for (int r = 0; r < FG_RB; ++r) {
         const int b = b0 + r;
         if (b >= B) break;
-        const float* gr = G + (int64_t)b * ldg;
-        const float* hr = gh + (int64_t)b * ldgh;
-        float gir = gr[u], giz = gr[D + u], gin = gr[2 * D + u];
+        float gir = gv[r][0], giz = gv[r][1], gin = gv[r][2];
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -249,12 +266,11 @@ __global__ __launch_bounds__(256) void fold_gru_kernel(
                 giz += a * mz[j][e];
                 gin += a * mn[j][e];
             }
-        const float ghr = hr[u], ghz = hr[D + u], ghn = hr[2 * D + u];
+        const float ghr = gv[r][3], ghz = gv[r][4], ghn = gv[r][5];
         const float rg = 1.0f / (1.0f + expf(-(ghr + gir)));
         const float zg = 1.0f / (1.0f + expf(-(ghz + giz)));
         const float ng = tanhf(gin + ghn * rg);
-        const float h = hp[(int64_t)b * D + u];
-        const float v = (h - ng) * zg + ng;
+        const float v = (hv[r] - ng) * zg + ng;
         hn[(int64_t)b * D + u] = v;
         hn_lp[(int64_t)b * D + u] = from_f<T>(v);
     }
@@ -292,7 +308,8 @@ struct Bufs {
     unsigned long long* xa2;
     unsigned long long* xz;
     int* gerr;
-    float* lq;               // (FS0, B, Q) log q of the persistent launch's draws
+    float* lq;               // (lq_steps, B, Q) log q of the persistent launches' draws
+    int lq_steps;            // FS0, or the upper tier's period FS0 FS1 when that tick draws
     size_t gm_bytes;
     // folded bottom tick (fold_ok): up[0] rows are [up (FS0 D) | gh of the next tick (3D)]
     bool fold;
@@ -300,9 +317,11 @@ struct Bufs {
     void* wcat;              // (FS0 D + 3D, D) [W_up; W_hh] of the bottom tier
     float* bcat;             // [b_up; b_hh]
     float* fmin;             // (3D, 16) W_ih W_in, rows zero-padded
-    void* wfold;             // (FS1 3D, D) W_ih0 W_up1[j]
-    float* bfold;            // (FS1 3D)
-    float* fg;               // (B, FS1 3D) G of the current upper frame
+    void* wfold;             // (FS1 3D + 3D, D) [W_ih0 W_up1[j], j < FS1; W_hh1]
+    float* bfold;            // (FS1 3D + 3D) [bfold[j]; b_hh1]
+    GenMlpArgs::Tick* ticks; // [fi][cur]: the persistent loop's gate-update operands
+    float* fg;               // (B, ldg1): [G of the current upper frame | gh1 of the next
+    int64_t ldg1;            //  upper tick], ldg1 = FS1 3D + 3D
 };
 
 bool fold_ok(const SrnnModel* m) {
@@ -338,6 +357,8 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
     b->ldup0 = (int64_t)m->tier[0].frame_size * D + (b->fold ? 3 * D : 0);
     b->wcat = nullptr;
     b->wfold = nullptr;
+    b->ticks = nullptr;
+    b->ldg1 = 0;
     b->bcat = b->fmin = b->bfold = b->fg = nullptr;
     if (b->fold) {
         const int N0 = m->tier[0].frame_size * D + 3 * D;
@@ -345,9 +366,11 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
         b->bcat = (float*)take((size_t)N0 * 4);
         b->fmin = (float*)take((size_t)3 * D * 16 * 4);
         const int F1 = m->tier[1].frame_size;
-        b->wfold = take((size_t)F1 * 3 * D * D * es);
-        b->bfold = (float*)take((size_t)F1 * 3 * D * 4);
-        b->fg = (float*)take((size_t)B * F1 * 3 * D * 4);
+        b->ldg1 = (int64_t)(F1 + 1) * 3 * D;
+        b->wfold = take((size_t)b->ldg1 * D * es);
+        b->bfold = (float*)take((size_t)b->ldg1 * 4);
+        b->fg = (float*)take((size_t)B * b->ldg1 * 4);
+        b->ticks = (GenMlpArgs::Tick*)take((size_t)2 * F1 * sizeof(GenMlpArgs::Tick));
     }
     b->a1 = take((size_t)B * D * es);
     b->a2 = take((size_t)B * D * es);
@@ -357,6 +380,7 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
     b->xa1 = b->xa2 = b->xz = nullptr;
     b->gerr = nullptr;
     b->lq = nullptr;
+    b->lq_steps = 0;
     b->gm_bytes = 0;
     if (pl && pl->ok) {
         const size_t start = off;
@@ -364,7 +388,8 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
         b->xa1 = (unsigned long long*)take(pl->xa_words * 8);
         b->xa2 = (unsigned long long*)take(pl->xa_words * 8);
         b->xz = (unsigned long long*)take(pl->xz_words * 8);
-        b->lq = (float*)take((size_t)m->tier[0].frame_size * B * Q * 4);
+        b->lq_steps = m->tier[0].frame_size * (b->fold ? m->tier[1].frame_size : 1);
+        b->lq = (float*)take((size_t)b->lq_steps * B * Q * 4);
         b->gm_bytes = off - start;
     }
     return off;
@@ -383,7 +408,11 @@ struct Ctx {
     float* logp;
     hipStream_t s;
     const GenMlpPlan* pl;     // persistent sample loop, or null for per-sample kernels
-    bool noise_ahead = false; // the last bottom tick's launch drew the next loop's noise
+    // lq holds the draws of block-relative steps [noise_beg, noise_end): drawn ahead by the
+    // input launch of the bottom tick (FS0 steps) or, with the folded bottom tick, of the
+    // upper tier's tick (its whole period)
+    int noise_beg = 0, noise_end = -1;
+    bool gate_done = false;   // the last persistent launch did the next bottom tick's gates
 };
 
 #define RET(x) do { int _r = (x); if (_r) return _r; } while (0)
@@ -401,19 +430,19 @@ int tier_tick(Ctx& c, int k, int off, int par) {
         // then [up | gh'] = h [W_up; W_hh]^T + [b_up; b_hh]
         const SrnnTier& u = m->tier[1];
         const int fi = (off / t.n_frame_samples) % u.frame_size;
-        NoiseJob nz{c.noise, c.seed, 0, nullptr};
+        const NoiseJob nz{c.noise, c.seed, 0, nullptr};    // (the upper tick drew them)
         const dim3 g2(cdiv(D, 256), cdiv(B, FG_RB));
-        int planes = 1;
-        if (c.pl && c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
-            nz.nsteps = t.frame_size;
-            nz.lq = c.b.lq;
-            planes = 1 + cdiv(cdiv((int64_t)nz.nsteps * B, 4), (int64_t)g2.x * g2.y);
-            c.noise_ahead = true;
-        }
+        const int planes = 1;
         const int64_t fs0d = (int64_t)t.frame_size * D;
+        if (c.gate_done) {
+            // the gate update ran at the end of the last persistent launch (GenMlpArgs::tk)
+            c.gate_done = false;
+            return linear_fwd(dt, SRNN_F32, B, (int)(fs0d + 3 * D), D, c.b.hlp[0][0][nxt], D,
+                              c.b.wcat, D, c.b.bcat, c.b.up[0], c.b.ldup0, 0, c.s);
+        }
         hipLaunchKernelGGL((fold_gru_kernel<bf16>), dim3(g2.x, g2.y, planes), dim3(256), 0, c.s,
                            c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.L,
-                           c.b.fmin, c.b.fg + (size_t)fi * 3 * D, (int64_t)u.frame_size * 3 * D,
+                           c.b.fmin, c.b.fg + (size_t)fi * 3 * D, c.b.ldg1,
                            c.b.up[0] + fs0d, c.b.ldup0, c.b.h[0][0][cur], c.b.h[0][0][nxt],
                            (bf16*)c.b.hlp[0][0][nxt], B, D, nz);
         SRNN_LAUNCH_CHECK();
@@ -448,12 +477,13 @@ int tier_tick(Ctx& c, int k, int off, int par) {
             }
             NoiseJob nz{c.noise, c.seed, 0, nullptr};
             int planes = 1;
-            if (k == 0 && c.pl && c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
-                nz.nsteps = t.frame_size;             // the persistent launch after this tick
+            if (k == (c.b.fold ? 1 : 0) && c.pl && c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
+                nz.nsteps = c.b.lq_steps;             // the persistent launches after this tick
                 nz.lq = c.b.lq;
                 const int per = cdiv(D, TI_OB) * cdiv(B, TI_RB);
                 planes = 1 + cdiv(cdiv((int64_t)nz.nsteps * B, 4), per);
-                c.noise_ahead = true;
+                c.noise_beg = off;
+                c.noise_end = off + nz.nsteps;
             }
             const dim3 grid(cdiv(D, TI_OB), cdiv(B, TI_RB), planes);
             if (dt == SRNN_F32)
@@ -482,6 +512,16 @@ int tier_tick(Ctx& c, int k, int off, int par) {
         SRNN_LAUNCH_CHECK();
     }
     // 3. GRU layers
+    if (k == 1 && c.b.fold) {
+        // folded upper tick: gh carried by its last GEMM ([Wfold; W_hh1] . h)
+        const int64_t g0 = (int64_t)t.frame_size * 3 * D;
+        RET(srnn_gru_cell_x_impl(dt, B, D, c.b.x[k], D, t.w_ih[0], t.b_ih[0], c.b.fg + g0,
+                                 c.b.ldg1, c.b.h[k][0][cur], D, c.b.h[k][0][nxt], D,
+                                 c.b.hlp[k][0][nxt], D, c.s));
+        // G = h . Wfold^T + bfold and the next tick's gh1, (B, ldg1) fp32
+        return linear_fwd(dt, SRNN_F32, B, (int)c.b.ldg1, D, c.b.hlp[k][0][nxt], D, c.b.wfold,
+                          D, c.b.bfold, c.b.fg, c.b.ldg1, 0, c.s);
+    }
     for (int l = 0; l < m->n_rnn; ++l) {
         const void* xin = l == 0 ? c.b.x[k] : c.b.hlp[k][l - 1][nxt];
         RET(srnn_gru_cell_impl(dt, B, D, D, xin, D, t.w_ih[l], t.b_ih[l], nullptr, 0,
@@ -490,12 +530,6 @@ int tier_tick(Ctx& c, int k, int off, int par) {
                                0, c.s));
     }
     // 4. LearnedUpsampling1d: up = h . W_up^T + b_up   (B, fs*D) fp32
-    if (k == 1 && c.b.fold) {
-        // feeds only the folded bottom tick: G = h . Wfold^T + bfold, (B, FS1 3D) fp32
-        return linear_fwd(dt, SRNN_F32, B, t.frame_size * 3 * D, D,
-                          c.b.hlp[k][m->n_rnn - 1][nxt], D, c.b.wfold, D, c.b.bfold, c.b.fg,
-                          (int64_t)t.frame_size * 3 * D, 0, c.s);
-    }
     RET(linear_fwd(dt, SRNN_F32, B, t.frame_size * D, D, c.b.hlp[k][m->n_rnn - 1][nxt], D, t.w_up,
                    D, t.b_up, c.b.up[k], (int64_t)t.frame_size * D, 0, c.s));
     return 0;
@@ -521,6 +555,8 @@ int mlp_step(Ctx& c, int off) {
 int run_block(Ctx& c, int periods) {
     const SrnnModel* m = c.m;
     int ticks[SRNN_MAX_TIERS] = {0};
+    c.noise_end = -1;
+    c.gate_done = false;
     for (int off = 0; off < periods * c.L; ++off) {
         for (int k = m->n_tiers - 1; k >= 0; --k) {
             if (off % m->tier[k].n_frame_samples != 0) continue;
@@ -543,12 +579,23 @@ int run_block(Ctx& c, int periods) {
             a.xa1 = c.b.xa1; a.xa2 = c.b.xa2; a.xz = c.b.xz; a.err = c.b.gerr;
             a.census = c.b.gerr + 64;
             if (c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
-                // drawn by the bottom tick's input launch just before, else by a launch here
-                if (!c.noise_ahead)
+                // drawn ahead by a tick's input launch, else by a launch here
+                if (off < c.noise_beg || off + a.nsteps > c.noise_end) {
                     RET(gen_noise_launch(c.noise, c.seed, c.b.base, off, a.nsteps, c.L, c.B,
                                          c.b.lq, c.s));
-                c.noise_ahead = false;
-                a.lq = c.b.lq;
+                    c.noise_beg = off;
+                    c.noise_end = off + a.nsteps;
+                }
+                a.lq = c.b.lq + (size_t)(off - c.noise_beg) * c.B * m->q_levels;
+            }
+            // the next bottom tick's gate update rides at the end of this launch unless an
+            // upper tick (new G) comes first
+            const int nx = off + m->tier[0].frame_size;
+            if (c.b.fold && nx < periods * c.L && nx % m->tier[1].n_frame_samples != 0 &&
+                env_flag("SRNN_GEN_FUSE_GATES", 1)) {
+                const int fi = (nx / m->tier[0].n_frame_samples) % m->tier[1].frame_size;
+                a.tk = c.b.ticks + 2 * fi + (ticks[0] & 1);    // that tick's G row, cur / nxt
+                c.gate_done = true;
             }
             RET(gen_mlp_launch(c.pl, a, c.s));
         }
@@ -688,6 +735,36 @@ extern "C" int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const f
                                 t1.w_up, D, (int64_t)D * D, 0.f, nullptr, 0, 0, c.b.wfold, D,
                                 (int64_t)3 * D * D, nullptr, 0, 0, t1.frame_size, -1, s);
             if (rc) break;
+            // [W_hh1; b_hh1] after the folded rows, and gh1 of the first upper tick
+            const size_t g0 = (size_t)t1.frame_size * 3 * D;
+            rc = (hipMemcpyAsync((char*)c.b.wfold + g0 * D * 2, t1.w_hh[0], (size_t)3 * D * D * 2,
+                                 hipMemcpyDeviceToDevice, s) ||
+                  (t1.b_hh[0] ? hipMemcpyAsync(c.b.bfold + g0, t1.b_hh[0], (size_t)3 * D * 4,
+                                               hipMemcpyDeviceToDevice, s)
+                              : hipMemsetAsync(c.b.bfold + g0, 0, (size_t)3 * D * 4, s)))
+                     ? 2 : 0;
+            if (rc) { srnn_set_error("generate: fold weight copy"); break; }
+            rc = linear_fwd(m->dtype, SRNN_F32, B, 3 * D, D, c.b.hlp[1][0][0], D, t1.w_hh[0], D,
+                            t1.b_hh[0], c.b.fg + g0, c.b.ldg1, 0, s);
+            if (rc) break;
+            // gate-update operand table of the persistent loop, [fi][cur]
+            std::vector<GenMlpArgs::Tick> tt(2 * t1.frame_size);
+            for (int fi = 0; fi < t1.frame_size; ++fi)
+                for (int pc = 0; pc < 2; ++pc) {
+                    GenMlpArgs::Tick& e = tt[2 * fi + pc];
+                    e.fmin = c.b.fmin;
+                    e.G = c.b.fg + (size_t)fi * 3 * D;
+                    e.ldg = c.b.ldg1;
+                    e.gh = c.b.up[0] + upw;
+                    e.ldgh = c.b.ldup0;
+                    e.hp = c.b.h[0][0][pc];
+                    e.hn = c.b.h[0][0][pc ^ 1];
+                    e.hn_lp = c.b.hlp[0][0][pc ^ 1];
+                    e.lut2 = c.b.lut2;
+                }
+            rc = (hipMemcpyAsync(c.b.ticks, tt.data(), tt.size() * sizeof(tt[0]),
+                                 hipMemcpyHostToDevice, s) || hipStreamSynchronize(s)) ? 2 : 0;
+            if (rc) { srnn_set_error("generate: tick table upload"); break; }
             rc = linear_fwd(m->dtype, SRNN_F32, B, 3 * D, D, c.b.hlp[0][0][0], D, t0.w_hh[0], D,
                             t0.b_hh[0], c.b.up[0] + upw, c.b.ldup0, 0, s);
         }

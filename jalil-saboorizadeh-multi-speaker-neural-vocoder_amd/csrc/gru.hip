@@ -37,6 +37,8 @@ struct GruCellArgs {
     int64_t ldhl;
     float* gates;       // optional saved r|z|n|ghn, row stride ldgt (4D per row)
     int64_t ldgt;
+    const float* ghp;   // optional precomputed h.W_hh^T + b_hh (fp32), row stride ldghp: the
+    int64_t ldghp;      // h GEMM is skipped (ring kernel only)
     int B, D, Din;
     int vec_x, vec_h, vec_wih, vec_whh;
 };
@@ -124,17 +126,19 @@ __global__ __launch_bounds__(256) void gru_cell_ring_kernel(GruCellArgs a) {
     if (a.x)
         ring_core<T, 32, 48, 2, 1, 2, GRU_NS>((const T*)a.x, a.ldx, RowClamp{m0, a.B}, (const T*)a.wih,
                                          a.Din, gmap, a.Din, smem, acc_i);
-    ring_core<T, 32, 48, 2, 1, 2, GRU_NS>((const T*)a.h, a.ldh, RowClamp{m0, a.B}, (const T*)a.whh, a.D,
-                                     gmap, a.D, smem, acc_h);
+    if (!a.ghp)
+        ring_core<T, 32, 48, 2, 1, 2, GRU_NS>((const T*)a.h, a.ldh, RowClamp{m0, a.B},
+                                             (const T*)a.whh, a.D, gmap, a.D, smem, acc_h);
     if (a.x) ring_reduce<T, 32, 48, 2, 1, 2, GRU_NS>(smem, acc_i);
-    ring_reduce<T, 32, 48, 2, 1, 2, GRU_NS>(smem, acc_h);
+    if (!a.ghp) ring_reduce<T, 32, 48, 2, 1, 2, GRU_NS>(smem, acc_h);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wm = wave % 2, wk = wave / 2;
     if (wk != 0) return;
     const int u = u0 + (lane & 15);
     if (u >= a.D) return;
     const int D = a.D;
-    const float bhr = a.bhh[u], bhz = a.bhh[D + u], bhn = a.bhh[2 * D + u];
+    const float bhr = a.ghp ? 0.f : a.bhh[u], bhz = a.ghp ? 0.f : a.bhh[D + u];
+    const float bhn = a.ghp ? 0.f : a.bhh[2 * D + u];
     float bir = 0.f, biz = 0.f, bin = 0.f;
     if (a.x) { bir = a.bih[u]; biz = a.bih[D + u]; bin = a.bih[2 * D + u]; }
 #pragma unroll
@@ -148,9 +152,13 @@ __global__ __launch_bounds__(256) void gru_cell_ring_kernel(GruCellArgs a) {
             const float* g = a.gi + (int64_t)row * a.ldgi;
             gir = g[u]; giz = g[D + u]; gin = g[2 * D + u];
         }
-        const float ghr = acc_h[0][0][i] + bhr;
-        const float ghz = acc_h[0][1][i] + bhz;
-        const float ghn = acc_h[0][2][i] + bhn;
+        float ghr, ghz, ghn;
+        if (a.ghp) {
+            const float* g = a.ghp + (int64_t)row * a.ldghp;
+            ghr = g[u]; ghz = g[D + u]; ghn = g[2 * D + u];
+        } else {
+            ghr = acc_h[0][0][i] + bhr; ghz = acc_h[0][1][i] + bhz; ghn = acc_h[0][2][i] + bhn;
+        }
         const float r = 1.0f / (1.0f + expf(-(ghr + gir)));
         const float z = 1.0f / (1.0f + expf(-(ghz + giz)));
         const float n = tanhf(gin + ghn * r);
@@ -171,6 +179,7 @@ static int launch_cell(GruCellArgs& a, hipStream_t s) {
     const int es = (int)sizeof(T);
     const bool ring = a.D % R::KB == 0 && (!a.x || a.Din % R::KB == 0) && a.vec_h && a.vec_whh &&
                       (!a.x || (a.vec_x && a.vec_wih));
+    SRNN_REQUIRE(ring || !a.ghp, "gru_cell: precomputed gh needs the ring shape");
     if (ring) {
         static bool attr = false;
         if (!attr) {
@@ -205,11 +214,35 @@ int srnn_gru_cell_impl(int dtype, int B, int D, int Din, const void* x, int64_t 
     a.h = h; a.ldh = ldh; a.hf = hf; a.ldhf = ldhf; a.whh = whh; a.bhh = bhh;
     a.hout = hout; a.ldho = ldho; a.hout_lp = hout_lp; a.ldhl = ldhl;
     a.gates = gates; a.ldgt = ldgt; a.B = B; a.D = D; a.Din = Din;
+    a.ghp = nullptr; a.ldghp = 0;
     a.vec_x = x ? al16(x, ldx, es) : 0;
     a.vec_h = al16(h, ldh, es);
     a.vec_wih = x ? al16(wih, Din, es) : 0;
     a.vec_whh = al16(whh, D, es);
     // 32-row tiles give >= 256 workgroups at B = 128, D = 1024
+    if (dtype == SRNN_F32) return launch_cell<float, 32>(a, s);
+    return launch_cell<bf16, 32>(a, s);
+}
+
+// GRU cell with h . W_hh^T + b_hh precomputed (the generation loop's folded upper tick carries
+// it in the previous tick's upsampling GEMM): x . W_ih^T + b_ih on MFMA, then the gate update
+int srnn_gru_cell_x_impl(int dtype, int B, int D, const void* x, int64_t ldx, const void* wih,
+                         const float* bih, const float* gh, int64_t ldgh, const float* hf,
+                         int64_t ldhf, float* hout, int64_t ldho, void* hout_lp, int64_t ldhl,
+                         hipStream_t s) {
+    SRNN_REQUIRE(B > 0 && D > 0 && x && gh, "gru_cell_x: bad args");
+    const int es = dtype == SRNN_F32 ? 4 : 2;
+    GruCellArgs a;
+    memset(&a, 0, sizeof(a));
+    a.x = x; a.ldx = ldx; a.wih = wih; a.bih = bih;
+    a.hf = hf; a.ldhf = ldhf;
+    a.hout = hout; a.ldho = ldho; a.hout_lp = hout_lp; a.ldhl = ldhl;
+    a.ghp = gh; a.ldghp = ldgh;
+    a.B = B; a.D = D; a.Din = D;
+    a.vec_x = al16(x, ldx, es);
+    a.vec_h = 1;
+    a.vec_wih = al16(wih, D, es);
+    a.vec_whh = 1;
     if (dtype == SRNN_F32) return launch_cell<float, 32>(a, s);
     return launch_cell<bf16, 32>(a, s);
 }
