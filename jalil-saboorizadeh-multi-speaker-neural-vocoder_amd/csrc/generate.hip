@@ -29,10 +29,10 @@ int srnn_gru_cell_impl(int dtype, int B, int D, int Din, const void* x, int64_t 
                        const void* h, int64_t ldh, const float* hf, int64_t ldhf, const void* whh,
                        const float* bhh, float* hout, int64_t ldho, void* hout_lp, int64_t ldhl,
                        float* gates, int64_t ldgt, hipStream_t s);
-int srnn_gru_cell_x_impl(int dtype, int B, int D, const void* x, int64_t ldx, const void* wih,
-                         const float* bih, const float* gh, int64_t ldgh, const float* hf,
-                         int64_t ldhf, float* hout, int64_t ldho, void* hout_lp, int64_t ldhl,
-                         hipStream_t s);
+int srnn_gru_cell_x_impl(int dtype, int B, int D, int Din, const void* x, int64_t ldx,
+                         const void* wih, const float* bih, const float* gadd, int64_t ldgadd,
+                         const float* gh, int64_t ldgh, const float* hf, int64_t ldhf, float* hout,
+                         int64_t ldho, void* hout_lp, int64_t ldhl, hipStream_t s);
 
 // Fused tier input (build_input + input projection of one tier tick), one row per block:
 //   a[s] = 2*deq(seq[b, i - nfs + s]) (s < nfs) | cond[b, i/L - 1, s - nfs]   (rounded to T,
@@ -276,6 +276,30 @@ __global__ __launch_bounds__(256) void fold_gru_kernel(
     }
 }
 
+// Input row of the folded top tick: a[b][s] = 2 deq(seq[b, i - nfs + s]) (s < nfs) |
+// cond[b, i/L - 1, s - nfs] (s < in_dim) | 0 (s < AP), rounded to T as the unfolded input's
+// GEMM operand; gi = a . Min1^T + P1[b] then replaces x = W_in a + row_bias, gi = W_ih x + b_ih
+// (Min1 = W_ih W_in, P1 = W_ih row_bias + b_ih, folded once per call).  Two rows per block;
+// planes blockIdx.z >= 1 draw the noise of the persistent launches of the tick's period.
+constexpr int TA_AP = 128;
+template <typename T>
+__global__ __launch_bounds__(256) void tier_a_kernel(
+    const int64_t* __restrict__ seq, int64_t ldseq, const int* __restrict__ base, int off,
+    int nfs, const float* __restrict__ lut2, const float* __restrict__ cond, int n_cond, int C,
+    int L, int in_dim, T* __restrict__ a, int B, NoiseJob nz) {
+    if (blockIdx.z > 0) {
+        noise_plane(nz, base, off, L, B);
+        return;
+    }
+    const int b = blockIdx.x * 2 + (int)(threadIdx.x >> 7), s = threadIdx.x & 127;
+    if (b >= B) return;
+    const int i = *base + off;
+    float v = 0.f;
+    if (s < nfs) v = lut2[seq[(int64_t)b * ldseq + i - nfs + s]];
+    else if (s < in_dim) v = cond[((int64_t)b * n_cond + (i / L - 1)) * C + (s - nfs)];
+    a[(int64_t)b * TA_AP + s] = from_f<T>(v);
+}
+
 template <typename T>
 __global__ void init_state_kernel(const float* __restrict__ h0, float* __restrict__ h,
                                   T* __restrict__ hlp, int B, int D) {
@@ -287,6 +311,11 @@ __global__ void init_state_kernel(const float* __restrict__ h0, float* __restric
 }
 
 __global__ void advance_kernel(int* base, int by) { *base += by; }
+
+__global__ void copy_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, int n) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < n) dst[e] = from_f<bf16>(src[e]);
+}
 
 namespace {
 
@@ -320,6 +349,11 @@ struct Bufs {
     void* wfold;             // (FS1 3D + 3D, D) [W_ih0 W_up1[j], j < FS1; W_hh1]
     float* bfold;            // (FS1 3D + 3D) [bfold[j]; b_hh1]
     GenMlpArgs::Tick* ticks; // [fi][cur]: the persistent loop's gate-update operands
+    // folded top tick (fold_top: two tiers, the upper one is the top)
+    bool fold_top;
+    void* min1;              // (3D, TA_AP) W_ih1 W_in1, zero columns past in_dim
+    float* p1;               // (B, 3D) W_ih1 row_bias + b_ih1
+    void* atop;              // (B, TA_AP) the top tick's input row
     float* fg;               // (B, ldg1): [G of the current upper frame | gh1 of the next
     int64_t ldg1;            //  upper tick], ldg1 = FS1 3D + 3D
 };
@@ -358,6 +392,9 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
     b->wcat = nullptr;
     b->wfold = nullptr;
     b->ticks = nullptr;
+    b->fold_top = false;
+    b->min1 = b->atop = nullptr;
+    b->p1 = nullptr;
     b->ldg1 = 0;
     b->bcat = b->fmin = b->bfold = b->fg = nullptr;
     if (b->fold) {
@@ -371,6 +408,13 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
         b->bfold = (float*)take((size_t)b->ldg1 * 4);
         b->fg = (float*)take((size_t)B * b->ldg1 * 4);
         b->ticks = (GenMlpArgs::Tick*)take((size_t)2 * F1 * sizeof(GenMlpArgs::Tick));
+        b->fold_top = m->n_tiers == 2 && m->tier[1].in_dim <= TA_AP &&
+                      env_flag("SRNN_GEN_FOLD_TOP", 1);
+        if (b->fold_top) {
+            b->min1 = take((size_t)3 * D * TA_AP * es);
+            b->p1 = (float*)take((size_t)B * 3 * D * 4);
+            b->atop = take((size_t)B * TA_AP * es);
+        }
     }
     b->a1 = take((size_t)B * D * es);
     b->a2 = take((size_t)B * D * es);
@@ -449,6 +493,30 @@ int tier_tick(Ctx& c, int k, int off, int par) {
         return linear_fwd(dt, SRNN_F32, B, (int)(fs0d + 3 * D), D, c.b.hlp[0][0][nxt], D,
                           c.b.wcat, D, c.b.bcat, c.b.up[0], c.b.ldup0, 0, c.s);
     }
+    if (k == 1 && c.b.fold_top) {
+        // folded top tick: a (+ the period's noise) -> gi = a Min1^T + P1, gh1 carried ->
+        // [G | gh1'] = h [Wfold; W_hh1]^T + [bfold; b_hh1]
+        NoiseJob nz{c.noise, c.seed, 0, nullptr};
+        const int gx = cdiv(B, 2);
+        int planes = 1;
+        if (c.pl && c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
+            nz.nsteps = c.b.lq_steps;
+            nz.lq = c.b.lq;
+            planes = 1 + cdiv(cdiv((int64_t)nz.nsteps * B, 4), gx);
+            c.noise_beg = off;
+            c.noise_end = off + nz.nsteps;
+        }
+        hipLaunchKernelGGL((tier_a_kernel<bf16>), dim3(gx, 1, planes), dim3(256), 0, c.s, c.seq,
+                           c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.cond, c.n_cond,
+                           m->cond_dim, c.L, t.in_dim, (bf16*)c.b.atop, B, nz);
+        SRNN_LAUNCH_CHECK();
+        const int64_t g0 = (int64_t)t.frame_size * 3 * D;
+        RET(srnn_gru_cell_x_impl(dt, B, D, TA_AP, c.b.atop, TA_AP, c.b.min1, nullptr, c.b.p1,
+                                 3 * D, c.b.fg + g0, c.b.ldg1, c.b.h[k][0][cur], D,
+                                 c.b.h[k][0][nxt], D, c.b.hlp[k][0][nxt], D, c.s));
+        return linear_fwd(dt, SRNN_F32, B, (int)c.b.ldg1, D, c.b.hlp[k][0][nxt], D, c.b.wfold,
+                          D, c.b.bfold, c.b.fg, c.b.ldg1, 0, c.s);
+    }
     // 1. x = A_in . W_in^T + (top: row_bias ; lower: b_in + upper-tier conditioning row)
     {
         const float* add;
@@ -515,8 +583,8 @@ int tier_tick(Ctx& c, int k, int off, int par) {
     if (k == 1 && c.b.fold) {
         // folded upper tick: gh carried by its last GEMM ([Wfold; W_hh1] . h)
         const int64_t g0 = (int64_t)t.frame_size * 3 * D;
-        RET(srnn_gru_cell_x_impl(dt, B, D, c.b.x[k], D, t.w_ih[0], t.b_ih[0], c.b.fg + g0,
-                                 c.b.ldg1, c.b.h[k][0][cur], D, c.b.h[k][0][nxt], D,
+        RET(srnn_gru_cell_x_impl(dt, B, D, D, c.b.x[k], D, t.w_ih[0], t.b_ih[0], nullptr, 0,
+                                 c.b.fg + g0, c.b.ldg1, c.b.h[k][0][cur], D, c.b.h[k][0][nxt], D,
                                  c.b.hlp[k][0][nxt], D, c.s));
         // G = h . Wfold^T + bfold and the next tick's gh1, (B, ldg1) fp32
         return linear_fwd(dt, SRNN_F32, B, (int)c.b.ldg1, D, c.b.hlp[k][0][nxt], D, c.b.wfold,
@@ -765,6 +833,22 @@ extern "C" int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const f
             rc = (hipMemcpyAsync(c.b.ticks, tt.data(), tt.size() * sizeof(tt[0]),
                                  hipMemcpyHostToDevice, s) || hipStreamSynchronize(s)) ? 2 : 0;
             if (rc) { srnn_set_error("generate: tick table upload"); break; }
+            if (c.b.fold_top) {
+                // Min1 = W_ih1 (3D x D) . W_in1 (D x in_dim), zero-padded to TA_AP columns;
+                // P1 = bf16(row_bias) . W_ih1^T + b_ih1
+                rc = hipMemsetAsync(c.b.min1, 0, (size_t)3 * D * TA_AP * 2, s) ? 2 : 0;
+                if (!rc)
+                    rc = srnn_gemm_impl(m->dtype, m->dtype, 0, 0, 3 * D, t1.in_dim, D, 1.f,
+                                        t1.w_ih[0], D, 0, t1.w_in, t1.in_dim, 0, 0.f, nullptr, 0,
+                                        0, c.b.min1, TA_AP, 0, nullptr, 0, 0, 1, -1, s);
+                if (!rc) {
+                    hipLaunchKernelGGL((copy_bf16_kernel), dim3(cdiv(B * D, 256)), dim3(256), 0,
+                                       s, c.row_bias, (bf16*)c.b.x[1], B * D);
+                    rc = linear_fwd(m->dtype, SRNN_F32, B, 3 * D, D, c.b.x[1], D, t1.w_ih[0], D,
+                                    t1.b_ih[0], c.b.p1, 3 * D, 0, s);
+                }
+                if (rc) break;
+            }
             rc = linear_fwd(m->dtype, SRNN_F32, B, 3 * D, D, c.b.hlp[0][0][0], D, t0.w_hh[0], D,
                             t0.b_hh[0], c.b.up[0] + upw, c.b.ldup0, 0, s);
         }

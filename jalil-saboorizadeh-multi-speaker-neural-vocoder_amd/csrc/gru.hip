@@ -39,6 +39,8 @@ struct GruCellArgs {
     int64_t ldgt;
     const float* ghp;   // optional precomputed h.W_hh^T + b_hh (fp32), row stride ldghp: the
     int64_t ldghp;      // h GEMM is skipped (ring kernel only)
+    const float* gadd;  // optional per-row term added to x.W_ih^T (fp32), row stride ldgadd
+    int64_t ldgadd;     // (ring kernel only)
     int B, D, Din;
     int vec_x, vec_h, vec_wih, vec_whh;
 };
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(256) void gru_cell_ring_kernel(GruCellArgs a) {
     const float bhr = a.ghp ? 0.f : a.bhh[u], bhz = a.ghp ? 0.f : a.bhh[D + u];
     const float bhn = a.ghp ? 0.f : a.bhh[2 * D + u];
     float bir = 0.f, biz = 0.f, bin = 0.f;
-    if (a.x) { bir = a.bih[u]; biz = a.bih[D + u]; bin = a.bih[2 * D + u]; }
+    if (a.x && a.bih) { bir = a.bih[u]; biz = a.bih[D + u]; bin = a.bih[2 * D + u]; }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         const int row = m0 + wm * 16 + (lane >> 4) * 4 + i;
@@ -148,6 +150,10 @@ __global__ __launch_bounds__(256) void gru_cell_ring_kernel(GruCellArgs a) {
         float gir, giz, gin;
         if (a.x) {
             gir = acc_i[0][0][i] + bir; giz = acc_i[0][1][i] + biz; gin = acc_i[0][2][i] + bin;
+            if (a.gadd) {
+                const float* ga = a.gadd + (int64_t)row * a.ldgadd;
+                gir += ga[u]; giz += ga[D + u]; gin += ga[2 * D + u];
+            }
         } else {
             const float* g = a.gi + (int64_t)row * a.ldgi;
             gir = g[u]; giz = g[D + u]; gin = g[2 * D + u];
@@ -179,7 +185,7 @@ static int launch_cell(GruCellArgs& a, hipStream_t s) {
     const int es = (int)sizeof(T);
     const bool ring = a.D % R::KB == 0 && (!a.x || a.Din % R::KB == 0) && a.vec_h && a.vec_whh &&
                       (!a.x || (a.vec_x && a.vec_wih));
-    SRNN_REQUIRE(ring || !a.ghp, "gru_cell: precomputed gh needs the ring shape");
+    SRNN_REQUIRE(ring || (!a.ghp && !a.gadd), "gru_cell: precomputed gh / gadd need the ring shape");
     if (ring) {
         static bool attr = false;
         if (!attr) {
@@ -215,6 +221,7 @@ int srnn_gru_cell_impl(int dtype, int B, int D, int Din, const void* x, int64_t 
     a.hout = hout; a.ldho = ldho; a.hout_lp = hout_lp; a.ldhl = ldhl;
     a.gates = gates; a.ldgt = ldgt; a.B = B; a.D = D; a.Din = Din;
     a.ghp = nullptr; a.ldghp = 0;
+    a.gadd = nullptr; a.ldgadd = 0;
     a.vec_x = x ? al16(x, ldx, es) : 0;
     a.vec_h = al16(h, ldh, es);
     a.vec_wih = x ? al16(wih, Din, es) : 0;
@@ -225,11 +232,12 @@ int srnn_gru_cell_impl(int dtype, int B, int D, int Din, const void* x, int64_t 
 }
 
 // GRU cell with h . W_hh^T + b_hh precomputed (the generation loop's folded upper tick carries
-// it in the previous tick's upsampling GEMM): x . W_ih^T + b_ih on MFMA, then the gate update
-int srnn_gru_cell_x_impl(int dtype, int B, int D, const void* x, int64_t ldx, const void* wih,
-                         const float* bih, const float* gh, int64_t ldgh, const float* hf,
-                         int64_t ldhf, float* hout, int64_t ldho, void* hout_lp, int64_t ldhl,
-                         hipStream_t s) {
+// it in the previous tick's upsampling GEMM): gi = x . W_ih^T (+ b_ih) (+ gadd[row]) on MFMA
+// (x: B x Din), then the gate update
+int srnn_gru_cell_x_impl(int dtype, int B, int D, int Din, const void* x, int64_t ldx,
+                         const void* wih, const float* bih, const float* gadd, int64_t ldgadd,
+                         const float* gh, int64_t ldgh, const float* hf, int64_t ldhf, float* hout,
+                         int64_t ldho, void* hout_lp, int64_t ldhl, hipStream_t s) {
     SRNN_REQUIRE(B > 0 && D > 0 && x && gh, "gru_cell_x: bad args");
     const int es = dtype == SRNN_F32 ? 4 : 2;
     GruCellArgs a;
@@ -238,10 +246,11 @@ int srnn_gru_cell_x_impl(int dtype, int B, int D, const void* x, int64_t ldx, co
     a.hf = hf; a.ldhf = ldhf;
     a.hout = hout; a.ldho = ldho; a.hout_lp = hout_lp; a.ldhl = ldhl;
     a.ghp = gh; a.ldghp = ldgh;
-    a.B = B; a.D = D; a.Din = D;
+    a.gadd = gadd; a.ldgadd = ldgadd;
+    a.B = B; a.D = D; a.Din = Din;
     a.vec_x = al16(x, ldx, es);
     a.vec_h = 1;
-    a.vec_wih = al16(wih, D, es);
+    a.vec_wih = al16(wih, Din, es);
     a.vec_whh = 1;
     if (dtype == SRNN_F32) return launch_cell<float, 32>(a, s);
     return launch_cell<bf16, 32>(a, s);
