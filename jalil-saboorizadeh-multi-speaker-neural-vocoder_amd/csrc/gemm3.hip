@@ -1104,7 +1104,9 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     if (!force) {
         const int64_t wg3 = (int64_t)tiles * ks;
         const int64_t wg2 = (int64_t)(M / 128) * (N / 128);
-        if (wg3 < 192 && wg2 > wg3) return -1;
+        // (measured: 96-128 tiles of 256 beat 384-512 of the 128-tile kernel on the TBPTT's
+        //  top-tier NT projections, 2048 x 3072/4096 x 1024; 32 tiles do not)
+        if (wg3 < 96 && wg2 > wg3) return -1;
     }
     g.ksplit = ks;
     g.part = nullptr;

@@ -582,9 +582,10 @@ class _MlpFn(torch.autograd.Function):
                      Tl, H.ptr(dtabT), H.dcode(T), D, FS0, Q, H.ptr(work), work.numel() * 8,
                      H.ptr(colsum), ctypes.byref(done), st())
         dE = H.gemm(dtabT, Wp.reshape(FS0 * D, Q))                       # (Q, Q)
+        # dWp[k] = dTab[:, k]^T E for every tap k at once: (FS0 D, Q) = dtabT^T . ET, one GEMM
+        # (the (FS0, D, Q) result is the same memory as the per-tap batch)
         dWp = torch.empty((FS0, D, Q), device=dev, dtype=torch.float32)
-        H.gemm(dtabT, ET, transA=True, out=dWp, M=D, N=Q, K=Q, lda=FS0 * D, ldb=Q, ldc=Q,
-               batch=FS0, sA=D, sB=0, sC=D * Q)
+        H.gemm(dtabT, ET, transA=True, out=dWp, M=FS0 * D, N=Q, K=Q, lda=FS0 * D, ldb=Q, ldc=Q)
         dW_in = H.permute3(dWp, (1, 2, 0))                               # (D, Q, FS0)
         grads = [dE]
         grads += nn.weight_grad_to_params(mlp.input, dW_in)
