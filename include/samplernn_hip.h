@@ -49,6 +49,21 @@ int srnn_gemm(int dtype, int out_dtype, int transA, int transB, int M, int N, in
               int bias_mode, int relu, int batch, int tile, const void* mask, int64_t ldmask,
               void* stream);
 
+/* The same product (batch 1) with ReLU masks as bits -- bit c % 16 of the u16 at
+ * [row * ld + c / 16] is (value(row, c) > 0): mask_bits (optional) zeroes the outputs whose
+ * bit is clear (in place of srnn_gemm's bf16 mask, 16x fewer bytes for the ReLU backward of
+ * model.py:320-321); bits_out (optional, bf16 out) receives the bits of C (the forward of
+ * the ReLU layer, for that backward). */
+int srnn_gemm_bits(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
+                   float alpha, const void* A, int64_t lda, const void* B, int64_t ldb,
+                   float beta, const float* Cin, int64_t ldcin, void* C, int64_t ldc,
+                   const float* bias, int bias_mode, int relu, int tile,
+                   const unsigned short* mask_bits, int64_t ldmb, unsigned short* bits_out,
+                   int64_t ldbo, void* stream);
+/* bits[row * ldb + c / 16] bit c % 16 = (a[row * lda + c] > 0), a in dtype (M x N). */
+int srnn_relu_bits(int dtype, const void* a, int64_t lda, int M, int N, unsigned short* bits,
+                   int64_t ldb, void* stream);
+
 /* ---- GRU (torch.nn.GRU, model.py:148-165,244) -----------------------------------------
  * One time step for B rows: h_t from h_{t-1} and either x (gi computed in-kernel with
  * W_ih) or a precomputed gi = x W_ih^T + b_ih.  Optionally saves r|z|n|gh_n (4D/row).  */
@@ -134,6 +149,11 @@ int srnn_gru_seq_bwd(int dtype, int B, int D, int Fr, const float* dy, int64_t l
 int srnn_mlp_l1(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff, int B,
                 int Tlen, int upper_dtype, const void* upper, int64_t ldu, void* out,
                 int64_t ldo, int D, int FS0, int Q, void* stream);
+/* The same (bf16 table, upper and a1) writing a1's ReLU mask as bits too (srnn_gemm_bits
+ * layout, row stride ldb u16), for the masked GEMM of the backward.                    */
+int srnn_mlp_l1_bits(const void* tab, const int64_t* x, int64_t ldx, int xoff, int B, int Tlen,
+                     const void* upper, int64_t ldu, void* out, int64_t ldo, int D, int FS0,
+                     int Q, unsigned short* bits, int64_t ldb, void* stream);
 /* dtab[x_{t+k}][k][:] += da_t  (Q, FS0, D) fp32 accumulate; backward of the folded     *
  * embedding+conv                                                                        */
 int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x, int64_t ldx,

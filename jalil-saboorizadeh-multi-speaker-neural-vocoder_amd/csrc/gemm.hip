@@ -282,7 +282,8 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
                    float alpha, const void* A, int64_t lda, const void* B, int64_t ldb,
                    float beta, const float* Cin, int64_t ldcin, void* C, int64_t ldc,
                    const float* bias, int bias_mode, int relu, const void* mask, int64_t ldmask,
-                   int force, hipStream_t s);
+                   int force, hipStream_t s, const unsigned short* mbi = nullptr,
+                   int64_t ldmbi = 0, unsigned short* mbo = nullptr, int64_t ldmbo = 0);
 
 int srnn_gemm_small_try(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
                         float alpha, const void* A, int64_t lda, const void* B, int64_t ldb,
@@ -315,12 +316,118 @@ static int pick_tile(int M, int N, int batch) {
     return 2;
 }
 
+static int gemm_core(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
+                     float alpha, const void* A, int64_t lda, int64_t strideA, const void* B,
+                     int64_t ldb, int64_t strideB, float beta, const float* Cin, int64_t ldcin,
+                     int64_t strideCin, void* C, int64_t ldc, int64_t strideC,
+                     const float* bias, int bias_mode, int relu, int batch, int tile,
+                     hipStream_t s, const void* mask, int64_t ldmask);
+
+// ---- ReLU masks as bits: bit c % 16 of u16 [row][c / 16] = (value(row, c) > 0) ----------
+// (one thread per 16-column group; a column group past N contributes zero bits)
+template <typename T>
+__global__ void relu_bits_kernel(const T* __restrict__ a, int64_t lda, int M, int N,
+                                 unsigned short* __restrict__ bits, int64_t ldb) {
+    const int ng = (N + 15) / 16;
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)M * ng) return;
+    const int r = (int)(e / ng), c0 = (int)(e % ng) * 16;
+    unsigned w = 0u;
+    for (int c = 0; c < 16 && c0 + c < N; ++c)
+        w |= (to_f(a[(int64_t)r * lda + c0 + c]) > 0.f ? 1u : 0u) << c;
+    bits[(int64_t)r * ldb + c0 / 16] = (unsigned short)w;
+}
+
+// the bits as a mask tensor of the GEMM input dtype (1 / 0), for the paths without bit input
+template <typename T>
+__global__ void bits_expand_kernel(const unsigned short* __restrict__ bits, int64_t ldb, int M,
+                                   int N, T* __restrict__ m, int64_t ldm) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)M * N) return;
+    const int r = (int)(e / N), c = (int)(e % N);
+    m[(int64_t)r * ldm + c] = from_f<T>((float)((bits[(int64_t)r * ldb + c / 16] >> (c & 15)) & 1u));
+}
+
+int srnn_relu_bits_impl(int dtype, const void* a, int64_t lda, int M, int N, unsigned short* bits,
+                        int64_t ldb, hipStream_t s) {
+    SRNN_REQUIRE(M >= 0 && N >= 0 && bits && ldb >= (N + 15) / 16, "relu_bits: bad args");
+    const int64_t n = (int64_t)M * ((N + 15) / 16);
+    if (n == 0) return 0;
+    if (dtype == SRNN_F32)
+        hipLaunchKernelGGL((relu_bits_kernel<float>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                           s, (const float*)a, lda, M, N, bits, ldb);
+    else
+        hipLaunchKernelGGL((relu_bits_kernel<bf16>), dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                           s, (const bf16*)a, lda, M, N, bits, ldb);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int srnn_relu_bits(int dtype, const void* a, int64_t lda, int M, int N,
+                              unsigned short* bits, int64_t ldb, void* stream) {
+    return srnn_relu_bits_impl(dtype, a, lda, M, N, bits, ldb, (hipStream_t)stream);
+}
+
 int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
                    float alpha, const void* A, int64_t lda, int64_t strideA, const void* B,
                    int64_t ldb, int64_t strideB, float beta, const float* Cin, int64_t ldcin,
                    int64_t strideCin, void* C, int64_t ldc, int64_t strideC, const float* bias,
                    int bias_mode, int relu, int batch, int tile, hipStream_t s,
-                   const void* mask, int64_t ldmask) {
+                   const void* mask, int64_t ldmask, const unsigned short* mbi, int64_t ldmbi,
+                   unsigned short* mbo, int64_t ldmbo) {
+    if (!mbi && !mbo)
+        return gemm_core(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, strideA, B,
+                         ldb, strideB, beta, Cin, ldcin, strideCin, C, ldc, strideC, bias,
+                         bias_mode, relu, batch, tile, s, mask, ldmask);
+    SRNN_REQUIRE(batch == 1 && !(mbi && mask), "gemm: bit masks need batch 1 and no bf16 mask");
+    if (M == 0 || N == 0) return 0;
+    // the 256-tile kernel reads / writes the bits in its epilogue
+    if ((tile < 0 || tile == 5) && (tile == 5 || g_use_gemm3())) {
+        const int rc = srnn_gemm3_try(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, B,
+                                      ldb, beta, Cin, ldcin, C, ldc, bias, bias_mode, relu, mask,
+                                      ldmask, tile == 5, s, mbi, ldmbi, mbo, ldmbo);
+        if (rc >= 0) return rc;
+    }
+    // other paths (and gemm3 without the bit epilogue, e.g. fp32 out): the bits as a mask
+    // tensor in, the output's bits computed after
+    const void* mk = mask;
+    int64_t ldmk = ldmask;
+    if (mbi) {
+        static void* scratch = nullptr;
+        static size_t bytes = 0;
+        const int es = dtype == SRNN_F32 ? 4 : 2;
+        const size_t need = (size_t)M * N * es;
+        if (need > bytes) {
+            if (scratch) SRNN_CHECK_HIP(hipFree(scratch));
+            scratch = nullptr;
+            bytes = 0;
+            SRNN_CHECK_HIP(hipMalloc(&scratch, need));
+            bytes = need;
+        }
+        const int64_t n = (int64_t)M * N;
+        if (dtype == SRNN_F32)
+            hipLaunchKernelGGL((bits_expand_kernel<float>), dim3((unsigned)cdiv(n, 256)), dim3(256),
+                               0, s, mbi, ldmbi, M, N, (float*)scratch, (int64_t)N);
+        else
+            hipLaunchKernelGGL((bits_expand_kernel<bf16>), dim3((unsigned)cdiv(n, 256)), dim3(256),
+                               0, s, mbi, ldmbi, M, N, (bf16*)scratch, (int64_t)N);
+        SRNN_LAUNCH_CHECK();
+        mk = scratch;
+        ldmk = N;
+    }
+    int rc = gemm_core(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, strideA, B, ldb,
+                       strideB, beta, Cin, ldcin, strideCin, C, ldc, strideC, bias, bias_mode,
+                       relu, batch, tile, s, mk, ldmk);
+    if (rc || !mbo) return rc;
+    return srnn_relu_bits_impl(out_dtype, C, ldc, M, N, mbo, ldmbo, s);
+}
+
+static int gemm_core(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
+                     float alpha, const void* A, int64_t lda, int64_t strideA, const void* B,
+                     int64_t ldb, int64_t strideB, float beta, const float* Cin, int64_t ldcin,
+                     int64_t strideCin, void* C, int64_t ldc, int64_t strideC,
+                     const float* bias, int bias_mode, int relu, int batch, int tile,
+                     hipStream_t s, const void* mask, int64_t ldmask) {
     SRNN_REQUIRE(M >= 0 && N >= 0 && K >= 0 && batch >= 1, "gemm: bad sizes");
     SRNN_REQUIRE(dtype == SRNN_F32 || dtype == SRNN_BF16, "gemm: bad dtype %d", dtype);
     SRNN_REQUIRE(out_dtype == SRNN_F32 || out_dtype == SRNN_BF16, "gemm: bad out dtype");
@@ -395,6 +502,17 @@ int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int 
     }
     if (out_dtype == SRNN_F32) return launch_types<bf16, float>(g, transA, transB, batch, tile, s);
     return launch_types<bf16, bf16>(g, transA, transB, batch, tile, s);
+}
+
+extern "C" int srnn_gemm_bits(int dtype, int out_dtype, int transA, int transB, int M, int N,
+                              int K, float alpha, const void* A, int64_t lda, const void* B,
+                              int64_t ldb, float beta, const float* Cin, int64_t ldcin, void* C,
+                              int64_t ldc, const float* bias, int bias_mode, int relu, int tile,
+                              const unsigned short* mask_bits, int64_t ldmb,
+                              unsigned short* bits_out, int64_t ldbo, void* stream) {
+    return srnn_gemm_impl(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, 0, B, ldb, 0,
+                          beta, Cin, ldcin, 0, C, ldc, 0, bias, bias_mode, relu, 1, tile,
+                          (hipStream_t)stream, nullptr, 0, mask_bits, ldmb, bits_out, ldbo);
 }
 
 extern "C" int srnn_gemm(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,

@@ -40,6 +40,13 @@ struct Gemm3Args {
     int diag;   // timing experiments (SRNN_G3DIAG): 1 no MFMA, 2 no DMA wait, 4 no DMA, 8 no epilogue
     float* part;  // split-K: [ksplit][M][N] fp32 partial tiles (summed in k order by
                   // g3_splitk_sum_kernel: deterministic); null -> fp32 atomics into C
+    // ReLU masks as bits (bit c % 16 of u16 [row][c / 16] = value(row, c) > 0): mbi zeroes
+    // the outputs whose bit is clear (in place of the bf16 mask); mbo receives the bits of
+    // this GEMM's bf16 output (the forward of a ReLU layer, for its backward)
+    const unsigned short* mbi;
+    int64_t ldmbi;
+    unsigned short* mbo;
+    int64_t ldmbo;
 };
 
 namespace g3 {
@@ -146,7 +153,7 @@ __device__ __forceinline__ void g3_store4(bf16* p, const float (&v)[4]) {
 // path, where a lane's 4 values are 4 rows of one column and each atomic instruction
 // covers 16 consecutive columns (64 B) of 4 rows instead of 16 rows x 4 B.
 // epilogue of one finished tile (registers -> C); zeroes the accumulators
-template <typename TO, bool SW, bool CIN>
+template <typename TO, bool SW, bool CIN, bool MB = false>
 __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
                                               int n0, int wm, int wn, int lane, int kb) {
     if constexpr (!SW) {
@@ -209,10 +216,16 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 #pragma unroll
         for (int i = 0; i < 8; ++i) brow[i] = 0.f;
     }
+    // bit mask: the row's 64 bits of the wave's columns, one 8-B load per row (per half,
+    // with the bf16 mask's loads); lane's bit for (fragment j, element e) at
+    // (j & 1) * 16 + (lane >> 4) * 4 + e of word j >> 1
+    const unsigned short* mbi = MB ? g.mbi : nullptr;
+    unsigned short* mbo = MB ? g.mbo : nullptr;
+    const int g4 = (lane >> 4) * 4;
     // the mask in two halves of 16 fragments (register budget): two waits per tile
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        u16x4 mk[4][4];
+        u16x4 mk[4][4];                        // (bit mask: row ii's 64 bits in mk[ii][0])
         if (mask) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
@@ -220,17 +233,29 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
                 for (int j = 0; j < 4; ++j)
                     mk[i][j] = *reinterpret_cast<const u16x4*>(
                         mask + (int64_t)(rbase + (4 * h + i) * 16) * g.ldmask + cbase + j * 16);
+        } else if (mbi) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                mk[i][0] = *reinterpret_cast<const u16x4*>(
+                    mbi + (int64_t)(rbase + (4 * h + i) * 16) * g.ldmbi + (n0 + wn * 64) / 16);
         }
+        auto mbit = [&](int ii, int j, int e) -> bool {
+            const unsigned w = (unsigned)mk[ii][0][(j >> 1) * 2] |
+                               ((unsigned)mk[ii][0][(j >> 1) * 2 + 1] << 16);
+            return (w >> (((j & 1) << 4) + g4 + e)) & 1u;
+        };
         if constexpr (sizeof(TO) == 2 && !CIN) {
             // bf16 out: fragments j, j + 1 of a row combined by two v_permlane16_swap per
             // pair, so every lane stores 16 B (8 columns) -- half the store instructions of
             // the 8-B-per-fragment form (the epilogue tail is store-issue-bound)
             const int grp = lane >> 4;
             const int coff = 16 * (grp & 1) + 8 * (grp >> 1) - 4 * grp;   // lane's 16-B column
+            unsigned wbits[4][2];                      // bits out: rows 4h + ii, words lo / hi
 #pragma unroll
             for (int ii = 0; ii < 4; ++ii) {
                 const int i = 4 * h + ii;
                 const int row = rbase + i * 16;
+                wbits[ii][0] = wbits[ii][1] = 0u;
 #pragma unroll
                 for (int jp = 0; jp < 2; ++jp) {
                     unsigned pk[2][2];
@@ -249,11 +274,24 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 #pragma unroll
                             for (int e = 0; e < 4; ++e)
                                 v[e] = __uint_as_float((unsigned)mk[ii][j][e] << 16) > 0.f ? v[e] : 0.f;
+                        } else if (mbi) {
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) v[e] = mbit(ii, j, e) ? v[e] : 0.f;
                         }
 #pragma unroll
                         for (int e = 0; e < 2; ++e)
                             pk[t][e] = (unsigned)__bfloat16_as_ushort(__float2bfloat16(v[2 * e])) |
                                        ((unsigned)__bfloat16_as_ushort(__float2bfloat16(v[2 * e + 1])) << 16);
+                        if (mbo) {
+                            // value > 0 of the stored bf16: 0x0001 .. 0x7f80 (no -0, no NaN)
+                            unsigned nib = 0u;
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const unsigned u = (pk[t][e >> 1] >> (16 * (e & 1))) & 0xffffu;
+                                nib |= (u - 1u < 0x7f80u ? 1u : 0u) << e;
+                            }
+                            wbits[ii][j >> 1] |= nib << (((j & 1) << 4) + g4);
+                        }
                     }
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
@@ -264,6 +302,24 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
                     *reinterpret_cast<uint4*>(Cp + (int64_t)row * g.ldc + cbase + 32 * jp + coff) =
                         make_uint4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
                 }
+            }
+            if (mbo) {
+                // OR over the 4 lanes of a row (lane ^ 16, ^ 32), then lane group g stores
+                // row 4h + g: one 8-B store per lane for the half's 4 rows
+                unsigned sel[2] = {0u, 0u};
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+                    for (int w = 0; w < 2; ++w) {
+                        unsigned a, b, x = wbits[ii][w];
+                        xpair16(x, a, b);
+                        x = a | b;
+                        xpair32(x, a, b);
+                        x = a | b;
+                        if (ii == grp) sel[w] = x;
+                    }
+                *reinterpret_cast<uint2*>(mbo + (int64_t)(rbase + (4 * h + grp) * 16) * g.ldmbo +
+                                          (n0 + wn * 64) / 16) = make_uint2(sel[0], sel[1]);
             }
             continue;
         }
@@ -294,6 +350,9 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
                         v[e] = __uint_as_float((unsigned)mk[ii][j][e] << 16) > 0.f ? v[e] : 0.f;
+                } else if (mbi) {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) v[e] = mbit(ii, j, e) ? v[e] : 0.f;
                 }
                 g3_store4(Cp + (int64_t)row * g.ldc + col, v);
             }
@@ -307,9 +366,14 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 // Returns the number of stores each wave issued (SW path): the main loops' counted DMA
 // waits leave exactly that many younger stores in flight, so the count must be exact -- a
 // larger allowance would let a stage's DMA pieces still be outstanding at the read.
-template <typename TO, bool SW>
+template <typename TO, bool SW, bool MB = false>
 __device__ __forceinline__ int g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
                                            int n0, int wm, int wn, int lane, int kb) {
+    if constexpr (MB) {
+        // the bit-mask kernels (their own instantiation: the plain epilogue keeps its registers)
+        g3_epilogue_t<TO, SW, false, true>(g, acc, m0, n0, wm, wn, lane, kb);
+        return sizeof(TO) == 2 ? 16 + (g.mbo ? 2 : 0) : 32;
+    }
     if (SW && g.beta != 0.f) {
         g3_epilogue_t<TO, SW, true>(g, acc, m0, n0, wm, wn, lane, kb);
         return 32;
@@ -345,7 +409,7 @@ __global__ __launch_bounds__(256) void g3_splitk_sum_kernel(const float* __restr
 // Persistent: workgroup w owns work units w, w + G, ... (unit = output tile x k-slice);
 // the k-stages of all its units form ONE stream through the ring, so the DMA of the next
 // tile's first stages runs under the current tile's last MFMAs and epilogue.
-template <typename TO, bool KCA, bool KCB, bool SW>
+template <typename TO, bool KCA, bool KCB, bool SW, bool MB = false>
 __global__ __launch_bounds__(512, 1) void gemm3_kernel(Gemm3Args g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -445,7 +509,7 @@ __global__ __launch_bounds__(512, 1) void gemm3_kernel(Gemm3Args g) {
         if (++ktc == nk) {
             int m0, n0, kb;
             unit(ic, m0, n0, kb);
-            epi = g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
+            epi = g3_epilogue<TO, SW, MB>(g, acc, m0, n0, wm, wn, lane, kb);
             ktc = 0;
             ++ic;
         }
@@ -459,6 +523,7 @@ __global__ __launch_bounds__(512, 1) void gemm3_kernel(Gemm3Args g) {
         // the 32 epilogue stores of a just-finished tile are younger than the pieces
         // waited for here: leave them in flight
         if (SW && epi == 16) g3_wait_vm<(g3::NS - 2) * PER + 16>();
+        else if (SW && epi == 18) g3_wait_vm<(g3::NS - 2) * PER + 18>();   // + mask bits
         else if (SW && epi) g3_wait_vm<(g3::NS - 2) * PER + 32>();
         else g3_wait_vm<(g3::NS - 2) * PER>();
         epi = 0;
@@ -547,7 +612,7 @@ __device__ __forceinline__ bf16x8 g3p_frag(const char* img, int f0, int u, int l
     }
 }
 
-template <typename TO, bool KCA, bool KCB, bool SW>
+template <typename TO, bool KCA, bool KCB, bool SW, bool MB = false>
 __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -639,7 +704,7 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
         if (++ktc == nk) {
             int m0, n0, kb;
             unit(ic, m0, n0, kb);
-            epi = (g.diag & 8) ? 0 : g3_epilogue<TO, SW>(g, acc, m0, n0, wm, wn, lane, kb);
+            epi = (g.diag & 8) ? 0 : g3_epilogue<TO, SW, MB>(g, acc, m0, n0, wm, wn, lane, kb);
             ktc = 0;
             ++ic;
         }
@@ -651,6 +716,7 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
         const char* img = smem + (s & 1) * g3p::SLOT;
         char* nimg = smem + ((s + 1) & 1) * g3p::SLOT;
         if (SW && epi == 16) g3_wait_vm<16>();
+        else if (SW && epi == 18) g3_wait_vm<18>();                        // + mask bits
         else if (SW && epi) g3_wait_vm<32>();
         else g3_wait_vm<0>();
         epi = 0;
@@ -1028,9 +1094,15 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
     auto k = q ? gemm3q_kernel<TO, KCA, KCB, SW>
                : pp ? gemm3pp_kernel<TO, KCA, KCB, SW>
                     : pair ? gemm3p_kernel<TO, KCA, KCB, SW> : gemm3_kernel<TO, KCA, KCB, SW>;
+    int ki = q ? 3 : pp ? 2 : pair ? 1 : 0;
+    if constexpr (sizeof(TO) == 2 && SW) {
+        if (g.mbi || g.mbo) {        // ReLU bit masks (srnn_gemm3_try admits modes 0-2 only)
+            k = pair ? gemm3p_kernel<TO, KCA, KCB, SW, true> : gemm3_kernel<TO, KCA, KCB, SW, true>;
+            ki += 4;
+        }
+    }
     const int lds = (pp || pair) ? g3p::LDS : g3::LDS;
-    const int ki = q ? 3 : pp ? 2 : pair ? 1 : 0;
-    static bool attr[4] = {false, false, false, false};
+    static bool attr[8] = {false, false, false, false, false, false, false, false};
     if (!attr[ki]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -1081,8 +1153,13 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
                    float alpha, const void* A, int64_t lda, const void* B, int64_t ldb,
                    float beta, const float* Cin, int64_t ldcin, void* C, int64_t ldc,
                    const float* bias, int bias_mode, int relu, const void* mask, int64_t ldmask,
-                   int force, hipStream_t s) {
+                   int force, hipStream_t s, const unsigned short* mbi, int64_t ldmbi,
+                   unsigned short* mbo, int64_t ldmbo) {
     if (dtype != SRNN_BF16) return -1;
+    if ((mbi || mbo) && (out_dtype != SRNN_BF16 || g3_mode() > 2)) return -1;
+    if ((mbi && ((uintptr_t)mbi % 8 || ldmbi % 4 || mask)) ||
+        (mbo && ((uintptr_t)mbo % 8 || ldmbo % 4 || beta != 0.f)))
+        return -1;
     if (M % g3::BM || N % g3::BN || K % g3::BK || K == 0) return -1;
     auto al = [](const void* p, int64_t ld, int es) {
         return ((uintptr_t)p % 16 == 0) && ((ld * es) % 16 == 0);
@@ -1098,8 +1175,10 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     g.M = M; g.N = N; g.K = K; g.alpha = alpha; g.beta = beta;
     g.bias_mode = bias ? bias_mode : 0; g.relu = relu;
     g.diag = env_flag("SRNN_G3DIAG", 0);
+    g.mbi = mbi; g.ldmbi = ldmbi; g.mbo = mbo; g.ldmbo = ldmbo;
     const int tiles = (M / g3::BM) * (N / g3::BN);
-    const bool plain = beta == 0.f && !bias && !relu && !mask && out_dtype == SRNN_F32;
+    const bool plain = beta == 0.f && !bias && !relu && !mask && !mbi && !mbo &&
+                       out_dtype == SRNN_F32;
     const int ks = plain ? g3_pick_split(tiles, K) : 1;
     if (!force) {
         const int64_t wg3 = (int64_t)tiles * ks;

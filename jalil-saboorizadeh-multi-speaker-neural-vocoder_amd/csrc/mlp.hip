@@ -156,7 +156,7 @@ __device__ __forceinline__ void l1l_add8(const uint4 v, float (&a)[8], l1_bf16x2
 __global__ __launch_bounds__(L1L_NT, 1) void mlp_l1_lds_kernel(
     const bf16* __restrict__ tab, const int64_t* __restrict__ x, int64_t ldx, int xoff, int B,
     int Tlen, int bpc, const bf16* __restrict__ upper, int64_t ldu, bf16* __restrict__ out,
-    int64_t ldo, int D) {
+    int64_t ldo, int D, unsigned short* __restrict__ bits, int64_t ldb) {
     constexpr int FS = 16, Q = 256;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     char* tl = smem;                                        // [FS * Q][16] bf16 = 128 KiB
@@ -255,6 +255,18 @@ __global__ __launch_bounds__(L1L_NT, 1) void mlp_l1_lds_kernel(
 #pragma unroll
             for (int k = 0; k < FS; ++k) l1l_add8(tv[k], a, lo1, hi1);
             l1_store8(out + r * ldo + c0 + h * 8, a);
+            if (bits) {
+                // ReLU mask bits of the 16 columns (stored bf16 > 0): this thread's 8, its
+                // pair lane's 8 (DPP quad_perm 1,0,3,2)
+                unsigned nib = 0u;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    const unsigned u = __bfloat16_as_ushort(__float2bfloat16(fmaxf(a[e], 0.f)));
+                    nib |= (u - 1u < 0x7f80u ? 1u : 0u) << e;
+                }
+                const unsigned pn = dpp_u32<0xB1>(nib);
+                if (h == 0) bits[r * ldb + (c0 >> 4)] = (unsigned short)(nib | (pn << 8));
+            }
         }
         if (more) put_x(ib + ((b + 1 - b0) & 1) * WP);
         __syncthreads();                                    // next buffer staged, cur free
@@ -264,7 +276,8 @@ __global__ __launch_bounds__(L1L_NT, 1) void mlp_l1_lds_kernel(
 template <typename T, typename TU>
 static int mlp_l1_launch(const T* tab, const int64_t* x, int64_t ldx, int xoff, const int* base,
                          int B, int Tlen, const TU* upper, int64_t ldu, T* out, int64_t ldo,
-                         int D, int FS0, int Q, hipStream_t s) {
+                         int D, int FS0, int Q, hipStream_t s, unsigned short* bits = nullptr,
+                         int64_t ldb = 0) {
     const int64_t nrows = (int64_t)B * Tlen;
     const int ue = (int)sizeof(TU);
     if constexpr (sizeof(T) == 2 && sizeof(TU) == 2) {
@@ -287,7 +300,7 @@ static int mlp_l1_launch(const T* tab, const int64_t* x, int64_t ldx, int xoff, 
             }
             hipLaunchKernelGGL(mlp_l1_lds_kernel, dim3(ncg * nrc2), dim3(L1L_NT), lds, s,
                                (const bf16*)tab, x, ldx, xoff, B, Tlen, bpc, (const bf16*)upper,
-                               ldu, (bf16*)out, ldo, D);
+                               ldu, (bf16*)out, ldo, D, bits, ldb);
             SRNN_LAUNCH_CHECK();
             return 0;
         }
@@ -307,6 +320,10 @@ static int mlp_l1_launch(const T* tab, const int64_t* x, int64_t ldx, int xoff, 
                            base, Tlen, upper, ldu, out, ldo, D, FS0, Q);
     }
     SRNN_LAUNCH_CHECK();
+    // (the other paths: the mask bits from the written rows)
+    if (bits)
+        return srnn_relu_bits_impl(sizeof(T) == 2 ? SRNN_BF16 : SRNN_F32, out, ldo, (int)nrows, D,
+                                   bits, ldb, s);
     return 0;
 }
 
@@ -329,6 +346,19 @@ int srnn_mlp_l1_impl(int dtype, const void* tab, const int64_t* x, int64_t ldx, 
                                           (const float*)upper, ldu, (bf16*)out, ldo, D, FS0, Q, s);
     return mlp_l1_launch<bf16, bf16>((const bf16*)tab, x, ldx, xoff, base, B, Tlen,
                                      (const bf16*)upper, ldu, (bf16*)out, ldo, D, FS0, Q, s);
+}
+
+// the same with the ReLU mask of a1 as bits (u16 per 16 columns, row stride ldb) for the
+// backward's masked GEMM (bf16 table and upper)
+extern "C" int srnn_mlp_l1_bits(const void* tab, const int64_t* x, int64_t ldx, int xoff, int B,
+                                int Tlen, const void* upper, int64_t ldu, void* out, int64_t ldo,
+                                int D, int FS0, int Q, unsigned short* bits, int64_t ldb,
+                                void* stream) {
+    SRNN_REQUIRE(D % 16 == 0 && FS0 <= 32 && bits && ldb >= D / 16, "mlp_l1_bits: bad args");
+    if ((int64_t)B * Tlen <= 0) return 0;
+    return mlp_l1_launch<bf16, bf16>((const bf16*)tab, x, ldx, xoff, nullptr, B, Tlen,
+                                     (const bf16*)upper, ldu, (bf16*)out, ldo, D, FS0, Q,
+                                     (hipStream_t)stream, bits, ldb);
 }
 
 extern "C" int srnn_mlp_l1(int dtype, const void* tab, const int64_t* x, int64_t ldx, int xoff,

@@ -7,7 +7,11 @@ int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int 
                    int64_t ldb, int64_t strideB, float beta, const float* Cin, int64_t ldcin,
                    int64_t strideCin, void* C, int64_t ldc, int64_t strideC, const float* bias,
                    int bias_mode, int relu, int batch, int tile, hipStream_t s,
-                   const void* mask = nullptr, int64_t ldmask = 0);
+                   const void* mask = nullptr, int64_t ldmask = 0,
+                   const unsigned short* mbi = nullptr, int64_t ldmbi = 0,
+                   unsigned short* mbo = nullptr, int64_t ldmbo = 0);
+int srnn_relu_bits_impl(int dtype, const void* a, int64_t lda, int M, int N, unsigned short* bits,
+                        int64_t ldb, hipStream_t s);
 
 // y[M,N] = act(x[M,K] . W[N,K]^T + bias)   (nn.Linear / Conv1d(k=1) forward)
 static inline int linear_fwd(int dt, int odt, int M, int N, int K, const void* x, int64_t ldx,

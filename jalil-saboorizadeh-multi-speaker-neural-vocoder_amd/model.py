@@ -535,11 +535,24 @@ class _MlpFn(torch.autograd.Function):
         tab, Wp, ET = _build_tab(mlp, T)
         a1 = torch.empty((B * Tl, D), device=dev, dtype=T)
         upper = upper.contiguous()
-        H.lib().call('srnn_mlp_l1', H.dcode(T), H.ptr(tab), H.ptr(x), x.shape[1], 0, B, Tl,
-                     H.dcode(upper), H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
+        # SRNN_MASK_BITS=1 (bf16): the ReLU masks of a1 and a2 leave the forward as bits, 16x
+        # fewer bytes for the backward's masked GEMMs to read than the activations.  Off by
+        # default: measured (MI355X, B = 128) the two masked dgrads gain 27 us each, but the
+        # hidden GEMM's bit epilogue costs 26 us and the L1 gather's 2-B bit stores 87 us.
+        bits = T == torch.bfloat16 and upper.dtype == T and D % 64 == 0 and \
+            os.environ.get('SRNN_MASK_BITS', '0') != '0'
+        m1 = m2 = None
+        if bits:
+            m1, m2 = H.relu_bits(B * Tl, D, dev), H.relu_bits(B * Tl, D, dev)
+            H.lib().call('srnn_mlp_l1_bits', H.ptr(tab), H.ptr(x), x.shape[1], 0, B, Tl,
+                         H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.ptr(m1), m1.stride(0),
+                         H.stream())
+        else:
+            H.lib().call('srnn_mlp_l1', H.dcode(T), H.ptr(tab), H.ptr(x), x.shape[1], 0, B, Tl,
+                         H.dcode(upper), H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
         W_hid = _wcast(mlp.hidden, T).reshape(D, D)
         W_out = _wcast(mlp.output, T).reshape(Q, D)
-        a2 = H.linear(a1, W_hid, bias=mlp.hidden.bias, relu=True, out_dtype=T)
+        a2 = H.linear(a1, W_hid, bias=mlp.hidden.bias, relu=True, out_dtype=T, bits_out=m2)
         z = H.linear(a2, W_out, bias=mlp.output.bias)                    # (B*T, Q) fp32
         logp = torch.empty((B * Tl, Q), device=dev, dtype=torch.float32)
         H.lib().call('srnn_logsoftmax_nll', H.ptr(z), Q, None, 0, Tl, B * Tl, Q, None,
@@ -549,6 +562,7 @@ class _MlpFn(torch.autograd.Function):
         ctx.udt = upper.dtype
         ctx.dims = (B, Tl, D, Q, FS0)
         ctx.save_for_backward(x, a1, a2, logp, Wp, ET, W_hid, W_out)
+        ctx.bits = (m1, m2)
         return logp.reshape(B, Tl, Q)
 
     @staticmethod
@@ -566,11 +580,19 @@ class _MlpFn(torch.autograd.Function):
                      H.dcode(T), Q, st())
         dW_out = H.gemm(dz, a2, transA=True)                             # (Q, D)
         db_out = H.colsum(dz, M, Q)
-        da2 = H.gemm(dz, W_out, mask=a2, out_dtype=T)                    # (M, D)
+        m1, m2 = ctx.bits
+        ctx.bits = None
+        if m2 is not None:
+            da2 = H.gemm(dz, W_out, mask_bits=m2, out_dtype=T)           # (M, D)
+        else:
+            da2 = H.gemm(dz, W_out, mask=a2, out_dtype=T)                # (M, D)
         dW_hid = H.gemm(da2, a1, transA=True)                            # (D, D)
         db_hid = H.colsum(da2, M, D)
         # d(upper) in upper's dtype: bf16 when the bottom tier hands the MLP a bf16 upper
-        da1 = H.gemm(da2, W_hid, mask=a1, out_dtype=ctx.udt)              # (M, D)
+        if m1 is not None:
+            da1 = H.gemm(da2, W_hid, mask_bits=m1, out_dtype=ctx.udt)     # (M, D)
+        else:
+            da1 = H.gemm(da2, W_hid, mask=a1, out_dtype=ctx.udt)          # (M, D)
         # folded embedding . conv backward: dTab[q][k][:] += da1[t] for x_{t+k} = q
         dtabT = torch.empty((Q, FS0 * D), device=dev, dtype=T)
         work = torch.empty(Q * FS0 * D, device=dev, dtype=torch.int64)

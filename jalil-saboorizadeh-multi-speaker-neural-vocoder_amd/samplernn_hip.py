@@ -36,6 +36,10 @@ _SIGS = {
     'srnn_udequantize_host': [_P, _P, _L, _I],
     'srnn_gemm': [_I, _I, _I, _I, _I, _I, _I, _F, _P, _L, _L, _P, _L, _L, _F, _P, _L, _L, _P, _L,
                   _L, _P, _I, _I, _I, _I, _P, _L, _P],
+    'srnn_gemm_bits': [_I, _I, _I, _I, _I, _I, _I, _F, _P, _L, _P, _L, _F, _P, _L, _P, _L, _P, _I,
+                       _I, _I, _P, _L, _P, _L, _P],
+    'srnn_relu_bits': [_I, _P, _L, _I, _I, _P, _L, _P],
+    'srnn_mlp_l1_bits': [_P, _P, _L, _I, _I, _I, _P, _L, _P, _L, _I, _I, _I, _P, _L, _P],
     'srnn_gru_cell': [_I, _I, _I, _I, _P, _L, _P, _P, _P, _L, _P, _L, _P, _L, _P, _P, _P, _L, _P,
                       _L, _P, _L, _P],
     'srnn_gru_cell_bwd': [_I, _I, _I, _P, _L, _P, _L, _P, _P, _P, _P, _L, _P, _L, _P, _L, _P, _L,
@@ -278,10 +282,18 @@ def need_cuda(*ts):
 _GEMM_LOG = os.environ.get('SRNN_GEMM_LOG', '0') == '1'
 
 
+def relu_bits(rows, cols, device):
+    """An (rows, ceil(cols / 16)) int16 buffer for a ReLU mask as bits (srnn_gemm_bits)."""
+    return torch.empty((rows, (cols + 15) // 16), device=device, dtype=torch.int16)
+
+
 def gemm(a, b, transA=False, transB=False, out=None, out_dtype=torch.float32, bias=None,
          bias_mode=1, relu=False, alpha=1.0, beta=0.0, cin=None, mask=None, M=None, N=None, K=None,
-         lda=None, ldb=None, ldc=None, ldcin=None, batch=1, sA=0, sB=0, sC=0, sCin=0, tile=-1):
-    """C = act(alpha op(A) op(B) + beta Cin + bias) on row-major 2-D views (or strided batches)."""
+         lda=None, ldb=None, ldc=None, ldcin=None, batch=1, sA=0, sB=0, sC=0, sCin=0, tile=-1,
+         mask_bits=None, bits_out=None):
+    """C = act(alpha op(A) op(B) + beta Cin + bias) on row-major 2-D views (or strided batches).
+    mask_bits / bits_out: the ReLU mask as bits (relu_bits buffers), read in place of `mask` /
+    written for C (batch 1)."""
     need_cuda(a, b)
     if M is None:
         M = a.shape[1] if transA else a.shape[0]
@@ -302,10 +314,19 @@ def gemm(a, b, transA=False, transB=False, out=None, out_dtype=torch.float32, bi
     if _GEMM_LOG:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-    lib().call('srnn_gemm', dcode(a), dcode(out), int(transA), int(transB), M, N, K, alpha,
-               ptr(a), lda, sA, ptr(b), ldb, sB, beta, ptr(cin), ldcin or 0, sCin, ptr(out), ldc,
-               sC, ptr(bias), bias_mode, int(relu), batch, tile, ptr(mask),
-               (mask.stride(0) if mask is not None else 0), stream())
+    if mask_bits is not None or bits_out is not None:
+        if batch != 1 or mask is not None:
+            raise ValueError('gemm: bit masks need batch 1 and no tensor mask')
+        lib().call('srnn_gemm_bits', dcode(a), dcode(out), int(transA), int(transB), M, N, K,
+                   alpha, ptr(a), lda, ptr(b), ldb, beta, ptr(cin), ldcin or 0, ptr(out), ldc,
+                   ptr(bias), bias_mode, int(relu), tile, ptr(mask_bits),
+                   mask_bits.stride(0) if mask_bits is not None else 0, ptr(bits_out),
+                   bits_out.stride(0) if bits_out is not None else 0, stream())
+    else:
+        lib().call('srnn_gemm', dcode(a), dcode(out), int(transA), int(transB), M, N, K, alpha,
+                   ptr(a), lda, sA, ptr(b), ldb, sB, beta, ptr(cin), ldcin or 0, sCin, ptr(out),
+                   ldc, sC, ptr(bias), bias_mode, int(relu), batch, tile, ptr(mask),
+                   (mask.stride(0) if mask is not None else 0), stream())
     if _GEMM_LOG:
         torch.cuda.synchronize()
         us = (time.perf_counter() - t0) * 1e6
@@ -317,10 +338,11 @@ def gemm(a, b, transA=False, transB=False, out=None, out_dtype=torch.float32, bi
     return out
 
 
-def linear(x, w, bias=None, relu=False, out_dtype=torch.float32, out=None, cin=None, beta=0.0):
+def linear(x, w, bias=None, relu=False, out_dtype=torch.float32, out=None, cin=None, beta=0.0,
+           bits_out=None):
     """y = act(x . w^T + bias (+ beta * cin)) for 2-D x (M, K) and w (N, K)."""
     return gemm(x, w, transB=True, bias=bias, relu=relu, out_dtype=out_dtype, out=out, cin=cin,
-                beta=beta)
+                beta=beta, bits_out=bits_out)
 
 
 def colsum(x, rows, cols, lds=None, out=None, alpha=1.0, accumulate=False):

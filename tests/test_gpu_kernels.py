@@ -903,3 +903,63 @@ def test_bf16_parameter_copies_follow_adam(hip):
     assert hip.shadow_of(w) is None
     torch.testing.assert_close(hip.cast_param(w, torch.bfloat16), w.detach().to(torch.bfloat16),
                                atol=0, rtol=0)
+
+
+def _bits_ref(a):
+    """ReLU mask bits of a (M, N) in the srnn_gemm_bits layout, as int16 (M, N / 16)."""
+    pos = (a.float() > 0).to(torch.int32).reshape(a.shape[0], -1, 16)
+    w = (pos << torch.arange(16, device=a.device, dtype=torch.int32)).sum(-1)
+    return w.to(torch.int32).view(-1).to(torch.int16).reshape(a.shape[0], -1)
+
+
+@pytest.mark.parametrize('B,Tl,D', [(128, 1024, 1024), (3, 4096, 272), (6, 1000, 512)])
+def test_mlp_l1_bits(hip, B, Tl, D, monkeypatch):
+    """a1 with its ReLU mask as bits (the LDS kernel's fused bits, and the bits pass after the
+    other gathers) == the plain gather's a1 and the bits of that a1."""
+    FS0, Q = 16, 256
+    g = torch.Generator().manual_seed(B * 7 + D)
+    tab = (torch.randn(FS0, Q, D, generator=g) * 0.3).to(DEV, torch.bfloat16)
+    x = torch.randint(0, Q, (B, Tl + FS0 + 3), generator=g).to(DEV)
+    upper = (torch.randn(B * Tl, D, generator=g) * 0.5).to(DEV, torch.bfloat16)
+    ref = torch.empty(B * Tl, D, device=DEV, dtype=torch.bfloat16)
+    hip.lib().call('srnn_mlp_l1', hip.BF16, hip.ptr(tab), hip.ptr(x), x.shape[1], 2, B, Tl,
+                   hip.BF16, hip.ptr(upper), D, hip.ptr(ref), D, D, FS0, Q, hip.stream())
+    for flag in ('1', '0'):
+        monkeypatch.setenv('SRNN_L1_LDS', flag)
+        out = torch.empty_like(ref)
+        bits = hip.relu_bits(B * Tl, D, DEV)
+        hip.lib().call('srnn_mlp_l1_bits', hip.ptr(tab), hip.ptr(x), x.shape[1], 2, B, Tl,
+                       hip.ptr(upper), D, hip.ptr(out), D, D, FS0, Q, hip.ptr(bits),
+                       bits.stride(0), hip.stream())
+        torch.testing.assert_close(out, ref, atol=0, rtol=0)
+        assert torch.equal(bits, _bits_ref(ref))
+
+
+@pytest.mark.parametrize('M,N,K,tB,tile', [(1024, 512, 256, False, 5), (512, 1024, 1024, True, 5),
+                                           (768, 512, 512, False, 5), (200, 144, 96, False, -1),
+                                           (256, 256, 64, True, -1)])
+def test_gemm_mask_bits(hip, M, N, K, tB, tile):
+    """ReLU masks as bits: the masked GEMM with bits == with the bf16 mask tensor, bit for
+    bit (256-tile kernel's bit epilogue, and the expanded-mask fallback of other shapes); the
+    ReLU forward's bits_out == the bits of its bf16 output."""
+    bf = torch.bfloat16
+    A = _rand(M, K, seed=1).to(DEV, bf)
+    W = (_rand(N, K, seed=2) if tB else _rand(K, N, seed=2)).to(DEV, bf)
+    act = _rand(M, N, seed=3).to(DEV, bf)               # the layer's forward activation
+    act[act.float().abs() < 0.3] = 0.0
+    bits = hip.relu_bits(M, N, DEV)
+    hip.lib().call('srnn_relu_bits', hip.BF16, hip.ptr(act), N, M, N, hip.ptr(bits),
+                   bits.stride(0), hip.stream())
+    assert torch.equal(bits, _bits_ref(act))
+    o1 = hip.gemm(A, W, transB=tB, mask=act, out_dtype=bf, tile=tile)
+    o2 = hip.gemm(A, W, transB=tB, mask_bits=bits, out_dtype=bf, tile=tile)
+    assert torch.equal(o1, o2)
+    o3 = hip.gemm(A, W, transB=tB, mask_bits=bits, tile=tile)     # fp32 out: fallback path
+    o4 = hip.gemm(A, W, transB=tB, mask=act, tile=tile)
+    assert torch.equal(o3, o4)
+    bias = _rand(N, seed=4).to(DEV)
+    bo = hip.relu_bits(M, N, DEV)
+    y = hip.gemm(A, W, transB=tB, bias=bias, relu=True, out_dtype=bf, tile=tile, bits_out=bo)
+    y0 = hip.gemm(A, W, transB=tB, bias=bias, relu=True, out_dtype=bf, tile=tile)
+    assert torch.equal(y, y0)
+    assert torch.equal(bo, _bits_ref(y))

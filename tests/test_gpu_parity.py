@@ -135,3 +135,31 @@ def test_generation_vs_oracle_philox_consistency(hip):
     torch.testing.assert_close(tf.cpu(), lp.cpu(), atol=1e-4, rtol=0)
     # sampled indices follow the distribution: mean log-prob of the drawn samples is finite
     assert torch.isfinite(lp).all()
+
+
+def test_mask_bits_step_bf16(hip, monkeypatch):
+    """SRNN_MASK_BITS=1 (ReLU masks of a1 / a2 kept as bits for the backward): the bf16
+    forward log-probs and every gradient equal the default path's bit for bit."""
+    import nn as snn
+    cfg = dict(recipe.CONFIGS['t3'], dim=256)
+    B, T = 4, 1024
+    g = torch.Generator().manual_seed(3)
+    outs = []
+    for flag in ('0', '1'):
+        monkeypatch.setenv('SRNN_MASK_BITS', flag)
+        m, pred = build(cfg, recipe.make_weights(cfg, 21), torch.bfloat16)
+        L = m.lookback
+        g.manual_seed(3)
+        x = torch.randint(0, 256, (B, L + T), generator=g)
+        cond = torch.rand(B, T // L, cfg['cond_dim'], generator=g)
+        spk = torch.arange(B).reshape(-1, 1) % cfg['spk_dim']
+        lp = pred(x[:, :-1].to(DEV), True, cond, spk)
+        loss = snn.sequence_nll_loss_bits(lp, x[:, L:].to(DEV))
+        loss.backward()
+        outs.append((lp.detach().cpu(), {k: p.grad.detach().cpu().clone()
+                                          for k, p in pred.named_parameters()
+                                          if p.grad is not None}))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert outs[0][1].keys() == outs[1][1].keys()
+    for k in outs[0][1]:
+        assert torch.equal(outs[0][1][k], outs[1][1][k]), k
