@@ -74,7 +74,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
 // Skinny NT path (M = batch rows, e.g. the generation loop's y = x W^T with M = 128):
 // small tiles so >= 256 workgroups exist, and the deep glds ring of ring_core.hpp so a
 // workgroup's K chain is not one exposed memory latency per stage.
-template <typename T, typename TO, int BM, int BN, int WM, int WN, int WK, int NS = 4>
+template <typename T, typename TO, int BM, int BN, int WM, int WN, int WK, int NS = 4,
+          int AUXB = 0>
 __global__ __launch_bounds__(256) void skinny_kernel(GemmArgs g) {
     typedef Ring<T, BM, BN, WM, WN, WK, NS> R;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -87,8 +88,9 @@ __global__ __launch_bounds__(256) void skinny_kernel(GemmArgs g) {
     unsigned long long* st = (g.diag && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
                                  ? g.diag : nullptr;
     if (st) st[0] = __builtin_amdgcn_s_memrealtime();
-    ring_core<T, BM, BN, WM, WN, WK, NS>((const T*)g.A, g.lda, RowClamp{m0, g.M}, (const T*)g.B,
-                                         g.ldb, RowClamp{n0, g.N}, g.K, smem, acc, st);
+    ring_core<T, BM, BN, WM, WN, WK, NS, RowClamp, RowClamp, AUXB>(
+        (const T*)g.A, g.lda, RowClamp{m0, g.M}, (const T*)g.B, g.ldb, RowClamp{n0, g.N}, g.K,
+        smem, acc, st);
     ring_reduce<T, BM, BN, WM, WN, WK, NS>(smem, acc);
     if (st) st[31] = __builtin_amdgcn_s_memrealtime();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -198,12 +200,18 @@ extern "C" int srnn_skinny_diag_dump(void) {
 template <typename T, typename TO, int BN, int WM, int WN, int NS>
 static int launch_skinny_rows(const GemmArgs& g, hipStream_t s) {
     typedef Ring<T, 128, BN, WM, WN, 1, NS> R;
-    auto k = skinny_kernel<T, TO, 128, BN, WM, WN, 1, NS>;
-    static bool attr = false;
-    if (!attr) {
+    // SRNN_SKINNY_NT=1: every weight row is read by exactly one workgroup, once, so the
+    // weights may take non-temporal loads (MI355X guide 'nt-weights'); measured in the
+    // generation loop's replayed ticks it is slower (16.2 -> 17.1 us for 128 x 19456 x 1024)
+    // and leaves the persistent loop's prologue unchanged, so the default policy stays
+    static const bool nt = env_flag("SRNN_SKINNY_NT", 0) != 0;
+    auto k = nt ? skinny_kernel<T, TO, 128, BN, WM, WN, 1, NS, 2>
+                : skinny_kernel<T, TO, 128, BN, WM, WN, 1, NS>;
+    static bool attr[2] = {false, false};
+    if (!attr[nt]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, R::LDS));
-        attr = true;
+        attr[nt] = true;
     }
     hipLaunchKernelGGL(k, dim3(cdiv(g.N, BN), 1), dim3(256), R::LDS, s, g);
     SRNN_LAUNCH_CHECK();

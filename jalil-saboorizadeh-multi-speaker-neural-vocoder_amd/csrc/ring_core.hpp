@@ -66,7 +66,7 @@ struct Ring {
     static constexpr int RED = (WK - 1) * WM * WN * FM * FN * 4 * 64 * 4;
 };
 
-template <typename T, int ROWS, int I, class Map>
+template <typename T, int ROWS, int I, class Map, int AUX = 0>
 __device__ __forceinline__ void rc_issue(const T* __restrict__ base, int64_t ld, Map map, int k0,
                                          char* img, int wave, int lane) {
     constexpr int E = 16 / (int)sizeof(T);
@@ -76,13 +76,15 @@ __device__ __forceinline__ void rc_issue(const T* __restrict__ base, int64_t ld,
         const int row = c * 4 + (lane >> 4);
         const int slot = (lane & 15) ^ (row & 15);
         const T* src = base + (int64_t)map(row) * ld + k0 + slot * E;
-        __builtin_amdgcn_global_load_lds(RC_GLB(src), RC_LDS(img + c * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds(RC_GLB(src), RC_LDS(img + c * 1024), 16, 0, AUX);
     }
 }
 
 // acc += A[rows of tile] . B[rows of tile]^T over k in [0, K); ends with a barrier so
-// the ring can be reused by a following call.
-template <typename T, int BM, int BN, int WM, int WN, int WK, int NS, class MapA, class MapB>
+// the ring can be reused by a following call.  AUXB: cache policy of the B pieces (2 = nt,
+// for weights that this workgroup alone reads, once).
+template <typename T, int BM, int BN, int WM, int WN, int WK, int NS, class MapA, class MapB,
+          int AUXB = 0>
 __device__ __forceinline__ void ring_core(
     const T* __restrict__ A, int64_t lda, MapA mapA, const T* __restrict__ B, int64_t ldb,
     MapB mapB, int K, char* smem,
@@ -96,7 +98,8 @@ __device__ __forceinline__ void ring_core(
     auto issue = [&](int kt) {
         char* slot = smem + (kt % NS) * R::SLOT;
         rc_issue<T, BM, R::IA>(A, lda, mapA, kt * R::KB, slot, wave, lane);
-        rc_issue<T, BN, R::IB>(B, ldb, mapB, kt * R::KB, slot + BM * R::KSB, wave, lane);
+        rc_issue<T, BN, R::IB, MapB, AUXB>(B, ldb, mapB, kt * R::KB, slot + BM * R::KSB, wave,
+                                           lane);
     };
 #pragma unroll
     for (int s = 0; s < NS - 1; ++s)
