@@ -1,0 +1,117 @@
+"""Data-parallel TBPTT with the real HIP model, world size 2 on one GPU.
+
+The driver's 8-GPU runs use RCCL; a one-GPU box cannot host two RCCL ranks, so this
+rehearsal runs both ranks on cuda:0 with the gloo backend (distributed.device_index maps
+LOCAL_RANK onto the visible devices).  What it covers that test_distributed_cpu's toy
+model does not: GradAllReduce's overlap hooks on the HIP autograd outputs (_TierFn /
+MLP), the late h0 group (grads only on reset chunks), the failure flag riding in the last
+bucket, the fused clip+Adam with NULL gradients, and the Trainer loop — checked against
+the reference's own full-batch trajectory (tests/golden/tbptt_t3.npz: B = 2, so each rank
+owns one stream row).  Tolerances as test_gpu_parity.test_tbptt_golden.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, name, overlap, q):
+    try:
+        sys.path[:0] = [HERE, os.path.join(HERE, 'golden'),
+                        os.path.join(os.path.dirname(HERE),
+                                     'jalil-saboorizadeh-multi-speaker-neural-vocoder_amd')]
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+        import distributed as D
+        import nn as snn
+        import optim
+        import recipe
+        import samplernn_hip as H
+        from conftest import golden
+        from test_gpu_parity import build
+        from trainer import Trainer
+        D.init(backend='gloo')
+        H.lib()
+        g = golden('tbptt_' + name)
+        cfg = recipe.CONFIGS[name]
+        m, pred = build(cfg, recipe.make_weights(cfg, int(g['weight_seed'])))
+        B = int(g['B'])
+        rows = D.shard_rows(B)
+        sync = D.GradAllReduce(bucket_mb=0.01,
+                               overlap_groups=D.readiness_groups(pred) if overlap else None)
+        opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=float(g['lr'])),
+                                      grad_sync=sync)
+        losses = []
+
+        def criterion(out, tgt):
+            loss = snn.sequence_nll_loss_bits(out, tgt)
+            losses.append(float(loss.detach()))
+            return loss
+        data = [(torch.from_numpy(g['input_%d' % s])[rows],
+                 torch.tensor([int(g['reset_%d' % s])] * (rows.stop - rows.start)),
+                 torch.from_numpy(g['target_%d' % s])[rows],
+                 torch.from_numpy(g['cond_%d' % s])[rows],
+                 torch.from_numpy(g['spk_%d' % s])[rows])
+                for s in range(int(g['n_steps']))]
+        tr = Trainer(pred, criterion, opt, data, True, None)
+        tr.run(1)
+        torch.cuda.synchronize()
+        H.check_persistent_errors()
+        glob = [D.mean_over_ranks(x) for x in losses]
+        params = {k: p.detach().cpu().numpy().copy() for k, p in pred.named_parameters()}
+        q.put((rank, glob, params, None))
+        D.barrier()
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    except Exception as e:          # surface the failure instead of a queue timeout
+        import traceback
+        q.put((rank, None, None, traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize('overlap', [True, False])
+def test_dp_two_ranks_match_reference_full_batch(hip, overlap):
+    from conftest import golden
+    name = 't3'
+    g = golden('tbptt_' + name)
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, overlap, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(2):
+        rank, losses, params, err = q.get(timeout=100)
+        assert err is None, 'rank %d failed:\n%s' % (rank, err)
+        got[rank] = (losses, params)
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    names = [str(s) for s in g['names']]
+    for rank in (0, 1):
+        losses, params = got[rank]
+        np.testing.assert_allclose(losses, g['losses'], atol=1e-4, rtol=0)
+        for k in names:
+            np.testing.assert_allclose(params[k], g['param_final/' + k], atol=2e-4, rtol=0,
+                                       err_msg='rank %d %s' % (rank, k))
+    # both ranks hold the same replica after every step
+    for k in names:
+        np.testing.assert_array_equal(got[0][1][k], got[1][1][k], err_msg=k)
