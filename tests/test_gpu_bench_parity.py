@@ -1,0 +1,76 @@
+"""Parity of the MEASURED path: bench.py's bf16 TBPTT step (configs[1]: 3-tier dim 1024,
+FS = [16, 4], cond 43, 6 speakers, B = 128 rows x T = 1024 -- the persistent XCD GRU sweeps,
+LDS-resident L1 gather, position-major dTab scatter, gemm3 epilogues, fused clip+Adam)
+against the fp32 HIP path, which is pinned to the reference's own goldens
+(test_gpu_parity.py).  Same weights (bench.make_model's seed), same synthetic chunks
+(bench.synth_batches), two TBPTT chunks (reset, then carried hidden state).
+
+Tolerances (bf16 operands with fp32 accumulation), set from the MI355X measurement
+(round 2: losses 6.6e-5 relative apart at most; gradient relative L2 error 0.2-0.5 % in the
+sample-level MLP, 1-7 % in the tiers, growing with the bf16 roundings carried through the
+recurrences, cosine >= 0.9978): the loss of each chunk (the 2nd and 3rd after clipped Adam
+steps, the 3rd on carried hidden states) within 3e-4 relative; every parameter gradient of
+the first chunk within 10 % relative L2 error and cosine >= 0.995 of the fp32 gradient.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+def _run(dtype, batches):
+    import bench
+    import nn as snn
+    import optim
+    _, pred = bench.make_model(dtype)
+    pred = pred.to(DEV)
+    opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3))
+    losses, grads = [], None
+    for n, (inp, reset, tgt, cnd, spk) in enumerate(batches):
+        opt.zero_grad()
+
+        def closure():
+            lp = pred(inp, reset, cnd, spk)
+            loss = snn.sequence_nll_loss_bits(lp, tgt)
+            loss.backward()
+            return loss
+        if n == 0:
+            # gradients of the first chunk, before the clamp + Adam
+            loss = closure()
+            grads = {k: p.grad.detach().float().cpu().clone()
+                     for k, p in pred.named_parameters() if p.grad is not None}
+            opt.zero_grad()
+            pred.reset_hidden_states()
+        losses.append(float(opt.step(closure).detach()))
+    torch.cuda.synchronize()
+    import samplernn_hip as H
+    H.check_persistent_errors()
+    return losses, grads
+
+
+def test_bench_bf16_step_matches_fp32(hip):
+    import bench
+    B, T, L = 128, 1024, 64
+    batches = bench.gpu_batches(bench.synth_batches(B, T, L, 3, 0), DEV)
+    l32, g32 = _run(torch.float32, batches)
+    l16, g16 = _run(torch.bfloat16, batches)
+    print('losses fp32', l32, 'bf16', l16)
+    np.testing.assert_allclose(l16, l32, rtol=3e-4, atol=0)
+    assert g16.keys() == g32.keys()
+    worst = []
+    for k in g32:
+        a, b = g16[k].double().reshape(-1), g32[k].double().reshape(-1)
+        nb = b.norm().item()
+        if nb == 0.0:
+            assert a.norm().item() == 0.0, k
+            continue
+        rel = (a - b).norm().item() / nb
+        cos = (a @ b).item() / (a.norm().item() * nb)
+        worst.append((rel, cos, k))
+    worst.sort(reverse=True)
+    for rel, cos, k in worst:
+        print('%-60s rel %.4f cos %.6f' % (k, rel, cos))
+    for rel, cos, k in worst:
+        assert rel < 0.1 and cos >= 0.995, (k, rel, cos)
