@@ -153,6 +153,11 @@ __device__ __forceinline__ void l1l_add8(const uint4 v, float (&a)[8], l1_bf16x2
     }
 }
 
+// RPT: rows per thread per batch row (Tlen <= RPT * L1L_NT / 2), compile-time so the prefetch
+// registers of unused rows are not allocated: at 1024 threads a wave has 128 VGPRs, and the
+// spills of RPT = 4 at Tlen = 1024 put scratch reloads -- each waiting, vmcnt being in order,
+// for every store issued before it -- inside the row loop
+template <int RPT>
 __global__ __launch_bounds__(L1L_NT, 1) void mlp_l1_lds_kernel(
     const bf16* __restrict__ tab, const int64_t* __restrict__ x, int64_t ldx, int xoff, int B,
     int Tlen, int bpc, const bf16* __restrict__ upper, int64_t ldu, bf16* __restrict__ out,
@@ -185,16 +190,16 @@ __global__ __launch_bounds__(L1L_NT, 1) void mlp_l1_lds_kernel(
     }
     // the next batch row's indices and `upper` rows are loaded into registers one batch
     // row ahead (loads in flight across the current row's gathers), written / used after
-    constexpr int RPT = 4;                                   // rows per thread per batch row
     const int nrt = (Tlen + L1L_NT / 2 - 1) / (L1L_NT / 2);
     const int h = tid & 1, t0 = tid >> 1;
-    int64_t xn[2];
+    // (the low 32-bit word of each int64 index: indices are < Q)
+    unsigned xn[2];
     auto load_x = [&](int b) {
-        const int64_t* xr = x + (int64_t)b * ldx + xoff;
+        const unsigned* xr = reinterpret_cast<const unsigned*>(x + (int64_t)b * ldx + xoff);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int p = tid + j * L1L_NT;
-            xn[j] = xr[min(p, W - 1)];
+            xn[j] = xr[2 * min(p, W - 1)];
         }
     };
     auto put_x = [&](unsigned char* dst) {
@@ -291,14 +296,16 @@ static int mlp_l1_launch(const T* tab, const int64_t* x, int64_t ldx, int xoff, 
             const int nrc = std::max(1, std::min(B, 256 / ncg));
             const int bpc = (B + nrc - 1) / nrc;
             const int nrc2 = (B + bpc - 1) / bpc;
-            static bool attr = false;
-            if (!attr) {
-                SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)mlp_l1_lds_kernel,
+            const int nrt = (Tlen + L1L_NT / 2 - 1) / (L1L_NT / 2);
+            auto kern = nrt <= 2 ? mlp_l1_lds_kernel<2> : mlp_l1_lds_kernel<4>;
+            static bool attr[2] = {false, false};
+            if (!attr[nrt > 2]) {
+                SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)kern,
                                                    hipFuncAttributeMaxDynamicSharedMemorySize,
                                                    160 * 1024));
-                attr = true;
+                attr[nrt > 2] = true;
             }
-            hipLaunchKernelGGL(mlp_l1_lds_kernel, dim3(ncg * nrc2), dim3(L1L_NT), lds, s,
+            hipLaunchKernelGGL(kern, dim3(ncg * nrc2), dim3(L1L_NT), lds, s,
                                (const bf16*)tab, x, ldx, xoff, B, Tlen, bpc, (const bf16*)upper,
                                ldu, (bf16*)out, ldo, D, bits, ldb);
             SRNN_LAUNCH_CHECK();
