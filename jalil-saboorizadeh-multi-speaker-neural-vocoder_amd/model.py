@@ -552,7 +552,14 @@ class _MlpFn(torch.autograd.Function):
                          H.dcode(upper), H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
         W_hid = _wcast(mlp.hidden, T).reshape(D, D)
         W_out = _wcast(mlp.output, T).reshape(Q, D)
+        probe = H.ROOF_EVENTS
+        if probe is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         a2 = H.linear(a1, W_hid, bias=mlp.hidden.bias, relu=True, out_dtype=T, bits_out=m2)
+        if probe is not None:
+            ev[1].record()
+            probe.append(ev)
         z = H.linear(a2, W_out, bias=mlp.output.bias)                    # (B*T, Q) fp32
         logp = torch.empty((B * Tl, Q), device=dev, dtype=torch.float32)
         H.lib().call('srnn_logsoftmax_nll', H.ptr(z), Q, None, 0, Tl, B * Tl, Q, None,

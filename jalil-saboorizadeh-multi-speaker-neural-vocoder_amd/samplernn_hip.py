@@ -167,6 +167,11 @@ def exported_symbols():
 # the current stream wait for every gradient all-reduce already in flight.
 BEFORE_PERSISTENT = []
 
+# Measurement hook (bench.py): when a list, the sample-level MLP's hidden-layer GEMM -- the
+# bench's roofline kernel -- is bracketed by HIP events on its stream at every launch and the
+# (start, end) pairs are appended, so its duration is measured inside the timed TBPTT steps
+ROOF_EVENTS = None
+
 
 def before_persistent_sweep():
     for f in BEFORE_PERSISTENT:
