@@ -172,6 +172,11 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
     const unsigned strip_base =
         (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)strip;
     unsigned long long colacc = 0;
+    // per-lane part of the 16 atomics' addresses (column, tap (j - li) mod 16): loop
+    // invariant; the index part q_j * (CW FS 8) is wave-uniform and added from a scalar
+    unsigned lb[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) lb[j] = acc_base + ((unsigned)(coff + ((j - li) & 15)) << 3);
     for (int b = wave; b < nbb; b += DTAB_NT / 64) {
         const T* drow = dcol + (int64_t)(b0 + b) * Tlen * ldda;
         const int64_t* srow = x + (int64_t)(b0 + b) * ldx + xoff;
@@ -210,10 +215,15 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
             // would hold the second until the first had read its operands)
             unsigned ad[16];
             unsigned long long va[16];
+            // the batch's 16 indices are the same in every lane (one broadcast LDS read):
+            // extracted on the scalar unit
+            unsigned qs[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) qs[w] = __builtin_amdgcn_readfirstlane(qc[w]);
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                const unsigned q = (qc[j >> 2] >> (8 * (j & 3))) & 0xffu;
-                ad[j] = acc_base + ((q * (CW * FS) + (unsigned)(coff + ((j - li) & 15))) << 3);
+                const unsigned q = (qs[j >> 2] >> (8 * (j & 3))) & 0xffu;
+                ad[j] = lb[j] + q * (unsigned)(CW * FS * 8);
                 va[j] = (unsigned long long)(li <= j ? nv : cur);   // row enters at tap 0
             }
             if (jmax == 16) {
