@@ -254,13 +254,14 @@ class _TierFn(torch.autograd.Function):
             h_in = h0.detach().reshape(L, 1, D).expand(L, B, D).contiguous()
         else:
             h_in = hidden.float().contiguous()
-        Wih, Whh, bih, bhh = [], [], [], []
+        Wih, Whh, WhhF, bih, bhh = [], [], [], [], []
         xs, outs, outsT, gates = [], [], [], []
         X = x0
         for l in range(L):
             wih, whh, b_ih, b_hh = next(it), next(it), next(it), next(it)
             Wih.append(H.cast_param(wih, T))
             Whh.append(H.cast_param(whh, T))
+            WhhF.append(whh)
             bih.append(b_ih)
             bhh.append(b_hh)
             XT = H.cast(X, T)
@@ -320,7 +321,7 @@ class _TierFn(torch.autograd.Function):
         ctx.dims = (B, Fr, nfs, D, L, k)
         ctx.T = T
         ctx.save_for_backward(prevT, condT, spk_embT, spk_flat, h_in, W_ie, W_c, W_s, W_up,
-                              *Wih, *Whh, *xs, *outs, *outsT, *gates)
+                              *Wih, *Whh, *xs, *outs, *outsT, *gates, *WhhF)
         ctx.mark_non_differentiable(h_new)
         return Y.reshape(B, Fr * k, D), h_new
 
@@ -335,6 +336,7 @@ class _TierFn(torch.autograd.Function):
         r = sv[9:]
         Wih, Whh = r[:L], r[L:2 * L]
         xs, outs, outsT, gates = r[2 * L:3 * L], r[3 * L:4 * L], r[4 * L:5 * L], r[5 * L:6 * L]
+        WhhF = r[6 * L:7 * L]                     # the fp32 parameters W_hh
         dev = dY.device
         st = H.stream
         M = B * Fr
@@ -362,8 +364,9 @@ class _TierFn(torch.autograd.Function):
         dh_in = [None] * L
         for l in reversed(range(L)):
             dOut = dX.reshape(B, Fr, D)
-            # W_hh^T (D, 3D): k-contiguous operand for the deep-ring backward kernel
-            WhhT = H.permute3(Whh[l].float().reshape(1, 3 * D, D), (0, 2, 1), dtype=T)
+            # W_hh^T (D, 3D): k-contiguous operand for the deep-ring backward kernel, straight
+            # from the fp32 parameter (the same bf16 values as the forward's copy, no cast pass)
+            WhhT = H.permute3(WhhF[l].detach().reshape(1, 3 * D, D), (0, 2, 1), dtype=T)
             xbw = H.gru_xcd_bwd_work_bytes(T, B, D) if lp else 0
             seq = lp and (xbw > 0 or H.gru_seq_supported(T, B, D))
             ddir = [torch.empty((B, D), device=dev, dtype=torch.float32) for _ in range(2)]
