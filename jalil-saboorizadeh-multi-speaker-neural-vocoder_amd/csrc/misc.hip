@@ -746,6 +746,9 @@ int srnn_colsum_impl(int dtype, const void* src, int64_t lds, int64_t rows, int 
     // ~2048 blocks in the first pass, at least 64 rows per block, partials within `work`
     int64_t nrb = std::max<int64_t>(1, std::min<int64_t>(2048 / cblk, rows / 64));
     nrb = std::min<int64_t>(nrb, work_elems / cols);
+    // few rows (per-row bias sums of the GRU sweeps, speaker rows: B = 128): one pass -- a
+    // second launch costs more than the rows it would parallelise
+    if (rows <= 256 && cblk >= 16) nrb = 1;
     if (rows <= 0 || nrb <= 1) {
         if (dtype == SRNN_F32)
             colsum_pass<float>((const float*)src, lds, rows, cols, std::max<int64_t>(rows, 1), 1,
