@@ -29,7 +29,7 @@ import utils
 import samplernn_hip as H
 
 verbose = False
-_STATS = {'fused_colsum': 0}     # (tests) how often a fused side result was consumed
+_STATS = {'fused_colsum': 0, 'fused_lp': 0}     # (tests) how often a fused side result was consumed
 
 
 def _default_dtype():
@@ -345,7 +345,14 @@ class _TierFn(torch.autograd.Function):
             dY2 = dYT = dY.reshape(M, k * D).contiguous()
         else:
             dY2 = dY.reshape(M, k * D).float().contiguous()
-            dYT = H.cast(dY2, T)
+            # the tier below already cast this gradient (its dx0) to the compute dtype
+            lpc = getattr(dY, '_srnn_lp', None)
+            if lpc is not None and lpc[1] == dY._version and lpc[0].dtype == T and \
+                    lpc[0].numel() == dY2.numel() and dY2.data_ptr() == dY.data_ptr():
+                dYT = lpc[0].reshape(M, k * D)
+                _STATS['fused_lp'] += 1
+            else:
+                dYT = H.cast(dY2, T)
         # weight gradient transposed, [i][j*D + o]: one row per input channel for the
         # per-channel weight-norm backward (no permute of the 16 x D x D gradient)
         dWupT = H.gemm(outsT[-1].reshape(M, D), dYT, transA=True)         # (D, k*D)
@@ -446,6 +453,8 @@ class _TierFn(torch.autograd.Function):
         g_ie = nn.weight_grad_to_params(mod.input_expand, dW_ie.reshape(D, nfs, 1))
         g_ie_b = H.colsum(dx0, M, D)
         d_upper = dx0.reshape(B, Fr, D) if ctx.has_upper else None
+        if d_upper is not None and dx0T is not dx0:
+            d_upper._srnn_lp = (dx0T, d_upper._version)     # (the upper tier's dY cast)
         grads = g_ie + [g_ie_b]
         if mod.is_cond:
             C = condT.shape[1]

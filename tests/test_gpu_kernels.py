@@ -610,7 +610,50 @@ def test_fused_upsampling_bias_grad_in_step(hip):
     torch.testing.assert_close(bot.upsampling.bias.grad, grad_fused, atol=1e-7, rtol=1e-5)
 
 
-@pytest.mark.parametrize('perm', [(0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1),
+def test_upper_tier_reuses_lower_bf16_gradient(hip):
+    """bf16 step: the top tier's upsampling backward takes the compute-dtype copy of its
+    output gradient from the bottom tier (which cast its dx0 for its own weight gradients)
+    instead of casting again; every top-tier gradient equals the un-fused step's bit for bit."""
+    import model as M
+    import nn as snn
+    torch.manual_seed(5)
+    m = M.SampleRNN([16, 4], 1, 1024, True, 256, True, False, 43, 6)
+    m.compute_dtype = torch.bfloat16
+    pred = M.Predictor(m).to(DEV)
+    B, T, L = 2, 128, 64
+    g = torch.Generator().manual_seed(6)
+    inp = torch.randint(0, 256, (B, L + T - 1), generator=g).to(DEV)
+    tgt = torch.randint(0, 256, (B, T), generator=g).to(DEV)
+    cond = torch.rand(B, T // L, 43, generator=g).to(DEV)
+    spk = torch.tensor([[2], [5]], device=DEV)
+    top = m.frame_level_rnns[1]
+    grads = []
+    for fused in (True, False):
+        for p in pred.parameters():
+            p.grad = None
+        pred.reset_hidden_states()
+        before = M._STATS['fused_lp']
+        loss = snn.sequence_nll_loss_bits(pred(inp, True, cond, spk), tgt)
+        orig = M._TierFn.backward
+
+        def strip(ctx, dY, dh_new):
+            if hasattr(dY, '_srnn_lp'):
+                del dY._srnn_lp
+            return orig(ctx, dY, dh_new)
+        if not fused:
+            M._TierFn.backward = staticmethod(strip)
+        try:
+            loss.backward()
+        finally:
+            M._TierFn.backward = staticmethod(orig)
+        assert M._STATS['fused_lp'] == before + (1 if fused else 0)
+        grads.append({k: p.grad.clone() for k, p in top.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys()
+    for k in grads[0]:
+        assert torch.equal(grads[0][k], grads[1][k]), k
+
+
+@pytest.mark.parametrize('perm',[(0, 1, 2), (0, 2, 1), (1, 0, 2), (1, 2, 0), (2, 0, 1),
                                   (2, 1, 0)])
 @pytest.mark.parametrize('shape', [(3, 37, 70), (16, 64, 33), (1, 1, 5)])
 def test_permute3(hip, perm, shape):
