@@ -99,6 +99,13 @@ int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t l
                      const float* h0, const void* whh, const float* bhh, float* out,
                      void* out_lp, int64_t ldo, int64_t so, float* gates, int64_t ldg,
                      int64_t sg, void* work, size_t work_bytes, void* stream);
+/* srnn_gru_xcd_fwd that also writes the previous-state sequence the W_hh gradient consumes,
+ * hprev_lp[b][t] = bf16(t == 0 ? h0[b] : out[b][t - 1]) (same ldo / so layout as out_lp), so the
+ * backward needs no shifted copy (model.py:222-244 carry; hprev_lp may be null). */
+int srnn_gru_xcd_fwd2(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi, int64_t sgi,
+                      const float* h0, const void* whh, const float* bhh, float* out,
+                      void* out_lp, int64_t ldo, int64_t so, float* gates, int64_t ldg,
+                      int64_t sg, void* hprev_lp, void* work, size_t work_bytes, void* stream);
 /* Reverse sweep of one layer in the same organisation (W_hh^T K-slices in VGPRs, dgh
  * hand-offs as granules): same operands and outputs as srnn_gru_seq_bwd; work =
  * srnn_gru_xcd_bwd_work_bytes(dtype, B, D) bytes. */

@@ -44,6 +44,7 @@ struct GruXArgs {
     const float* h0;                                // (B, D) fp32
     const bf16* whh; const float* bhh;
     float* out; bf16* out_lp; int64_t ldo; int64_t so;
+    bf16* hp_lp;                                    // optional: h_{t-1} (bf16), same layout as out
     float* gates; int64_t ldg; int64_t sg;          // r | z | n | gh_n per row and step
     u64* xh;                                        // 2 x G x RG x D/2 granules
     int* census;                                    // [G][P] zeroed slots, or null (global mode)
@@ -112,6 +113,8 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     const int unit = u0 + uu;
     const float bhr = a.bhh[unit], bhz = a.bhh[D + unit], bhn = a.bhh[2 * D + unit];
     float hprev = a.h0[(int64_t)b * D + unit];
+    // the previous-state sequence for the backward's W_hh gradient: [h0, h_0 .. h_{F-2}]
+    if (a.hp_lp && wr) a.hp_lp[(int64_t)b * a.ldo + unit] = __float2bfloat16(hprev);
     const __amdgpu_buffer_rsrc_t rx = hx_rsrc(a.xh);
     const size_t bufw = (size_t)a.G * RG * DG;                  // granules per buffer
     auto publish = [&](int s, float h) {        // h_s -> buffer (s + 1) & 1, tag s + 2
@@ -218,6 +221,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
                 const int64_t o = (int64_t)b * a.ldo + (int64_t)t * a.so + unit;
                 a.out[o] = hn;
                 a.out_lp[o] = __float2bfloat16(hn);
+                if (a.hp_lp && t + 1 < a.Fr) a.hp_lp[o + a.so] = __float2bfloat16(hn);
                 float* gt = a.gates + (int64_t)b * a.ldg + (int64_t)t * a.sg;
                 gt[unit] = rr; gt[D + unit] = zz; gt[2 * D + unit] = nn; gt[3 * D + unit] = ghn;
             }
@@ -470,11 +474,11 @@ extern "C" size_t srnn_gru_xcd_work_bytes(int dtype, int B, int D) {
     return gx::HDR + (size_t)2 * G * gx::RG * (D / 2) * 8;
 }
 
-extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
-                                int64_t sgi, const float* h0, const void* whh, const float* bhh,
-                                float* out, void* out_lp, int64_t ldo, int64_t so, float* gates,
-                                int64_t ldg, int64_t sg, void* work, size_t work_bytes,
-                                void* stream) {
+extern "C" int srnn_gru_xcd_fwd2(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
+                                 int64_t sgi, const float* h0, const void* whh, const float* bhh,
+                                 float* out, void* out_lp, int64_t ldo, int64_t so, float* gates,
+                                 int64_t ldg, int64_t sg, void* hprev_lp, void* work,
+                                 size_t work_bytes, void* stream) {
     const size_t need = srnn_gru_xcd_work_bytes(dtype, B, D);
     SRNN_REQUIRE(need > 0, "gru_xcd: shape/device not supported");
     SRNN_REQUIRE(work && work_bytes >= need, "gru_xcd: workspace %zu < %zu", work_bytes, need);
@@ -486,6 +490,7 @@ extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi
     a.gi = gi; a.ldgi = ldgi; a.sgi = sgi;
     a.h0 = h0; a.whh = (const bf16*)whh; a.bhh = bhh;
     a.out = out; a.out_lp = (bf16*)out_lp; a.ldo = ldo; a.so = so;
+    a.hp_lp = (bf16*)hprev_lp;
     a.gates = gates; a.ldg = ldg; a.sg = sg;
     a.err = (int*)work;
     a.sticky = srnn_sticky_flag();
@@ -526,6 +531,15 @@ extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi
     hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
+                                int64_t sgi, const float* h0, const void* whh, const float* bhh,
+                                float* out, void* out_lp, int64_t ldo, int64_t so, float* gates,
+                                int64_t ldg, int64_t sg, void* work, size_t work_bytes,
+                                void* stream) {
+    return srnn_gru_xcd_fwd2(dtype, B, D, Fr, gi, ldgi, sgi, h0, whh, bhh, out, out_lp, ldo, so,
+                             gates, ldg, sg, nullptr, work, work_bytes, stream);
 }
 
 

@@ -255,7 +255,7 @@ class _TierFn(torch.autograd.Function):
         else:
             h_in = hidden.float().contiguous()
         Wih, Whh, WhhF, bih, bhh = [], [], [], [], []
-        xs, outs, outsT, gates = [], [], [], []
+        xs, outs, outsT, gates, hprevs = [], [], [], [], []
         X = x0
         for l in range(L):
             wih, whh, b_ih, b_hh = next(it), next(it), next(it), next(it)
@@ -275,13 +275,17 @@ class _TierFn(torch.autograd.Function):
             seq = lp and (xw > 0 or H.gru_seq_supported(T, B, D))
             if seq:
                 H.before_persistent_sweep()
+            hprevT = None
             if xw > 0:
-                # whole sequence in one persistent launch, row groups per XCD, W_hh in VGPRs
+                # whole sequence in one persistent launch, row groups per XCD, W_hh in VGPRs;
+                # it also writes the previous-state sequence [h0, h_0 .. h_{F-2}] in bf16 for
+                # the backward's W_hh gradient
                 work = torch.empty(xw, device=dev, dtype=torch.uint8)
-                H.lib().call('srnn_gru_xcd_fwd', H.dcode(T), B, D, Fr, H.ptr(gi), Fr * 3 * D,
+                hprevT = torch.empty((B, Fr, D), device=dev, dtype=T)
+                H.lib().call('srnn_gru_xcd_fwd2', H.dcode(T), B, D, Fr, H.ptr(gi), Fr * 3 * D,
                              3 * D, H.ptr(hpf), H.ptr(Whh[l]), H.ptr(b_hh), H.ptr(out),
-                             H.ptr(outT), Fr * D, D, H.ptr(gt), Fr * 4 * D, 4 * D, H.ptr(work),
-                             xw, H.stream())
+                             H.ptr(outT), Fr * D, D, H.ptr(gt), Fr * 4 * D, 4 * D,
+                             H.ptr(hprevT), H.ptr(work), xw, H.stream())
             elif seq:
                 # whole sequence in one persistent launch (W_hh resident in LDS)
                 work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
@@ -300,6 +304,7 @@ class _TierFn(torch.autograd.Function):
                              H.ptr(outT[:, t]) if lp else None, Fr * D, H.ptr(gt[:, t]),
                              Fr * 4 * D, H.stream())
             xs.append(XT)
+            hprevs.append(hprevT)
             outs.append(out)
             outsT.append(outT)
             gates.append(gt)
@@ -321,7 +326,7 @@ class _TierFn(torch.autograd.Function):
         ctx.dims = (B, Fr, nfs, D, L, k)
         ctx.T = T
         ctx.save_for_backward(prevT, condT, spk_embT, spk_flat, h_in, W_ie, W_c, W_s, W_up,
-                              *Wih, *Whh, *xs, *outs, *outsT, *gates, *WhhF)
+                              *Wih, *Whh, *xs, *outs, *outsT, *gates, *WhhF, *hprevs)
         ctx.mark_non_differentiable(h_new)
         return Y.reshape(B, Fr * k, D), h_new
 
@@ -337,6 +342,7 @@ class _TierFn(torch.autograd.Function):
         Wih, Whh = r[:L], r[L:2 * L]
         xs, outs, outsT, gates = r[2 * L:3 * L], r[3 * L:4 * L], r[4 * L:5 * L], r[5 * L:6 * L]
         WhhF = r[6 * L:7 * L]                     # the fp32 parameters W_hh
+        hprevs = r[7 * L:8 * L]                   # [h_in, out[:, :F-1]] in T, or None
         dev = dY.device
         st = H.stream
         M = B * Fr
@@ -425,13 +431,16 @@ class _TierFn(torch.autograd.Function):
             # dh_0 = dgh_0 . W_hh + dh_direct, as an NT product on W_hh^T (skinny ring path)
             dh_in[l] = H.gemm(dGHT[:, 0], WhhT, transB=True, M=B, N=D, K=3 * D,
                               lda=Fr * 3 * D, ldb=3 * D, cin=ddir[0], beta=1.0)
-            # previous hidden states of every step: [h_in, out[:, :F-1]]
-            hprevT = torch.empty((B, Fr, D), device=dev, dtype=T)
-            H.lib().call('srnn_copy2d', H.F32, H.dcode(T), B, D, H.ptr(h_in[l]), D,
-                         H.ptr(hprevT), Fr * D, st())
-            if Fr > 1:
-                H.lib().call('srnn_copy2d', H.dcode(T), H.dcode(T), B, (Fr - 1) * D,
-                             H.ptr(outsT[l]), Fr * D, H.ptr(hprevT[:, 1:]), Fr * D, st())
+            # previous hidden states of every step: [h_in, out[:, :F-1]] (written by the
+            # persistent forward sweep when it ran, else built here)
+            hprevT = hprevs[l]
+            if hprevT is None:
+                hprevT = torch.empty((B, Fr, D), device=dev, dtype=T)
+                H.lib().call('srnn_copy2d', H.F32, H.dcode(T), B, D, H.ptr(h_in[l]), D,
+                             H.ptr(hprevT), Fr * D, st())
+                if Fr > 1:
+                    H.lib().call('srnn_copy2d', H.dcode(T), H.dcode(T), B, (Fr - 1) * D,
+                                 H.ptr(outsT[l]), Fr * D, H.ptr(hprevT[:, 1:]), Fr * D, st())
             dW_hh = H.gemm(dGHT.reshape(M, 3 * D), hprevT.reshape(M, D), transA=True)
             if bsum is not None:
                 bs = H.colsum(bsum, B, 4 * D)               # sums of [dar | daz | dghn | dan]

@@ -70,6 +70,8 @@ _SIGS = {
                          _L, _L, _P, _P, _SZ, _P],
     'srnn_gru_xcd_fwd': [_I, _I, _I, _I, _P, _L, _L, _P, _P, _P, _P, _P, _L, _L, _P, _L, _L, _P,
                          _SZ, _P],
+    'srnn_gru_xcd_fwd2': [_I, _I, _I, _I, _P, _L, _L, _P, _P, _P, _P, _P, _L, _L, _P, _L, _L, _P,
+                          _P, _SZ, _P],
     'srnn_gru_xcd_bwd': [_I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L, _P, _P, _P, _P, _P,
                          _L, _L, _P, _P, _SZ, _P],
     'srnn_gru_xcd_bwd2': [_I, _I, _I, _I, _P, _L, _L, _P, _L, _L, _P, _L, _L, _P, _P, _P, _P, _P,

@@ -208,6 +208,21 @@ def test_gru_xcd_fwd(hip, B, D, Fr):
     torch.testing.assert_close(out.cpu(), ref_out, atol=2e-3, rtol=0)
     torch.testing.assert_close(gt.cpu(), ref_gt, atol=2e-3, rtol=0)
     torch.testing.assert_close(outT.float().cpu(), out.cpu().to(T).float(), atol=0, rtol=0)
+    # srnn_gru_xcd_fwd2: the same outputs bit for bit, plus [bf16(h0), outT[:, :F-1]]
+    out2 = torch.full_like(out, float('nan'))
+    outT2 = torch.zeros_like(outT)
+    gt2 = torch.full_like(gt, float('nan'))
+    hp = torch.full((B, Fr, D), float('nan'), device=DEV).to(T)
+    work.fill_(7)
+    hip.lib().call('srnn_gru_xcd_fwd2', hip.BF16, B, D, Fr, hip.ptr(gi), Fr * 3 * D, 3 * D,
+                   hip.ptr(h0), hip.ptr(whh), hip.ptr(bhh), hip.ptr(out2), hip.ptr(outT2), Fr * D,
+                   D, hip.ptr(gt2), Fr * 4 * D, 4 * D, hip.ptr(hp), hip.ptr(work), nb,
+                   hip.stream())
+    torch.cuda.synchronize()
+    assert hip.lib().dll.srnn_gru_xcd_error(hip.ptr(work)) == 0, 'gru_xcd gave up waiting'
+    assert torch.equal(out2, out) and torch.equal(outT2, outT) and torch.equal(gt2, gt)
+    assert torch.equal(hp[:, 0], h0.to(T))
+    assert torch.equal(hp[:, 1:], outT[:, :-1])
 
 
 @pytest.mark.parametrize('B,D,Fr', [(128, 1024, 64), (64, 1024, 5), (100, 256, 9), (16, 512, 3)])
