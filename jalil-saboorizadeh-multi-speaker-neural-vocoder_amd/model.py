@@ -270,8 +270,9 @@ class _TierFn(torch.autograd.Function):
             outT = torch.empty((B, Fr, D), device=dev, dtype=T) if lp else out
             gt = torch.empty((B, Fr, 4 * D), device=dev, dtype=torch.float32)
             hpf = h_in[l]
-            hpT = H.cast(hpf, T)
             xw = H.gru_xcd_work_bytes(T, B, D) if lp else 0
+            # (the XCD sweep reads the fp32 state itself; the other paths take a T copy)
+            hpT = H.cast(hpf, T) if xw == 0 else None
             seq = lp and (xw > 0 or H.gru_seq_supported(T, B, D))
             if seq:
                 H.before_persistent_sweep()
