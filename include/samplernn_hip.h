@@ -35,6 +35,10 @@ int srnn_uquantize_f64(const double* x, int64_t* out, int64_t n, int q_levels, v
  * (utils.py:18-19, mode 1); scale = 2 gives the model's `2 * dequantize` (model.py:385,471) */
 int srnn_udequantize(const int64_t* k, float* out, int64_t n, int q_levels, float scale,
                      int mode, void* stream);
+/* srnn_udequantize of a rows x cols window with row stride ldk (a slice of the index stream,
+ * model.py:385 `input_sequences[:, a:b]`) into contiguous rows (no copy of the slice first) */
+int srnn_udequantize2d(const int64_t* k, int64_t ldk, float* out, int rows, int cols,
+                       int q_levels, float scale, int mode, void* stream);
 
 /* ---- dense projections -------------------------------------------------------------
  * C = act(alpha * op(A) . op(B) + beta * Cin + bias)  (bias_mode 1: per column, 2: per row)

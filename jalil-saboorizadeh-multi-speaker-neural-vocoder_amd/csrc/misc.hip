@@ -76,11 +76,7 @@ __global__ void uquantize_f64_kernel(const double* __restrict__ x, int64_t* __re
 }
 
 // mode 0: mu-law (utils.py:62-63, LUT for q = 256), mode 1: linear (utils.py:18-19)
-__global__ void udequantize_kernel(const int64_t* __restrict__ k, float* __restrict__ out,
-                                   int64_t n, int q, float scale, int mode) {
-    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    int64_t kk = k[i];
+__device__ __forceinline__ float udeq_one(int64_t kk, int q, float scale, int mode) {
     float v;
     if (mode == 1) {
         v = (float)kk / (float)(q / 2) - 1.0f;
@@ -91,7 +87,24 @@ __global__ void udequantize_kernel(const int64_t* __restrict__ k, float* __restr
         float e = expf(fabsf(c) * 5.5451774444795623f) - 1.0f;
         v = (float)((c > 0) - (c < 0)) * e / 255.0f;
     }
-    out[i] = scale * v;
+    return scale * v;
+}
+
+__global__ void udequantize_kernel(const int64_t* __restrict__ k, float* __restrict__ out,
+                                   int64_t n, int q, float scale, int mode) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = udeq_one(k[i], q, scale, mode);
+}
+
+// strided rows (a window of the index stream) -> contiguous rows x cols
+__global__ void udequantize2d_kernel(const int64_t* __restrict__ k, int64_t ldk,
+                                     float* __restrict__ out, int cols, int64_t n, int q,
+                                     float scale, int mode) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t r = i / cols, c = i - r * cols;
+    out[i] = udeq_one(k[r * ldk + c], q, scale, mode);
 }
 
 extern "C" int srnn_uquantize_f32(const float* x, int64_t* out, int64_t n, int q, void* stream) {
@@ -116,6 +129,17 @@ extern "C" int srnn_udequantize(const int64_t* k, float* out, int64_t n, int q, 
     if (n <= 0) return 0;
     hipLaunchKernelGGL(udequantize_kernel, dim3(cdiv(n, 256)), dim3(256), 0,
                        (hipStream_t)stream, k, out, n, q, scale, mode);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int srnn_udequantize2d(const int64_t* k, int64_t ldk, float* out, int rows, int cols,
+                                  int q, float scale, int mode, void* stream) {
+    if (int e = ensure_tables()) return e;
+    const int64_t n = (int64_t)rows * cols;
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(udequantize2d_kernel, dim3(cdiv(n, 256)), dim3(256), 0,
+                       (hipStream_t)stream, k, ldk, out, cols, n, q, scale, mode);
     SRNN_LAUNCH_CHECK();
     return 0;
 }

@@ -528,7 +528,11 @@ class SampleLevelMLP(torch.nn.Module):
     def forward(self, prev_samples, upper_tier_conditioning):
         """model.py:308-325: indices (B, T+FS0-1), conditioning (B, T, D) -> log-probs (B,T,Q)."""
         H.need_cuda(upper_tier_conditioning)
-        x = prev_samples.to(upper_tier_conditioning.device).long().contiguous()
+        # (a window of the index stream is read in place: the kernels take a row stride)
+        x = prev_samples.to(upper_tier_conditioning.device).long()
+        if x.dim() != 2 or x.stride(1) != 1 or x.shape[1] != upper_tier_conditioning.shape[1] + \
+                self.frame_size - 1:
+            x = x.contiguous()
         u = upper_tier_conditioning
         if u.dtype not in (torch.float32, _dt(self)):
             u = u.float()
@@ -566,11 +570,11 @@ class _MlpFn(torch.autograd.Function):
         m1 = m2 = None
         if bits:
             m1, m2 = H.relu_bits(B * Tl, D, dev), H.relu_bits(B * Tl, D, dev)
-            H.lib().call('srnn_mlp_l1_bits', H.ptr(tab), H.ptr(x), x.shape[1], 0, B, Tl,
+            H.lib().call('srnn_mlp_l1_bits', H.ptr(tab), H.ptr(x), x.stride(0), 0, B, Tl,
                          H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.ptr(m1), m1.stride(0),
                          H.stream())
         else:
-            H.lib().call('srnn_mlp_l1', H.dcode(T), H.ptr(tab), H.ptr(x), x.shape[1], 0, B, Tl,
+            H.lib().call('srnn_mlp_l1', H.dcode(T), H.ptr(tab), H.ptr(x), x.stride(0), 0, B, Tl,
                          H.dcode(upper), H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
         W_hid = _wcast(mlp.hidden, T).reshape(D, D)
         W_out = _wcast(mlp.output, T).reshape(Q, D)
@@ -629,7 +633,7 @@ class _MlpFn(torch.autograd.Function):
         # gradient (its output is this layer's `upper`), handed over on the returned gradient
         colsum = torch.empty(FS0 * D, device=dev, dtype=torch.float32)
         done = ctypes.c_int(0)
-        H.lib().call('srnn_mlp_dtab2', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.shape[1], 0, B,
+        H.lib().call('srnn_mlp_dtab2', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.stride(0), 0, B,
                      Tl, H.ptr(dtabT), H.dcode(T), D, FS0, Q, H.ptr(work), work.numel() * 8,
                      H.ptr(colsum), ctypes.byref(done), st())
         dE = H.gemm(dtabT, Wp.reshape(FS0 * D, Q))                       # (Q, Q)
@@ -689,7 +693,7 @@ class Predictor(Runner, torch.nn.Module):
         upper = None
         for rnn in reversed(self.model.frame_level_rnns):
             n = rnn.n_frame_samples
-            seg = input_sequences[:, L - n: input_sequences.shape[1] - n + 1].contiguous()
+            seg = input_sequences[:, L - n: input_sequences.shape[1] - n + 1]
             prev = utils._dequant(seg, q, 2.0, mode)                    # 2 * dequantize
             prev = prev.view(batch_size, -1, n)
             if upper is None:

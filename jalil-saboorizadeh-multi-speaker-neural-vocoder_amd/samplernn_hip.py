@@ -31,6 +31,7 @@ _SIGS = {
     'srnn_uquantize_f32': [_P, _P, _L, _I, _P],
     'srnn_uquantize_f64': [_P, _P, _L, _I, _P],
     'srnn_udequantize': [_P, _P, _L, _I, _F, _I, _P],
+    'srnn_udequantize2d': [_P, _L, _P, _I, _I, _I, _F, _I, _P],
     'srnn_uquantize_f64_host': [_P, _P, _L, _I],
     'srnn_uquantize_f32_host': [_P, _P, _L, _I],
     'srnn_udequantize_host': [_P, _P, _L, _I],

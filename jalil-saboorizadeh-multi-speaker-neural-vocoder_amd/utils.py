@@ -78,6 +78,13 @@ def uquantize(samples, q_levels):
 
 
 def _dequant(samples, q_levels, scale, mode=0):
+    if samples.is_cuda and samples.dtype == torch.long and samples.dim() == 2 and \
+            samples.stride(1) == 1 and not samples.is_contiguous():
+        # a window of the index stream: read in place (no copy of the slice first)
+        out = torch.empty(samples.shape, dtype=torch.float32, device=samples.device)
+        H.lib().call('srnn_udequantize2d', H.ptr(samples), samples.stride(0), H.ptr(out),
+                     samples.shape[0], samples.shape[1], q_levels, scale, mode, H.stream())
+        return out
     k = samples.long().contiguous()
     out = torch.empty(k.shape, dtype=torch.float32, device=k.device)
     H.lib().call('srnn_udequantize', H.ptr(k), H.ptr(out), k.numel(), q_levels, scale, mode,

@@ -478,6 +478,20 @@ def test_uquantize_f32_exhaustive(hip):
             assert torch.equal(q, ref), 'mismatch in chunk %x' % lo
 
 
+@pytest.mark.parametrize('mode', [0, 1])
+def test_udequantize_window_in_place(hip, mode):
+    """srnn_udequantize2d on a strided window of the index stream (Predictor's per-tier
+    slices) equals srnn_udequantize of the copied slice, bit for bit."""
+    import utils
+    g = torch.Generator().manual_seed(11)
+    seq = torch.randint(0, 256, (5, 300), generator=g).to(DEV)
+    win = seq[:, 37:37 + 211]
+    assert not win.is_contiguous()
+    got = utils._dequant(win, 256, 2.0, mode)
+    want = utils._dequant(win.contiguous(), 256, 2.0, mode)
+    assert torch.equal(got, want)
+
+
 def test_uquantize_kats(hip):
     g = golden('ulaw')
     import utils
