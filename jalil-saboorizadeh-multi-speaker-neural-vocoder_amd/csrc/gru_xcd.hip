@@ -22,10 +22,11 @@
 
 namespace gx {
 constexpr int NW = 8, NTHR = NW * 64;
-constexpr int RG = 16;                 // rows per group
+constexpr int RG = 16;                 // rows per tile (one MFMA M tile)
 constexpr int CU = 32;                 // units per workgroup
 constexpr int NT = 6;                  // n tiles: 3 gates x 2 x 16 units
 constexpr int UK = 32;                 // k per bf16 MFMA unit
+constexpr int MAXMT = 4;               // row tiles per group (B up to 512 rows at D = 1024)
 // work header: [0] error word, ints [16, HDR / 4) the placement-check slots ([G][P])
 constexpr int HDR = 2048;
 }  // namespace gx
@@ -39,6 +40,12 @@ __device__ __forceinline__ void gx_note_failure(const int* err, int* sticky) {
         __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Row layout of a sweep (host-chosen, gx_layout): G groups x MT tiles of RV <= 16 valid rows;
+// tile m of group g holds batch rows [(g MT + m) RV, +RV).  MT > 1 (B > 16 G: several
+// 128-row sets per launch) runs the tiles of one step back to back in every workgroup, so
+// one tile's hand-off latency hides behind the others' work; RV < 16 (B < 128) keeps all
+// eight XCDs busy with fewer rows each.  Hand-off slots are indexed per tile with a 16-row
+// stride whatever RV is.
 struct GruXArgs {
     const float* gi; int64_t ldgi; int64_t sgi;     // gi[b][t] (3D, includes b_ih)
     const float* h0;                                // (B, D) fp32
@@ -46,23 +53,23 @@ struct GruXArgs {
     float* out; bf16* out_lp; int64_t ldo; int64_t so;
     bf16* hp_lp;                                    // optional: h_{t-1} (bf16), same layout as out
     float* gates; int64_t ldg; int64_t sg;          // r | z | n | gh_n per row and step
-    u64* xh;                                        // 2 x G x RG x D/2 granules
+    u64* xh;                                        // 2 x G x MT x RG x D/2 granules
     int* census;                                    // [G][P] zeroed slots, or null (global mode)
     int* err;
     int* sticky;                                    // persist.hip flag
     int spin_limit;
     int withhold;                                   // test switch: workgroup 0 never publishes
-    int B, D, Fr, G, P;
+    int B, D, Fr, G, P, RV;
     int poll_sleep;                                 // s_sleep 1 repeats between polls
     unsigned long long* diag;                       // optional phase timestamps (timing only)
 };
 
-template <int UPW>
+template <int UPW, int MT>
 __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     using namespace gx;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int D = a.D, B = a.B;
+    const int D = a.D, B = a.B, RV = a.RV;
     const int NU = D / UK, KW = NW < NU ? NW : NU;
     floatx4* red = (floatx4*)smem;                              // [KW][NT][64]
     int* gsh = (int*)(smem + (size_t)KW * NT * 64 * sizeof(floatx4));
@@ -106,40 +113,52 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     __syncthreads();
     const bool local = gsh[2] != 0;
     if (dg) dg[255] = local ? 1 : 2;
-    // ---- this thread's state element: row r of the group, unit u0 + uu
+    // ---- this thread's state elements: row r of each tile, unit u0 + uu
     const int r = tid >> 5, uu = tid & 31;
-    const int b = min(g * RG + r, B - 1);
-    const bool wr = g * RG + r < B;
+    const bool rv = r < RV;
     const int unit = u0 + uu;
+    auto row_of = [&](int m) { return (g * MT + m) * RV + r; };
     const float bhr = a.bhh[unit], bhz = a.bhh[D + unit], bhn = a.bhh[2 * D + unit];
-    float hprev = a.h0[(int64_t)b * D + unit];
-    // the previous-state sequence for the backward's W_hh gradient: [h0, h_0 .. h_{F-2}]
-    if (a.hp_lp && wr) a.hp_lp[(int64_t)b * a.ldo + unit] = __float2bfloat16(hprev);
+    float hprev[MT];
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int row = row_of(m);
+        const int b = min(row, B - 1);
+        hprev[m] = a.h0[(int64_t)b * D + unit];
+        // the previous-state sequence for the backward's W_hh gradient: [h0, h_0 .. h_{F-2}]
+        if (a.hp_lp && rv && row < B)
+            a.hp_lp[(int64_t)b * a.ldo + unit] = __float2bfloat16(hprev[m]);
+    }
     const __amdgpu_buffer_rsrc_t rx = hx_rsrc(a.xh);
-    const size_t bufw = (size_t)a.G * RG * DG;                  // granules per buffer
-    auto publish = [&](int s, float h) {        // h_s -> buffer (s + 1) & 1, tag s + 2
+    const size_t bufw = (size_t)a.G * MT * RG * DG;             // granules per buffer
+    auto publish = [&](int s, int m, float h) {   // h_s of tile m -> buffer (s + 1) & 1, tag s + 2
         const uint32_t mine = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(h));
         const uint32_t nb = lane_next16(mine);
         if ((uu & 1) == 0 && !(a.withhold && blockIdx.x == 0))
-            hx_put(a.xh + ((s + 1) & 1) * bufw + (size_t)(g * RG + r) * DG + unit / 2,
+            hx_put(a.xh + ((s + 1) & 1) * bufw + (size_t)((g * MT + m) * RG + r) * DG + unit / 2,
                    (uint32_t)(s + 2), mine | (nb << 16), local);
     };
-    publish(-1, hprev);
+#pragma unroll
+    for (int m = 0; m < MT; ++m) publish(-1, m, hprev[m]);
     const int lrow = lane & 15;
-    // input projections are loaded one step ahead: issued at the end of step t-1, they land
-    // during step t's hand-off wait instead of stalling its epilogue
-    const float* gp0 = a.gi + (int64_t)b * a.ldgi;
-    // input projections: step t + 1's are issued as soon as step t's hand-off has landed
-    // (vmcnt is in order: issued after the publish they made the next hand-off check wait for
-    // their latency too), into the other of two register sets used alternately (loop unrolled
-    // by two: a copy into the current set would wait for the loads at once)
+    // input projections: the next (step, tile)'s are issued as soon as this one's hand-off
+    // has landed (vmcnt is in order: issued after the publish they made the next hand-off
+    // check wait for their latency too), into the other of two register sets used
+    // alternately (the (step, tile) sequence unrolled by two: a copy into the current set
+    // would wait for the loads at once)
     struct Gi { float r, z, n; };
-    Gi ga{gp0[unit], gp0[D + unit], gp0[2 * D + unit]}, gb{0.f, 0.f, 0.f};
-    auto fetch_gi = [&](int t, Gi& nx) {
-        const float* gp = a.gi + (int64_t)b * a.ldgi + (int64_t)min(t + 1, a.Fr - 1) * a.sgi;
+    Gi ga, gb{0.f, 0.f, 0.f};
+    {
+        const float* gp0 = a.gi + (int64_t)min(row_of(0), B - 1) * a.ldgi;
+        ga = Gi{gp0[unit], gp0[D + unit], gp0[2 * D + unit]};
+    }
+    auto fetch_gi = [&](int t, int m, Gi& nx) {     // operands of the (step, tile) after (t, m)
+        int tn = t, mn = m + 1;
+        if (mn == MT) { mn = 0; tn = min(t + 1, a.Fr - 1); }
+        const float* gp = a.gi + (int64_t)min(row_of(mn), B - 1) * a.ldgi + (int64_t)tn * a.sgi;
         nx.r = gp[unit]; nx.z = gp[D + unit]; nx.n = gp[2 * D + unit];
     };
-    auto step = [&](int t, const Gi& cu, Gi& nx) {
+    auto step = [&](int t, int m, const Gi& cu, Gi& nx) {
             floatx4 acc[NT];
     #pragma unroll
             for (int i = 0; i < NT; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -147,11 +166,11 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
             //  wait analysis sees the poll's vmcnt(0) on every path and the step's operands
             //  from the previous step need no further wait)
             const bool polls = UPW >= 2 || wave < KW;
-            if (!polls) fetch_gi(t, nx);
+            if (!polls) fetch_gi(t, m, nx);
             if (polls) {
                 const uint32_t tag = (uint32_t)(t + 1);
                 const uint32_t base = (uint32_t)(((size_t)(t & 1) * bufw +
-                                                  (size_t)(g * RG + lrow) * DG) * 8);
+                                                  (size_t)((g * MT + m) * RG + lrow) * DG) * 8);
                 uint32_t w[UPW][4];
                 int spins = 0;
                 for (;;) {
@@ -171,13 +190,13 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
                         const bool v = wave + NW * j < NU;
                         w[j][0] = v ? x[j][0].x : 0u; w[j][1] = v ? x[j][0].z : 0u;
                         w[j][2] = v ? x[j][1].x : 0u; w[j][3] = v ? x[j][1].z : 0u;
-                        ok &= !v || ((x[j][0].y == tag) & (x[j][0].w == tag) & (x[j][1].y == tag) &
-                                     (x[j][1].w == tag));
+                        ok &= !v || ((x[j][0].y == tag) & (x[j][0].w == tag) &
+                                     (x[j][1].y == tag) & (x[j][1].w == tag));
                     }
                     if (__all(ok)) break;
                     if (hx_spin_fail(spins, a.err, lane, a.poll_sleep, a.spin_limit)) break;
                 }
-                fetch_gi(t, nx);
+                fetch_gi(t, m, nx);
                 GX_STAMP();
     #pragma unroll
                 for (int j = 0; j < UPW; ++j) {
@@ -213,24 +232,33 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
             const float rr = 1.0f / (1.0f + expf(-(ghr + cu.r)));
             const float zz = 1.0f / (1.0f + expf(-(ghz + cu.z)));
             const float nn = tanhf(cu.n + ghn * rr);
-            const float hn = (hprev - nn) * zz + nn;
-            hprev = hn;
-            publish(t, hn);
+            const float hn = (hprev[m] - nn) * zz + nn;
+            hprev[m] = hn;
+            publish(t, m, hn);
             GX_STAMP();
-            if (wr) {
-                const int64_t o = (int64_t)b * a.ldo + (int64_t)t * a.so + unit;
+            const int row = row_of(m);
+            if (rv && row < B) {
+                const int64_t o = (int64_t)row * a.ldo + (int64_t)t * a.so + unit;
                 a.out[o] = hn;
                 a.out_lp[o] = __float2bfloat16(hn);
                 if (a.hp_lp && t + 1 < a.Fr) a.hp_lp[o + a.so] = __float2bfloat16(hn);
-                float* gt = a.gates + (int64_t)b * a.ldg + (int64_t)t * a.sg;
+                float* gt = a.gates + (int64_t)row * a.ldg + (int64_t)t * a.sg;
                 gt[unit] = rr; gt[D + unit] = zz; gt[2 * D + unit] = nn; gt[3 * D + unit] = ghn;
             }
-            __syncthreads();                       // red is rewritten next step
+            __syncthreads();                       // red is rewritten next (step, tile)
             GX_STAMP();
     };
-    for (int t = 0; t < a.Fr; t += 2) {
-        step(t, ga, gb);
-        if (t + 1 < a.Fr) step(t + 1, gb, ga);
+    // (step, tile) sequence, unrolled by two for the alternating operand sets (MT = 1: two
+    // steps per trip; MT even: the tiles of one step)
+    constexpr int TU = MT == 1 ? 2 : 1;
+    for (int t0 = 0; t0 < a.Fr; t0 += TU) {
+#pragma unroll
+        for (int q = 0; q < TU * MT; ++q) {
+            const int t = t0 + q / MT, m = q % MT;
+            if (t >= a.Fr) break;
+            if (q & 1) step(t, m, gb, ga);
+            else step(t, m, ga, gb);
+        }
     }
 #undef GX_STAMP
     gx_note_failure(a.err, a.sticky);
@@ -239,9 +267,9 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
 // ------------------------------------------------------------------ backward
 // Reverse sweep of one layer (gru_seq.hip's backward, same pointwise code, gru_point.hpp):
 //   dh_t = dy_t + ddir_{t+1} + dgh_{t+1} . W_hh,  then the gate backward.
-// Same groups as the forward; each wave keeps its K-slice (3D / 8 = 384 k) of the
-// workgroup's 32 W_hh^T rows as B fragments (96 VGPRs at D = 1024); per step the group's
-// dgh_{t+1} (16 rows x 3D bf16) arrives as granules (double-buffered, tag = Fr - step).
+// Same groups and tiles as the forward; each wave keeps its K-slice (3D / 8 = 384 k) of the
+// workgroup's 32 W_hh^T rows as B fragments (96 VGPRs at D = 1024); per step and tile the
+// tile's dgh_{t+1} (16 rows x 3D bf16) arrives as granules (double-buffered, tag = Fr - step).
 struct GruXBwdArgs {
     const float* dy; int64_t lddy; int64_t sdy;
     const float* gates; int64_t ldg; int64_t sg;
@@ -253,21 +281,21 @@ struct GruXBwdArgs {
     float* bsum;                                    // optional (B, 4D): per-row sums over t of
                                                     // [dar | daz | dghn | dan] (bias grads)
     float* ddir0;                                   // (B, D)
-    u64* xg;                                        // 2 x G x RG x 3D/2 granules
+    u64* xg;                                        // 2 x G x MT x RG x 3D/2 granules
     int* census;
     int* err;
     int* sticky;
     int spin_limit;
     int withhold;
-    int B, D, Fr, G, P;
+    int B, D, Fr, G, P, RV;
 };
 
-template <int UPW, bool FULL>     // FULL: NU == UPW * NW (every unit of every wave in range)
+template <int UPW, bool FULL, int MT>   // FULL: NU == UPW * NW (every unit of every wave in range)
 __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a) {
     using namespace gx;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int D = a.D, B = a.B, K3 = 3 * D;
+    const int D = a.D, B = a.B, K3 = 3 * D, RV = a.RV;
     const int NU = K3 / UK, KW = NW < NU ? NW : NU;
     constexpr int NTB = 2;                                      // 32 units = 2 n tiles
     floatx4* red = (floatx4*)smem;                              // [KW][2][64]
@@ -308,15 +336,16 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
     __syncthreads();
     const bool local = gsh[2] != 0;
     const int r = tid >> 5, uu = tid & 31;
-    const int b = min(g * RG + r, B - 1);
-    const bool wr = g * RG + r < B;
+    const bool rv = r < RV;
     const int unit = u0 + uu;
+    auto row_of = [&](int m) { return (g * MT + m) * RV + r; };
     const __amdgpu_buffer_rsrc_t rx = hx_rsrc(a.xg);
-    const size_t bufw = (size_t)a.G * RG * KG;
+    const size_t bufw = (size_t)a.G * MT * RG * KG;
     const int lrow = lane & 15;
-    float ddir = 0.f;
-    // this step's operands, loaded one step ahead (see the forward)
-    auto fetch = [&](int t, float& dyv, float& gr, float& gz, float& gn, float& gg, float& hp) {
+    // this (step, tile)'s operands, loaded one (step, tile) ahead (see the forward)
+    auto fetch = [&](int t, int m, float& dyv, float& gr, float& gz, float& gn, float& gg,
+                     float& hp) {
+        const int b = min(row_of(m), B - 1);
         dyv = a.dy[(int64_t)b * a.lddy + (int64_t)t * a.sdy + unit];
         const float* gp = a.gates + (int64_t)b * a.ldg + (int64_t)t * a.sg;
         gr = gp[unit]; gz = gp[D + unit]; gn = gp[2 * D + unit]; gg = gp[3 * D + unit];
@@ -324,10 +353,20 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
                    : a.h0[(int64_t)b * D + unit];
     };
     float dyv, gr, gz, gn, gg, hp;
-    float sar = 0.f, saz = 0.f, sghn = 0.f, san = 0.f;   // bias-gradient row sums (over t)
-    fetch(a.Fr - 1, dyv, gr, gz, gn, gg, hp);
+    // per-tile state (the carried dh_direct and the bias-gradient row sums over t): registers
+    // at MT = 1, per-thread LDS slots above (the register file is full at D = 1024: W_hh^T
+    // slice + poll buffer; the tile loop is not unrolled, so its index is not a constant)
+    float ddir1 = 0.f, sar1 = 0.f, saz1 = 0.f, sghn1 = 0.f, san1 = 0.f;
+    float* sl = (float*)(smem + (size_t)KW * NTB * 64 * sizeof(floatx4) + 64);   // [MT][5][NTHR]
+    if (MT > 1)
+        for (int k = 0; k < 5 * MT; ++k) sl[k * NTHR + tid] = 0.f;
+    fetch(a.Fr - 1, 0, dyv, gr, gz, gn, gg, hp);
     for (int t = a.Fr - 1; t >= 0; --t) {
+#pragma unroll 1
+    for (int m = 0; m < MT; ++m) {
         const bool has_next = t + 1 < a.Fr;
+        float* q = sl + (m * 5) * NTHR + tid;             // (MT > 1) this tile's state slots
+        const float ddir_in = MT == 1 ? ddir1 : q[0];
         floatx4 acc[NTB];
 #pragma unroll
         for (int i = 0; i < NTB; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -335,7 +374,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
             if (UPW >= 2 || wave < KW) {                        // (as the forward)
                 const uint32_t tag = (uint32_t)(a.Fr - 1 - t);     // dgh_{t+1}
                 const uint32_t base = (uint32_t)((((size_t)((t + 1) & 1)) * bufw +
-                                                  (size_t)(g * RG + lrow) * KG) * 8);
+                                                  (size_t)((g * MT + m) * RG + lrow) * KG) * 8);
                 uint4 x[UPW][2];
                 int spins = 0;
                 // unit j's granules sit at lane offset + j * NW units (every unit of the wave
@@ -388,13 +427,14 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
             for (int kw = 0; kw < NW; ++kw) s += kw < KW ? pr[kw] : 0.f;
         }
         float dh = s + dyv;
-        if (has_next) dh += ddir;
+        if (has_next) dh += ddir_in;
         const GruBwdPoint o = gru_bwd_point(dh, gr, gz, gn, gg, hp);
-        ddir = o.ddir;
+        if (MT == 1) ddir1 = o.ddir;
+        else q[0] = o.ddir;
         // publish dgh_t = [dar | daz | dghn] (bf16 granules, pairs of units), tag Fr - t
         {
             const float vals[3] = {o.dar, o.daz, o.dghn};
-            u64* dst = a.xg + (size_t)(t & 1) * bufw + (size_t)(g * RG + r) * KG;
+            u64* dst = a.xg + (size_t)(t & 1) * bufw + (size_t)((g * MT + m) * RG + r) * KG;
 #pragma unroll
             for (int gt = 0; gt < 3; ++gt) {
                 const uint32_t mine = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(vals[gt]));
@@ -404,9 +444,11 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
             }
         }
         const float cdar = o.dar, cdaz = o.daz, cdghn = o.dghn, cdan = o.dan;
-        if (t > 0) fetch(t - 1, dyv, gr, gz, gn, gg, hp);
-        if (wr) {
-            const int64_t ob = (int64_t)b * a.ldd + (int64_t)t * a.sd;
+        if (m + 1 < MT) fetch(t, m + 1, dyv, gr, gz, gn, gg, hp);
+        else if (t > 0) fetch(t - 1, 0, dyv, gr, gz, gn, gg, hp);
+        const int row = row_of(m);
+        if (rv && row < B) {
+            const int64_t ob = (int64_t)row * a.ldd + (int64_t)t * a.sd;
             if (a.dgh) {
                 float* dg = a.dgh + ob;
                 dg[unit] = cdar; dg[D + unit] = cdaz; dg[2 * D + unit] = cdghn;
@@ -422,14 +464,30 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
                 bf16* dj = a.dgi_lp + ob;
                 dj[unit] = har; dj[D + unit] = haz; dj[2 * D + unit] = __float2bfloat16(cdan);
             }
-            sar += cdar; saz += cdaz; sghn += cdghn; san += cdan;
-            if (t == 0) a.ddir0[(int64_t)b * D + unit] = ddir;
+            if (MT == 1) {
+                sar1 += cdar; saz1 += cdaz; sghn1 += cdghn; san1 += cdan;
+            } else {
+                q[NTHR] += cdar; q[2 * NTHR] += cdaz; q[3 * NTHR] += cdghn; q[4 * NTHR] += cdan;
+            }
+            if (t == 0) a.ddir0[(int64_t)row * D + unit] = o.ddir;
         }
         __syncthreads();
     }
-    if (a.bsum && wr) {
-        float* bs = a.bsum + (int64_t)b * 4 * D;
-        bs[unit] = sar; bs[D + unit] = saz; bs[2 * D + unit] = sghn; bs[3 * D + unit] = san;
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int row = row_of(m);
+        if (a.bsum && rv && row < B) {
+            float* bs = a.bsum + (int64_t)row * 4 * D;
+            if (MT == 1) {
+                bs[unit] = sar1; bs[D + unit] = saz1; bs[2 * D + unit] = sghn1;
+                bs[3 * D + unit] = san1;
+            } else {
+                const float* q = sl + (m * 5) * NTHR + tid;
+                bs[unit] = q[NTHR]; bs[D + unit] = q[2 * NTHR]; bs[2 * D + unit] = q[3 * NTHR];
+                bs[3 * D + unit] = q[4 * NTHR];
+            }
+        }
     }
     gx_note_failure(a.err, a.sticky);
 }
@@ -465,13 +523,41 @@ static int gx_cus() {
     return g_gx_ncu;
 }
 
+// Row layout of one launch for B rows at width D (GruXArgs): false if the device or shape
+// is not supported.  B beyond what one launch holds (16 MAXMT rows per group) is run as
+// several launches of gx_launch_rows(D) rows each (srnn_gru_xcd_fwd2 / bwd2).
+struct GxLayout { int mt, G, rv, P; };
+
+static int gx_launch_rows(int D) {
+    const int ncu = gx_cus();
+    if (ncu <= 0 || D % 256 != 0 || D > 1024) return 0;
+    return (ncu / (D / gx::CU)) * gx::RG * gx::MAXMT;
+}
+
+static bool gx_layout(int B, int D, GxLayout& L) {
+    const int ncu = gx_cus();
+    if (ncu <= 0 || B <= 0 || D % 256 != 0 || D > 1024) return false;
+    L.P = D / gx::CU;
+    const int gmax = ncu / L.P;
+    if (gmax < 1) return false;
+    L.mt = 1;
+    while (L.mt < gx::MAXMT && cdiv(B, gx::RG * L.mt) > gmax) L.mt *= 2;
+    int G = cdiv(B, gx::RG * L.mt);
+    if (G > gmax) return false;
+    // whole groups of 8: with the round-robin dealing every group then sits on one XCD, and a
+    // small batch spreads over all of them (fewer rows per group, e.g. 8 at B = 64)
+    L.G = (G + 7) / 8 * 8 <= gmax ? (G + 7) / 8 * 8 : G;
+    L.rv = cdiv(B, L.G * L.mt);
+    return L.rv <= gx::RG;
+}
+
 // work-buffer bytes of srnn_gru_xcd_fwd for (B, D); 0 if the shape / device is not supported
 extern "C" size_t srnn_gru_xcd_work_bytes(int dtype, int B, int D) {
-    if (dtype != SRNN_BF16 || D % 256 != 0 || D > 1024 || B <= 0) return 0;
-    const int G = cdiv(B, gx::RG), P = D / gx::CU;
-    const int ncu = gx_cus();
-    if (ncu <= 0 || G * P > ncu) return 0;
-    return gx::HDR + (size_t)2 * G * gx::RG * (D / 2) * 8;
+    if (dtype != SRNN_BF16 || B <= 0) return 0;
+    const int lr = gx_launch_rows(D);
+    GxLayout L;
+    if (lr <= 0 || !gx_layout(B < lr ? B : lr, D, L)) return 0;
+    return gx::HDR + (size_t)2 * L.G * L.mt * gx::RG * (D / 2) * 8;
 }
 
 extern "C" int srnn_gru_xcd_fwd2(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
@@ -483,6 +569,22 @@ extern "C" int srnn_gru_xcd_fwd2(int dtype, int B, int D, int Fr, const float* g
     SRNN_REQUIRE(need > 0, "gru_xcd: shape/device not supported");
     SRNN_REQUIRE(work && work_bytes >= need, "gru_xcd: workspace %zu < %zu", work_bytes, need);
     if (Fr <= 0) return 0;
+    const int lr = gx_launch_rows(D);
+    if (B > lr) {     // rows are independent: consecutive launches over row chunks
+        for (int c = 0; c < B; c += lr) {
+            const int n = B - c < lr ? B - c : lr;
+            const int rc = srnn_gru_xcd_fwd2(
+                dtype, n, D, Fr, gi + (int64_t)c * ldgi, ldgi, sgi, h0 + (int64_t)c * D, whh,
+                bhh, out + (int64_t)c * ldo, (bf16*)out_lp + (int64_t)c * ldo, ldo, so,
+                gates + (int64_t)c * ldg, ldg, sg,
+                hprev_lp ? (void*)((bf16*)hprev_lp + (int64_t)c * ldo) : nullptr, work,
+                work_bytes, stream);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    GxLayout L;
+    SRNN_REQUIRE(gx_layout(B, D, L), "gru_xcd: no row layout for B=%d D=%d", B, D);
     hipStream_t s = (hipStream_t)stream;
     // granules, census and error word start zeroed every call (tags count from 1)
     SRNN_CHECK_HIP(hipMemsetAsync(work, 0, need, s));
@@ -513,20 +615,26 @@ extern "C" int srnn_gru_xcd_fwd2(int dtype, int B, int D, int Fr, const float* g
             gx_diag_buf() = diag;
         }
     }
-    a.G = cdiv(B, gx::RG);
-    a.P = D / gx::CU;
+    a.G = L.G;
+    a.P = L.P;
+    a.RV = L.rv;
     const int NU = D / gx::UK;
     const int KW = NU < gx::NW ? NU : gx::NW;
     const size_t lds = (size_t)KW * gx::NT * 64 * 16 + 16;
     const int upw = cdiv(NU, gx::NW);
-    void (*k)(GruXArgs) = upw <= 1 ? gru_xcd_fwd_kernel<1>
-                          : upw <= 2 ? gru_xcd_fwd_kernel<2> : gru_xcd_fwd_kernel<4>;
-    static bool attr[3] = {false, false, false};
-    const int ai = upw <= 1 ? 0 : upw <= 2 ? 1 : 2;
-    if (!attr[ai]) {
+    const int ui = upw <= 1 ? 0 : upw <= 2 ? 1 : 2;
+    const int mi = L.mt == 1 ? 0 : L.mt == 2 ? 1 : 2;
+    typedef void (*FwdK)(GruXArgs);
+    static const FwdK ks[3][3] = {
+        {gru_xcd_fwd_kernel<1, 1>, gru_xcd_fwd_kernel<1, 2>, gru_xcd_fwd_kernel<1, 4>},
+        {gru_xcd_fwd_kernel<2, 1>, gru_xcd_fwd_kernel<2, 2>, gru_xcd_fwd_kernel<2, 4>},
+        {gru_xcd_fwd_kernel<4, 1>, gru_xcd_fwd_kernel<4, 2>, gru_xcd_fwd_kernel<4, 4>}};
+    const FwdK k = ks[ui][mi];
+    static bool attr[3][3] = {};
+    if (!attr[ui][mi]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
-        attr[ai] = true;
+        attr[ui][mi] = true;
     }
     hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
     SRNN_LAUNCH_CHECK();
@@ -546,8 +654,10 @@ extern "C" int srnn_gru_xcd_fwd(int dtype, int B, int D, int Fr, const float* gi
 // work-buffer bytes of srnn_gru_xcd_bwd for (B, D); 0 if not supported
 extern "C" size_t srnn_gru_xcd_bwd_work_bytes(int dtype, int B, int D) {
     if (!srnn_gru_xcd_work_bytes(dtype, B, D)) return 0;
-    const int G = cdiv(B, gx::RG);
-    return gx::HDR + (size_t)2 * G * gx::RG * (3 * D / 2) * 8;
+    const int lr = gx_launch_rows(D);
+    GxLayout L;
+    if (!gx_layout(B < lr ? B : lr, D, L)) return 0;
+    return gx::HDR + (size_t)2 * L.G * L.mt * gx::RG * (3 * D / 2) * 8;
 }
 
 extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* dy, int64_t lddy,
@@ -559,7 +669,26 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
     const size_t need = srnn_gru_xcd_bwd_work_bytes(dtype, B, D);
     SRNN_REQUIRE(need > 0, "gru_xcd_bwd: shape/device not supported");
     SRNN_REQUIRE(work && work_bytes >= need, "gru_xcd_bwd: workspace %zu < %zu", work_bytes, need);
+    SRNN_REQUIRE(dgh_lp, "gru_xcd_bwd: dgh_lp is required");
     if (Fr <= 0) return 0;
+    const int lr = gx_launch_rows(D);
+    if (B > lr) {     // rows are independent: consecutive launches over row chunks
+        for (int c = 0; c < B; c += lr) {
+            const int n = B - c < lr ? B - c : lr;
+            const int rc = srnn_gru_xcd_bwd2(
+                dtype, n, D, Fr, dy + (int64_t)c * lddy, lddy, sdy, gates + (int64_t)c * ldg,
+                ldg, sg, hout + (int64_t)c * ldo, ldo, so, h0 + (int64_t)c * D, whh_t,
+                dgh ? dgh + (int64_t)c * ldd : nullptr, (bf16*)dgh_lp + (int64_t)c * ldd,
+                dgi ? dgi + (int64_t)c * ldd : nullptr,
+                dgi_lp ? (void*)((bf16*)dgi_lp + (int64_t)c * ldd) : nullptr,
+                bsum ? bsum + (int64_t)c * 4 * D : nullptr, ldd, sd, ddir0 + (int64_t)c * D,
+                work, work_bytes, stream);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    GxLayout L;
+    SRNN_REQUIRE(gx_layout(B, D, L), "gru_xcd_bwd: no row layout for B=%d D=%d", B, D);
     hipStream_t s = (hipStream_t)stream;
     SRNN_CHECK_HIP(hipMemsetAsync(work, 0, need, s));
     GruXBwdArgs a;
@@ -567,7 +696,6 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
     a.gates = gates; a.ldg = ldg; a.sg = sg;
     a.hout = hout; a.ldo = ldo; a.so = so; a.h0 = h0;
     a.whh_t = (const bf16*)whh_t;
-    SRNN_REQUIRE(dgh_lp, "gru_xcd_bwd: dgh_lp is required");
     a.dgh = dgh; a.dgh_lp = (bf16*)dgh_lp; a.dgi = dgi; a.ldd = ldd; a.sd = sd;
     a.dgi_lp = (bf16*)dgi_lp; a.bsum = bsum;
     a.ddir0 = ddir0;
@@ -579,16 +707,32 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
     a.census = env_flag("SRNN_GEN_LOCAL", 1) ? (int*)work + 16 : nullptr;
     a.xg = (u64*)((char*)work + gx::HDR);
     a.B = B; a.D = D; a.Fr = Fr;
-    a.G = cdiv(B, gx::RG);
-    a.P = D / gx::CU;
+    a.G = L.G;
+    a.P = L.P;
+    a.RV = L.rv;
     const int NU = 3 * D / gx::UK;
     const int KW = NU < gx::NW ? NU : gx::NW;
-    const size_t lds = (size_t)KW * 2 * 64 * 16 + 16;
+    const size_t lds = (size_t)KW * 2 * 64 * 16 + 64 +
+                       (L.mt > 1 ? (size_t)L.mt * 5 * gx::NTHR * 4 : 0);
     const int upw = cdiv(NU, gx::NW);
-    void (*k)(GruXBwdArgs) =
-        upw <= 3 ? (NU == 3 * gx::NW ? gru_xcd_bwd_kernel<3, true> : gru_xcd_bwd_kernel<3, false>)
-        : upw <= 6 ? (NU == 6 * gx::NW ? gru_xcd_bwd_kernel<6, true> : gru_xcd_bwd_kernel<6, false>)
-        : (NU == 12 * gx::NW ? gru_xcd_bwd_kernel<12, true> : gru_xcd_bwd_kernel<12, false>);
+    const int ui = upw <= 3 ? 0 : upw <= 6 ? 1 : 2;
+    const bool full = NU == (ui == 0 ? 3 : ui == 1 ? 6 : 12) * gx::NW;
+    const int mi = L.mt == 1 ? 0 : L.mt == 2 ? 1 : 2;
+    typedef void (*BwdK)(GruXBwdArgs);
+    // FULL holds for D = 256 / 512 / 1024 (UPW = 3 / 6 / 12); D = 768 takes the UPW = 12 form
+    static const BwdK ks[2][3][3] = {
+        {{nullptr, nullptr, nullptr},
+         {nullptr, nullptr, nullptr},
+         {gru_xcd_bwd_kernel<12, false, 1>, gru_xcd_bwd_kernel<12, false, 2>,
+          gru_xcd_bwd_kernel<12, false, 4>}},
+        {{gru_xcd_bwd_kernel<3, true, 1>, gru_xcd_bwd_kernel<3, true, 2>,
+          gru_xcd_bwd_kernel<3, true, 4>},
+         {gru_xcd_bwd_kernel<6, true, 1>, gru_xcd_bwd_kernel<6, true, 2>,
+          gru_xcd_bwd_kernel<6, true, 4>},
+         {gru_xcd_bwd_kernel<12, true, 1>, gru_xcd_bwd_kernel<12, true, 2>,
+          gru_xcd_bwd_kernel<12, true, 4>}}};
+    const BwdK k = ks[full ? 1 : 0][ui][mi];
+    SRNN_REQUIRE(k, "gru_xcd_bwd: no kernel for D=%d", D);
     hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;

@@ -29,7 +29,9 @@ import utils
 import samplernn_hip as H
 
 verbose = False
-_STATS = {'fused_colsum': 0, 'fused_lp': 0}     # (tests) how often a fused side result was consumed
+# (tests) how often a fused side result was consumed, and which recurrence kernels ran
+_STATS = {'fused_colsum': 0, 'fused_lp': 0, 'gru_xcd_fwd': 0, 'gru_xcd_bwd': 0, 'gru_seq': 0,
+          'gru_cell_steps': 0, 'gru_cell_bwd_steps': 0}
 
 
 def _default_dtype():
@@ -283,6 +285,7 @@ class _TierFn(torch.autograd.Function):
                 # the backward's W_hh gradient
                 work = torch.empty(xw, device=dev, dtype=torch.uint8)
                 hprevT = torch.empty((B, Fr, D), device=dev, dtype=T)
+                _STATS['gru_xcd_fwd'] += 1
                 H.lib().call('srnn_gru_xcd_fwd2', H.dcode(T), B, D, Fr, H.ptr(gi), Fr * 3 * D,
                              3 * D, H.ptr(hpf), H.ptr(Whh[l]), H.ptr(b_hh), H.ptr(out),
                              H.ptr(outT), Fr * D, D, H.ptr(gt), Fr * 4 * D, 4 * D,
@@ -290,10 +293,12 @@ class _TierFn(torch.autograd.Function):
             elif seq:
                 # whole sequence in one persistent launch (W_hh resident in LDS)
                 work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
+                _STATS['gru_seq'] += 1
                 H.lib().call('srnn_gru_seq_fwd', H.dcode(T), B, D, Fr, H.ptr(gi), Fr * 3 * D,
                              3 * D, H.ptr(hpf), H.ptr(hpT), H.ptr(Whh[l]), H.ptr(b_hh),
                              H.ptr(out), H.ptr(outT), Fr * D, D, H.ptr(gt), Fr * 4 * D, 4 * D,
                              H.ptr(work), work.numel() * 4, H.stream())
+            _STATS['gru_cell_steps'] += 0 if seq else Fr
             for t in range(0 if not seq else Fr, Fr):
                 if t == 0:
                     hp_t, hp_f, ldh = hpT, hpf, D
@@ -402,6 +407,7 @@ class _TierFn(torch.autograd.Function):
                 # reverse sweep in one persistent launch, row groups per XCD, W_hh^T in VGPRs
                 work = torch.empty(xbw, device=dev, dtype=torch.uint8)
                 dOutc = dOut.contiguous()
+                _STATS['gru_xcd_bwd'] += 1
                 H.lib().call('srnn_gru_xcd_bwd2', H.dcode(T), B, D, Fr, H.ptr(dOutc), Fr * D, D,
                              H.ptr(gates[l]), Fr * 4 * D, 4 * D, H.ptr(outs[l]), Fr * D, D,
                              H.ptr(h_in[l]), H.ptr(WhhT), None, H.ptr(dGHT), None, H.ptr(dGIT),
@@ -416,6 +422,7 @@ class _TierFn(torch.autograd.Function):
                              H.ptr(h_in[l]), H.ptr(WhhT), H.ptr(dGH), H.ptr(dGHT), H.ptr(dGI),
                              Fr * 3 * D, 3 * D, H.ptr(ddir[0]), H.ptr(work), work.numel() * 4,
                              st())
+            _STATS['gru_cell_bwd_steps'] += 0 if seq else Fr
             for t in reversed(range(Fr)) if not seq else ():
                 nxt = t + 1 < Fr
                 if t > 0:

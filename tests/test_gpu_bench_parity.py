@@ -50,12 +50,22 @@ def _run(dtype, batches):
     return losses, grads
 
 
-def test_bench_bf16_step_matches_fp32(hip):
+@pytest.mark.parametrize('B', [128, 64, 512])
+def test_bench_bf16_step_matches_fp32(hip, B):
+    """B = 128: configs[1]; 512: configs[3]'s global batch on one GPU (the strong-scaling
+    N = 1 point, 4 row tiles per sweep group); 64: its per-GPU share at 8 GPUs."""
     import bench
-    B, T, L = 128, 1024, 64
+    import model as M
+    T, L = 1024, 64
     batches = bench.gpu_batches(bench.synth_batches(B, T, L, 3, 0), DEV)
     l32, g32 = _run(torch.float32, batches)
+    before = dict(M._STATS)
     l16, g16 = _run(torch.bfloat16, batches)
+    # the bf16 step ran the persistent XCD sweeps, never the per-step recurrence kernels
+    assert M._STATS['gru_xcd_fwd'] > before['gru_xcd_fwd']
+    assert M._STATS['gru_xcd_bwd'] > before['gru_xcd_bwd']
+    assert M._STATS['gru_cell_steps'] == before['gru_cell_steps']
+    assert M._STATS['gru_cell_bwd_steps'] == before['gru_cell_bwd_steps']
     print('losses fp32', l32, 'bf16', l16)
     np.testing.assert_allclose(l16, l32, rtol=3e-4, atol=0)
     assert g16.keys() == g32.keys()

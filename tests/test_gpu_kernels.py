@@ -182,7 +182,14 @@ def _gru_ref(gi, h0, whh, bhh, Fr):
     return torch.stack(out, 1), torch.stack(gates, 1)
 
 
-@pytest.mark.parametrize('B,D,Fr', [(128, 1024, 64), (64, 1024, 5), (100, 256, 9), (16, 512, 3)])
+# row layouts (gru_xcd.hip gx_layout): B = 128 one 16-row tile per group; B <= 64 fewer valid
+# rows per tile on all 8 XCDs; 256 / 300 / 512 several tiles per group (configs[3]'s 512 rows on
+# one GPU, 256 on two); 600 two launches (512 + 88 rows); D = 512 / 256 other group widths
+XCD_SHAPES = [(128, 1024, 64), (64, 1024, 5), (100, 256, 9), (16, 512, 3), (512, 1024, 16),
+              (256, 1024, 9), (300, 1024, 5), (600, 1024, 4), (64, 1024, 64), (512, 512, 7)]
+
+
+@pytest.mark.parametrize('B,D,Fr', XCD_SHAPES)
 def test_gru_xcd_fwd(hip, B, D, Fr):
     """XCD-grouped persistent GRU forward (gru_xcd.hip) vs the torch recurrence; same outputs
     as the gru_seq kernel within MFMA summation-order noise."""
@@ -225,7 +232,7 @@ def test_gru_xcd_fwd(hip, B, D, Fr):
     assert torch.equal(hp[:, 1:], outT[:, :-1])
 
 
-@pytest.mark.parametrize('B,D,Fr', [(128, 1024, 64), (64, 1024, 5), (100, 256, 9), (16, 512, 3)])
+@pytest.mark.parametrize('B,D,Fr', XCD_SHAPES)
 def test_gru_xcd_bwd(hip, B, D, Fr):
     """XCD-grouped persistent GRU backward vs torch autograd of the same recurrence (bf16
     W_hh and bf16 dgh operands on the MFMA path: tolerance, not bits)."""
@@ -277,6 +284,78 @@ def test_gru_xcd_bwd(hip, B, D, Fr):
     dh0 = dgh[:, 0].cpu() @ whh.float() + ddir0.cpu()
     torch.testing.assert_close(dh0, h0_r.grad, atol=2e-2 * h0_r.grad.abs().max().item(), rtol=0)
     torch.testing.assert_close(dgh_lp.float().cpu(), dgh.cpu().to(T).float(), atol=0, rtol=0)
+    # srnn_gru_xcd_bwd2 (the training path): the same dgh / dgi in bf16 bit for bit, and the
+    # per-row bias-gradient sums over t of [dar | daz | dghn | dan]
+    dgh2 = torch.zeros((B, Fr, 3 * D), device=DEV, dtype=T)
+    dgi2 = torch.zeros((B, Fr, 3 * D), device=DEV, dtype=T)
+    bsum = torch.full((B, 4 * D), float('nan'), device=DEV)
+    ddir2 = torch.full((B, D), float('nan'), device=DEV)
+    work.fill_(7)
+    hip.lib().call('srnn_gru_xcd_bwd2', hip.BF16, B, D, Fr, hip.ptr(dyd), Fr * D, D, hip.ptr(gtd),
+                   Fr * 4 * D, 4 * D, hip.ptr(outd), Fr * D, D, hip.ptr(h0d), hip.ptr(whh_t),
+                   None, hip.ptr(dgh2), None, hip.ptr(dgi2), hip.ptr(bsum), Fr * 3 * D, 3 * D,
+                   hip.ptr(ddir2), hip.ptr(work), nb, hip.stream())
+    torch.cuda.synchronize()
+    assert hip.lib().dll.srnn_gru_xcd_error(hip.ptr(work)) == 0, 'gru_xcd_bwd2 gave up waiting'
+    assert torch.equal(dgh2, dgh_lp) and torch.equal(ddir2, ddir0)
+    assert torch.equal(dgi2, dgi.to(T))
+    ref_bs = torch.cat([dgh.sum(1), dgi[:, :, 2 * D:].sum(1)], 1)
+    torch.testing.assert_close(bsum, ref_bs, atol=1e-5 * ref_bs.abs().max().item(), rtol=1e-5)
+
+
+@pytest.mark.parametrize('D', [1024, 512])
+def test_gru_xcd_layouts_bit_identical(hip, D):
+    """Rows are independent and every row's arithmetic is the same in every row layout, so a
+    512-row sweep (4 tiles per group), a 64-row one (8 valid rows per tile), 600 rows (two
+    launches) and the 128-row launches of the same rows give identical bits, forward and
+    backward (a size-independent check of the B > 128 layouts against the B = 128 one)."""
+    T = torch.bfloat16
+    Fr = 6
+    g = torch.Generator().manual_seed(D + 5)
+    Bt = 600
+    whh = (torch.randn(3 * D, D, generator=g) * 0.03).to(DEV, T)
+    whh_t = whh.float().t().contiguous().to(T)
+    bhh = (torch.randn(3 * D, generator=g) * 0.1).to(DEV)
+    gi = (torch.randn(Bt, Fr, 3 * D, generator=g) * 0.5).to(DEV)
+    h0 = (torch.randn(Bt, D, generator=g) * 0.5).to(DEV)
+    dy = (torch.randn(Bt, Fr, D, generator=g) * 0.1).to(DEV)
+
+    def run(r0, n):
+        nf = hip.gru_xcd_work_bytes(T, n, D)
+        nb = hip.gru_xcd_bwd_work_bytes(T, n, D)
+        assert nf and nb
+        wf = torch.empty(nf, device=DEV, dtype=torch.uint8)
+        wb = torch.empty(nb, device=DEV, dtype=torch.uint8)
+        out = torch.empty((n, Fr, D), device=DEV)
+        outT = torch.empty((n, Fr, D), device=DEV, dtype=T)
+        gt = torch.empty((n, Fr, 4 * D), device=DEV)
+        hp = torch.empty((n, Fr, D), device=DEV, dtype=T)
+        gi_ = gi[r0:r0 + n].contiguous()
+        h0_ = h0[r0:r0 + n].contiguous()
+        hip.lib().call('srnn_gru_xcd_fwd2', hip.BF16, n, D, Fr, hip.ptr(gi_), Fr * 3 * D, 3 * D,
+                       hip.ptr(h0_), hip.ptr(whh), hip.ptr(bhh), hip.ptr(out), hip.ptr(outT),
+                       Fr * D, D, hip.ptr(gt), Fr * 4 * D, 4 * D, hip.ptr(hp), hip.ptr(wf), nf,
+                       hip.stream())
+        dgh = torch.empty((n, Fr, 3 * D), device=DEV, dtype=T)
+        dgi = torch.empty((n, Fr, 3 * D), device=DEV, dtype=T)
+        bsum = torch.empty((n, 4 * D), device=DEV)
+        ddir = torch.empty((n, D), device=DEV)
+        dy_ = dy[r0:r0 + n].contiguous()
+        hip.lib().call('srnn_gru_xcd_bwd2', hip.BF16, n, D, Fr, hip.ptr(dy_), Fr * D, D,
+                       hip.ptr(gt), Fr * 4 * D, 4 * D, hip.ptr(out), Fr * D, D, hip.ptr(h0_),
+                       hip.ptr(whh_t), None, hip.ptr(dgh), None, hip.ptr(dgi), hip.ptr(bsum),
+                       Fr * 3 * D, 3 * D, hip.ptr(ddir), hip.ptr(wb), nb, hip.stream())
+        torch.cuda.synchronize()
+        assert hip.lib().dll.srnn_gru_xcd_error(hip.ptr(wf)) == 0
+        assert hip.lib().dll.srnn_gru_xcd_error(hip.ptr(wb)) == 0
+        return [x.cpu() for x in (out, outT, gt, hp, dgh, dgi, bsum, ddir)]
+
+    ref = [run(r0, 128) for r0 in range(0, 512, 128)] + [run(512, 88)]
+    ref = [torch.cat([c[i] for c in ref], 0) for i in range(8)]
+    for r0, n in ((0, 512), (0, 600), (64, 64), (0, 256), (128, 300)):
+        got = run(r0, n)
+        for i, (a, b) in enumerate(zip(got, ref)):
+            assert torch.equal(a, b[r0:r0 + n]), (r0, n, i)
 
 
 @pytest.mark.parametrize('B,D,Fr', [(128, 1024, 16), (64, 1024, 5), (100, 256, 9)])
