@@ -1,17 +1,27 @@
 """Benchmark of the SampleRNN hot path on MI355X (BASELINE.json metric).
 
-One JSON line (rank 0).  `value` = aggregate TBPTT training throughput (audio samples
-per second = ranks x B x T / step time) for configs[1]: 3-tier SampleRNN, dim 1024,
-frame_sizes [16, 4], 6-speaker + 43-d Ahocoder conditioning, T = 1024, B = 128 rows per
-GPU, bf16 MFMA (fp32 master weights / recurrences), one step = forward + backward +
-(all-reduce) + clipped Adam.  Weak scaling: every rank owns its own 128 stream rows.
-The line also carries `tbptt_steps_per_s`, the generation throughput of configs[2]
-(128 utterances x 3 s per GPU, replicas only; `gen` = bf16 through the persistent sample
-loop, `gen_fp32` = the parity-grade fp32 path), the roofline of the dominant kernel
-(its launches inside the timed steps, bracketed by HIP events on the launching stream)
-and a bounded CPU baseline.
+One JSON line (rank 0).  `value` = aggregate TBPTT training throughput (audio samples per
+second = global batch x T / step time) of the drop-in Trainer.train (trainer/__init__.py:62-117,
+the product path: forward, NLL, backward, DP all-reduce, fused clip + Adam, lagged failure
+check) on a 3-tier SampleRNN, dim 1024, frame_sizes [16, 4], 6 speakers + 43-d Ahocoder
+conditioning, T = 1024, bf16 MFMA with fp32 master weights / recurrences.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--no-gen] [--no-cpu]
+Default workload = configs[3]: global batch 512 stream rows sharded over the N ranks
+(512 / N rows per GPU, strong scaling; N = 1 is the whole 512-row batch on one GPU).  Beside
+it the line carries
+  * `config_b` (N = 1): configs[1], 128 rows on one GPU;
+  * `weak_64`: 64 rows per GPU (weak scaling at configs[3]'s 8-GPU share);
+  * `roofline`: the step's DOMINANT kernel (largest time per step among the probed launch
+    sites: GRU sweeps, dTab scatter, MLP hidden GEMM, fused clip + Adam), measured inside the
+    timed steps with HIP events on the launching stream; `kernels` lists every probed site;
+    `step_mfma`: executed MFMA work of the whole step / step time / bf16 peak;
+  * generation throughput of configs[2] (`gen` bf16 persistent loop, `gen_fp32` the reference
+    precision) and configs[4] (`gen_config_e`), rows sharded over ranks (each rank its
+    contiguous 1/N share of the utterances, no collective in the loop);
+  * `cpu_baseline`: the oracle (torch-CPU restatement) on the host cores, bounded samples of
+    the TBPTT step at configs[1]'s batch and of generation at configs[2]'s.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch ROWS_PER_GPU] [--no-gen]
 """
 import argparse
 import json
@@ -32,6 +42,8 @@ METRIC = ('audio samples/sec gen (3-tier dim1024) + TBPTT steps/sec @1/2/4/8 GPU
 MI355X_HBM_TBS = 8.0          # TB/s spec (MI355X_MICROARCH.md)
 MI355X_BF16_TFLOPS = 2500.0   # dense bf16 MFMA spec
 MI355X_FP32_TFLOPS = 157.3    # fp32 MFMA / vector spec
+GLOBAL_B = 512                # configs[3]
+T_SEQ, D_MODEL, FS, COND, SPK, Q = 1024, 1024, (16, 4), 43, 6, 256
 
 
 def log(*a):
@@ -71,127 +83,152 @@ def gpu_batches(batches, dev):
     return [(a.to(dev), r, t.to(dev), c.to(dev), s.to(dev)) for a, r, t, c, s in batches]
 
 
-def run_tbptt(args, dev, dist_mod):
+def step_mfma_flops(B, T=T_SEQ, D=D_MODEL, fs=FS, C=COND, S=SPK, Q=Q, n_rnn=1):
+    """MFMA work one TBPTT step executes (model.py's GEMMs and persistent sweeps, the folded
+    L1: the table build replaces the reference's 4.2 M-MAC/sample input conv).  flop = 2 MAC."""
+    f = 0.0
+    nfs = list(np.cumprod(fs))
+    for k, (fsz, n) in enumerate(zip(fs, nfs)):
+        M = B * T // n                                    # rows x frames of tier k
+        fwd = 2.0 * M * n * D                             # input_expand
+        if k == len(fs) - 1:
+            fwd += 2.0 * M * C * D + 2.0 * B * S * D      # cond_expand, spk_expand
+        fwd += n_rnn * (2.0 * M * D * 3 * D) * 2          # GRU input projection + recurrence
+        fwd += 2.0 * M * D * fsz * D                      # upsampling
+        bwd = 2 * (2.0 * M * D * fsz * D)                 # upsampling dW + dX
+        bwd += n_rnn * (2.0 * M * 3 * D * D * 4 + 2.0 * B * 3 * D * D)   # sweep, dW_hh,
+        bwd += 2.0 * M * D * n                            # dW_ih, dX; dh0 / input dW
+        if k == len(fs) - 1:
+            bwd += 2.0 * M * D * C + 2 * 2.0 * B * D * S
+        f += fwd + bwd
+    BT, F0 = B * T, fs[0]
+    f += 2.0 * F0 * Q * Q * D                             # Tab = Wp . E (forward)
+    f += 2.0 * BT * D * D + 2.0 * BT * D * Q              # hidden, output
+    f += 2 * 2.0 * BT * D * Q + 2 * 2.0 * BT * D * D      # their dW + dX
+    f += 2 * 2.0 * F0 * D * Q * Q                         # dE, dWp from dTab
+    return f
+
+
+def site_roofline(site, ms, work_per_step, dtype_peak):
+    """Roofline entry of one probed launch site: achieved = algorithmic work / its time."""
+    if site in ('dtab_scatter', 'adam_clip'):
+        ach = work_per_step / (ms * 1e-3) / 1e9
+        return {'bound': 'hbm', 'achieved': round(ach, 1), 'peak': MI355X_HBM_TBS * 1000,
+                'unit': 'GB/s', 'frac': round(ach / (MI355X_HBM_TBS * 1000), 4)}
+    ach = work_per_step / (ms * 1e-3) / 1e12
+    return {'bound': 'mfma', 'achieved': round(ach, 1), 'peak': dtype_peak, 'unit': 'TFLOP/s',
+            'frac': round(ach / dtype_peak, 4)}
+
+
+SITE_NOTES = {
+    'gru_xcd_bwd': 'gru_xcd_bwd_kernel: the GRU reverse sweeps (every tier, one persistent '
+                   'launch each; dgh_{t+1} W_hh products; latency-bound: one hand-off of dgh '
+                   'per step)',
+    'gru_xcd_fwd': 'gru_xcd_fwd_kernel: the GRU forward sweeps (W_hh h products; one hand-off '
+                   'of h per step)',
+    'dtab_scatter': 'dtab_pos_kernel: backward of the folded embedding.conv (dTab scatter; '
+                    'bound by LDS u64-atomic issue, priced against HBM)',
+    'mlp_hidden_gemm': 'gemm3p_kernel: sample-level MLP hidden layer (B*T x D x D, bias + '
+                       'ReLU epilogue)',
+    'adam_clip': 'adam_clip_multi_kernel: fused clamp + Adam over every parameter',
+}
+
+
+def run_tbptt(dev, dist_mod, rows, steps, warmup, dtype, probe=True):
+    """Warm-up then `steps` timed chunks of the drop-in Trainer.train on `rows` stream rows
+    of this rank.  Returns a dict (seconds = max over ranks)."""
     import nn as snn
     import optim
-    B, T, L = args.batch, 1024, 64
-    dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
+    import samplernn_hip as H
+    from trainer import Trainer
+    T, L = T_SEQ, 64
     m, pred = make_model(dtype)
     pred = pred.to(dev)
     sync = dist_mod.GradAllReduce(overlap_groups=dist_mod.readiness_groups(pred)) \
         if dist_mod.world() > 1 else None
     opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3), grad_sync=sync)
-    rows = slice(0, B)
-    n_chunks = args.warmup + args.steps
-    batches = gpu_batches(synth_batches(B, T, L, n_chunks, dist_mod.rank() * B), dev)
+    batches = gpu_batches(synth_batches(rows, T, L, warmup + steps, dist_mod.rank() * rows), dev)
     losses = []
 
-    def step(n):
-        inp, reset, tgt, cnd, spk = batches[n]
-        opt.zero_grad()     # fused clip+Adam: grads dropped, None == zero
-
-        def closure():
-            lp = pred(inp, reset, cnd, spk)
-            loss = snn.sequence_nll_loss_bits(lp, tgt)
-            loss.backward()
-            return loss
-        return opt.step(closure)
-
-    for n in range(args.warmup):
-        losses.append(step(n))
+    def criterion(out, tgt):
+        loss = snn.sequence_nll_loss_bits(out, tgt)
+        losses.append(loss.detach())
+        return loss
+    tr = Trainer(pred, criterion, opt, batches[:warmup], True, None)
+    tr.train()                              # warm-up chunks (ends with the failure check)
     torch.cuda.synchronize()
     dist_mod.barrier()
     torch.cuda.synchronize()
-    import samplernn_hip as H
-    # the roofline kernel's launches inside the timed steps, bracketed by HIP events on its
-    # stream (two event records per step; model.py _MlpFn.forward)
-    H.ROOF_EVENTS = []
+    tr.dataset = batches[warmup:]
+    tr.enqueue_s = 0.0
+    H.ROOF_EVENTS = {} if probe else None
     t0 = time.perf_counter()
-    for n in range(args.warmup, n_chunks):
-        losses.append(step(n))
-    t_host = time.perf_counter() - t0      # enqueue time: close to dt when launch-bound
+    tr.train()                              # the timed chunks
     torch.cuda.synchronize()
     dist_mod.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    roof_ev, H.ROOF_EVENTS = H.ROOF_EVENTS, None
-    kms_step = (sum(a.elapsed_time(b) for a, b in roof_ev) / len(roof_ev)) if roof_ev else None
-    sys.stderr.write('tbptt host enqueue %.2f ms/step\n' % (t_host * 1e3 / max(args.steps, 1)))
-    H.check_persistent_errors()            # (after the timed region) no hand-off given up
-    if H.HOST_TIME:
-        n_all = args.warmup + args.steps
-        tot = sum(s for _, s in H.HOST_TIME.values())
-        sys.stderr.write('host time in C entry points: %.2f ms/step (%d calls/step)\n' % (
-            tot * 1e3 / n_all, sum(n for n, _ in H.HOST_TIME.values()) // n_all))
-        for name, (n, s) in sorted(H.HOST_TIME.items(), key=lambda kv: -kv[1][1])[:30]:
-            sys.stderr.write('  %-34s %6d calls %8.1f us/call\n' % (name, n, s * 1e6 / n))
+    ev, H.ROOF_EVENTS = H.ROOF_EVENTS, None
+    sites = {}
+    for site, lst in (ev or {}).items():
+        ms = sum(a.elapsed_time(b) for a, b, _ in lst) / steps
+        work = sum(w for _, _, w in lst) / steps
+        sites[site] = (ms, work, len(lst) // steps)
     dt = dist_mod.max_over_ranks(dt, dev)
-    loss_vals = [float(l.detach()) if torch.is_tensor(l) else float(l) for l in losses]
-    return dt, loss_vals, pred, m, kms_step
+    res = {'seconds': dt, 'ms_per_step': dt / steps * 1e3,
+           'enqueue_ms_per_step': tr.enqueue_s / steps * 1e3,
+           'losses': [float(l) for l in losses], 'sites': sites, 'rows': rows}
+    del tr, opt, pred, m, batches
+    torch.cuda.empty_cache()
+    return res
 
 
-def run_gen(args, dev, n_seqs, n_cond, dtype, frame_sizes=(16, 4), cond_dim=43):
-    """One timed Generator call; returns (seconds, algorithmic weight elements read per
-    generation step: the sample-level MLP every step, tier k once per nfs_k steps)."""
-    import model as M
-    m, _ = make_model(dtype, seed=4242, frame_sizes=frame_sizes, cond_dim=cond_dim)
-    m = m.to(dev)
-    w_step = sum(p.numel() for p in m.sample_level_mlp.parameters()) + sum(
-        sum(p.numel() for p in t.parameters()) / t.n_frame_samples for t in m.frame_level_rnns)
-    cond = torch.rand(n_seqs, n_cond, cond_dim, generator=torch.Generator().manual_seed(1))
-    spk = np.arange(n_seqs) % 6
-    gen = M.Generator(m, True)
-    # warm-up (graph capture, kernel attributes) on a short run
-    gen(n_seqs, 0, cond[:, :4], spk, sampler='philox', seed=5)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    gen(n_seqs, 0, cond, spk, sampler='philox', seed=5)
-    torch.cuda.synchronize()
-    return time.perf_counter() - t0, w_step
+def tbptt_summary(r, N, dtype_peak, label):
+    samples = N * r['rows'] * T_SEQ
+    out = {'value': round(samples / (r['ms_per_step'] * 1e-3), 1), 'unit': 'samples/s',
+           'ms_per_step': round(r['ms_per_step'], 3),
+           'tbptt_steps_per_s': round(1e3 / r['ms_per_step'], 3),
+           'rows_per_gpu': r['rows'], 'global_batch': N * r['rows'],
+           'host_enqueue_ms_per_step': round(r['enqueue_ms_per_step'], 3),
+           'final_loss': round(r['losses'][-1], 4), 'workload': label}
+    flops = step_mfma_flops(r['rows'])
+    ach = flops / (r['ms_per_step'] * 1e-3) / 1e12
+    out['step_mfma'] = {'flop_per_step': flops, 'achieved': round(ach, 1), 'peak': dtype_peak,
+                        'unit': 'TFLOP/s', 'frac': round(ach / dtype_peak, 4)}
+    return out
 
 
-def kernel_roofline_gemm(dev, M, N, K, dtype, reps=20):
-    """Average duration of the dominant GEMM launch (same shape/layout/dtype as in the
-    step), timed with HIP events on the stream it is launched on."""
-    import samplernn_hip as H
-    a = torch.randn(M, K, device=dev).to(dtype)
-    w = torch.randn(N, K, device=dev).to(dtype)
-    bias = torch.zeros(N, device=dev)
-    out = torch.empty(M, N, device=dev, dtype=dtype)
-    for _ in range(10):
-        H.linear(a, w, bias=bias, relu=True, out=out)
-    s = torch.cuda.current_stream()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(reps):
-        H.linear(a, w, bias=bias, relu=True, out=out)
-    e1.record(s)
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / reps
-    return ms
+def kernels_block(r, dtype_peak):
+    ks = {}
+    for site, (ms, work, launches) in r['sites'].items():
+        e = site_roofline(site, ms, work, dtype_peak)
+        e.update({'ms_per_step': round(ms, 4), 'launches_per_step': launches,
+                  'work_per_step': work})
+        ks[site] = e
+    return ks
 
 
-def pmc_traffic(kernel, path=os.path.join(ROOT, 'profiles', 'r02_pmc_gemm.txt')):
-    """HBM bytes per launch of the roofline kernel from the committed rocprofv3 PMC passes
-    (tools/roofline_kernel.py under --pmc FETCH_SIZE, then --pmc WRITE_SIZE): FETCH_SIZE kB x 2
-    (gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md HBM section) + WRITE_SIZE kB."""
+def pmc_traffic(site, rows):
+    """HBM bytes per step of a probed site from the round's committed rocprofv3 PMC passes
+    (profiles/r03_pmc_<site>_b<rows>.txt, `avg_step_bytes` = (2 x FETCH_SIZE + WRITE_SIZE) over
+    the site's launches of one step, gfx950 FETCH correction per MI355X_MICROARCH.md); None
+    when no pass was committed for this site and batch."""
+    path = os.path.join(ROOT, 'profiles', 'r03_pmc_%s_b%d.txt' % (site, rows))
     try:
-        vals = {}
         for line in open(path):
-            m = line.split()
-            if len(m) >= 6 and m[0] == 'avg':
-                vals[m[1]] = float(m[-1])
-        return int(round((2 * vals['FETCH_SIZE'] + vals['WRITE_SIZE']) * 1024))
-    except (OSError, KeyError, ValueError):
-        return None
+            f = line.split()
+            if len(f) == 2 and f[0] == 'avg_step_bytes':
+                return int(f[1])
+    except (OSError, ValueError):
+        pass
+    return None
 
 
 def gru_sweep_roofline(dev, B=128, D=1024, Fr=64, reps=5):
     """MFMA utilisation of the recurrence's hidden x hidden products (the persistent XCD-grouped
-    sweeps, gru_xcd.hip): the bottom tier's forward and backward sweep at the TBPTT step's shape
-    (bf16, B rows, Fr frames), timed with HIP events on their stream; flop = Fr x 2 x B x 3D x D
-    per sweep (the forward's W_hh h, the backward's W_hh^T dgh).  Latency-bound: one hand-off of
-    h (dgh) between the group's workgroups per step."""
+    sweeps, gru_xcd.hip) in isolation: the bottom tier's forward and backward sweep at the
+    TBPTT step's shape (bf16, B rows, Fr frames), HIP events on their stream; flop = Fr x 2 x B
+    x 3D x D per sweep.  Latency-bound: one hand-off of h (dgh) per step."""
     import samplernn_hip as H
     T = torch.bfloat16
     g = torch.Generator(device=dev).manual_seed(3)
@@ -243,7 +280,33 @@ def gru_sweep_roofline(dev, B=128, D=1024, Fr=64, reps=5):
         res[name] = {'us_per_step': round(ms * 1e3 / Fr, 2), 'tflops': round(tf, 1),
                      'frac': round(tf / MI355X_BF16_TFLOPS, 4)}
     H.check_persistent_errors()
+    res.update({'bound': 'latency (one hand-off of h / dgh per step)', 'unit': 'TFLOP/s',
+                'peak': MI355X_BF16_TFLOPS,
+                'kernel': 'gru_xcd_fwd/bwd_kernel in isolation, bottom tier B=%d D=%d %d frames'
+                          % (B, D, Fr)})
     return res
+
+
+def run_gen(dev, n_seqs, n_cond, dtype, frame_sizes=(16, 4), cond_dim=43, row0=0):
+    """One timed Generator call over this rank's rows [row0, row0 + n_seqs); returns
+    (seconds, algorithmic weight elements read per generation step: the sample-level MLP
+    every step, tier k once per nfs_k steps)."""
+    import model as M
+    m, _ = make_model(dtype, seed=4242, frame_sizes=frame_sizes, cond_dim=cond_dim)
+    m = m.to(dev)
+    w_step = sum(p.numel() for p in m.sample_level_mlp.parameters()) + sum(
+        sum(p.numel() for p in t.parameters()) / t.n_frame_samples for t in m.frame_level_rnns)
+    cond = torch.rand(row0 + n_seqs, n_cond, cond_dim,
+                      generator=torch.Generator().manual_seed(1))[row0:]
+    spk = (np.arange(n_seqs) + row0) % 6
+    gen = M.Generator(m, True)
+    # warm-up (graph capture, kernel attributes) on a short run
+    gen(n_seqs, 0, cond[:, :4], spk, sampler='philox', seed=5)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gen(n_seqs, 0, cond, spk, sampler='philox', seed=5, row_offset=row0)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, w_step
 
 
 def gen_traffic(path=os.path.join(ROOT, 'profiles', 'r02_pmc_gen.txt')):
@@ -260,9 +323,11 @@ def gen_traffic(path=os.path.join(ROOT, 'profiles', 'r02_pmc_gen.txt')):
     return None
 
 
-def cpu_baseline(seconds_budget=20.0):
-    """The oracle (torch-CPU restatement of the reference) on the host cores: a bounded
-    TBPTT sample of the same workload (config B dims, T = 1024, B = 4 rows)."""
+def cpu_baseline(seconds_budget=30.0):
+    """The oracle (torch-CPU restatement of the reference, validated against the reference's
+    timing here: profiles/r03_oracle_vs_reference.txt) on the host cores: a bounded TBPTT
+    sample at configs[1]'s batch (B = 128 rows x T = 1024) and a bounded generation sample at
+    configs[2]'s (128 utterances x 4 top-tier frames = 256 steps)."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import samplernn_oracle as O
     threads = min(16, os.cpu_count() or 1)
@@ -274,21 +339,39 @@ def cpu_baseline(seconds_budget=20.0):
     om = O.from_state_dict(cfg, sd)
     names = [k for k, p in pred.named_parameters()]
     opt = O.OracleAdam([om.p[k] for k in names], lr=1e-3)
-    B = 4
+    B = 128
     batches = synth_batches(B, 1024, 64, 3, 0)
+    t0 = time.perf_counter()
     O.tbptt_step(om, opt, names, batches[0])          # warm-up
+    t_warm = time.perf_counter() - t0
     t0 = time.perf_counter()
     n = 0
     for b in batches[1:]:
         O.tbptt_step(om, opt, names, b)
         n += 1
-        if time.perf_counter() - t0 > seconds_budget:
+        if time.perf_counter() - t0 + t_warm > seconds_budget:
             break
     dt = time.perf_counter() - t0
-    return {'value': round(n * B * 1024 / dt, 2), 'unit': 'samples/s', 'cores': threads,
-            'kind': 'port',
-            'sample': '%d TBPTT step(s) of the oracle (torch-CPU fp32 restatement) at config-B '
-                      'dims, B=%d rows x T=1024, %d threads' % (n, B, threads)}
+    tb = {'value': round(n * B * 1024 / dt, 2), 'unit': 'samples/s', 'cores': threads,
+          'kind': 'port', 'steps_per_s': round(n / dt, 4),
+          'sample': '%d TBPTT step(s) of the oracle (torch-CPU fp32 restatement) at configs[1], '
+                    'B=%d rows x T=1024, after 1 warm-up step, %d threads' % (n, B, threads)}
+    # generation: 128 rows, 4 top-tier frames (256 steps) after a 1-frame warm-up
+    gm = O.from_state_dict(cfg, {k: v.detach().clone() for k, v in
+                                 make_model(torch.float32, seed=4242)[1].state_dict().items()})
+    nb, nc = 128, 4
+    cond = torch.rand(nb, nc, 43, generator=torch.Generator().manual_seed(1)).numpy()
+    noise = torch.empty(nc * 64, nb, 256).exponential_(1)
+    gm.generate(nb, cond[:, :1], np.arange(nb) % 6, noise[:64])
+    t0 = time.perf_counter()
+    gm.generate(nb, cond, np.arange(nb) % 6, noise)
+    dtg = time.perf_counter() - t0
+    gen = {'value': round(nb * nc * 64 / dtg, 1), 'unit': 'samples/s', 'cores': threads,
+           'kind': 'port', 'x_realtime': round(nb * nc * 64 / dtg / 16000, 3),
+           'sample': 'oracle Generator loop (model.py:445-520 restated), 128 utterances x 256 '
+                     'samples at configs[2] dims after a 64-sample warm-up, %d threads' % threads}
+    tb['gen'] = gen
+    return tb
 
 
 def main():
@@ -296,15 +379,17 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--batch', type=int, default=128)
+    ap.add_argument('--batch', type=int, default=None,
+                    help='rows per GPU (default: configs[3], global 512 / N, strong scaling)')
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--gen-dtype', default='bf16', choices=['bf16', 'fp32'])
     ap.add_argument('--no-gen-fp32', action='store_true')
     ap.add_argument('--no-gen-e', action='store_true')
-    ap.add_argument('--gen-seqs', type=int, default=128)
+    ap.add_argument('--gen-seqs', type=int, default=128, help='utterances per GPU')
     ap.add_argument('--gen-cond', type=int, default=750)
     ap.add_argument('--no-gen', action='store_true')
     ap.add_argument('--no-cpu', action='store_true')
+    ap.add_argument('--no-extra', action='store_true', help='skip config_b / weak_64 lines')
     args = ap.parse_args()
 
     import distributed as D
@@ -314,50 +399,58 @@ def main():
     N = D.world()
     if N != args.gpus:
         log('warning: --gpus %d but WORLD_SIZE %d' % (args.gpus, N))
-
-    dt, losses, pred, m, kms_step = run_tbptt(args, dev, D)
-    ms = dt / args.steps * 1000.0
-    rows = args.batch
-    samples = N * rows * 1024 * args.steps
-    value = samples / dt
-    log('tbptt: %.2f ms/step, losses %s' % (ms, ['%.3f' % l for l in losses]))
-    del pred, m
-    torch.cuda.empty_cache()
-
-    # dominant kernel of the TBPTT step: the MLP hidden layer GEMM (B*T x D x D, bf16)
-    tdt = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
-    M_, N_, K_ = rows * 1024, 1024, 1024
-    # achieved: the hidden-layer GEMM's average launch inside the timed steps; the same shape
-    # launched back to back in isolation (random operands, bias + ReLU) is reported beside it
-    kms_iso = kernel_roofline_gemm(dev, M_, N_, K_, tdt)
-    kms = kms_step if kms_step else kms_iso
-    flops = 2.0 * M_ * N_ * K_
-    ach = flops / (kms * 1e-3) / 1e12
+    dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
     peak = MI355X_BF16_TFLOPS if args.dtype == 'bf16' else MI355X_FP32_TFLOPS
-    roof = {'bound': 'mfma', 'achieved': round(ach, 1), 'peak': peak, 'unit': 'TFLOP/s',
-            'frac': round(ach / peak, 4),
-            'traffic': pmc_traffic('gemm3p_kernel') if (args.dtype == 'bf16' and rows == 128)
-            else None,
-            'traffic_algorithmic': 2 * (M_ * K_ + N_ * K_ + M_ * N_),
-            'kernel': 'gemm3p_kernel (MLP hidden layer %dx%dx%d %s, bias + relu epilogue), '
-                      '%.3f ms/launch inside the timed steps (%d launches, HIP events on its '
-                      'stream); %.3f ms/launch isolated, back to back'
-                      % (M_, N_, K_, args.dtype, kms, args.steps, kms_iso)}
-    # MFMA utilisation of the GRU recurrence (north star: "MFMA utilisation for the GRU GEMMs")
+    strong = args.batch is None
+    rows = GLOBAL_B // N if strong else args.batch
+    if strong and GLOBAL_B % N:
+        raise SystemExit('global batch %d not divisible by %d ranks' % (GLOBAL_B, N))
+
+    main_r = run_tbptt(dev, D, rows, args.steps, args.warmup, dtype)
+    log('tbptt %d rows/GPU: %.2f ms/step (host enqueue %.2f ms/step), losses %s' % (
+        rows, main_r['ms_per_step'], main_r['enqueue_ms_per_step'],
+        ['%.3f' % l for l in main_r['losses']]))
+    label = ('configs[3]: TBPTT step, 3-tier SampleRNN dim1024 FS=[16,4] n_rnn=1 cond 43 spk 6, '
+             'T=1024, global batch %d = %d rows/GPU x %d GPU, Trainer.train (fwd+bwd+%sclip+'
+             'Adam)' % (N * rows, rows, N, 'all-reduce+' if N > 1 else ''))
+    summ = tbptt_summary(main_r, N, peak, label)
+    ks = kernels_block(main_r, peak)
+    dom = max(ks, key=lambda k: ks[k]['ms_per_step']) if ks else None
+    roof = None
+    if dom:
+        roof = dict(ks[dom])
+        roof['traffic'] = pmc_traffic(dom, rows)
+        roof['kernel'] = '%s; %.3f ms per step inside the timed steps (%d launches, HIP events on '\
+                         'the launching stream)' % (SITE_NOTES.get(dom, dom), ks[dom]['ms_per_step'],
+                                                    ks[dom]['launches_per_step'])
+        roof['site'] = dom
+
+    extra = {}
+    if not args.no_extra:
+        if N == 1 and not (not strong and rows == 128):
+            r = run_tbptt(dev, D, 128, args.steps, args.warmup, dtype)
+            extra['config_b'] = tbptt_summary(
+                r, N, peak, 'configs[1]: the same step at B=128 rows on one GPU')
+            extra['config_b']['kernels'] = kernels_block(r, peak)
+            log('config_b: %.2f ms/step' % r['ms_per_step'])
+        if not (not strong and rows == 64) and not (strong and rows == 64):
+            r = run_tbptt(dev, D, 64, args.steps, args.warmup, dtype)
+            extra['weak_64'] = tbptt_summary(
+                r, N, peak, '64 rows per GPU x %d GPU (configs[3]\'s 8-GPU share, weak scaling)'
+                % N)
+            log('weak_64: %.2f ms/step' % r['ms_per_step'])
+
     gru = None
-    if args.dtype == 'bf16' and rows == 128:
-        gru = gru_sweep_roofline(dev)
-        if gru:
-            gru.update({'bound': 'latency (one hand-off of h / dgh per step)', 'unit': 'TFLOP/s',
-                        'peak': MI355X_BF16_TFLOPS,
-                        'kernel': 'gru_xcd_fwd/bwd_kernel, bottom tier B=128 D=1024 64 frames'})
+    if args.dtype == 'bf16':
+        gru = gru_sweep_roofline(dev, B=rows)
 
     def gen_line(dname, frame_sizes=(16, 4), cond_dim=43, n_cond=None, tag='3-tier dim1024 '
                  'FS=[16,4]'):
         gdt = torch.bfloat16 if dname == 'bf16' else torch.float32
         n_cond = n_cond or args.gen_cond
         L = int(np.prod(frame_sizes))
-        t, W_step = run_gen(args, dev, args.gen_seqs, n_cond, gdt, frame_sizes, cond_dim)
+        t, W_step = run_gen(dev, args.gen_seqs, n_cond, gdt, frame_sizes, cond_dim,
+                            row0=D.rank() * args.gen_seqs)
         t = D.max_over_ranks(t, dev)
         gs = N * args.gen_seqs * n_cond * L / t
         steps_per_s = n_cond * L / t
@@ -375,8 +468,10 @@ def main():
                 'sample_loop': ('persistent (gen_mlp.hip, %d rows/group)' % rows_pg) if rows_pg
                                else 'per-sample kernels (hipGraph)',
                 'config': {'workload': 'generate %s cond %d, %d utt x %d cond rows (%d samples) '
-                                       'per GPU, Philox sampler'
-                                       % (tag, cond_dim, args.gen_seqs, n_cond, n_cond * L)},
+                                       'per GPU (rows %d..%d of %d), Philox sampler'
+                                       % (tag, cond_dim, args.gen_seqs, n_cond, n_cond * L,
+                                          D.rank() * args.gen_seqs,
+                                          (D.rank() + 1) * args.gen_seqs - 1, N * args.gen_seqs)},
                 'roofline': {'bound': 'hbm',
                              'achieved': round(bytes_step * steps_per_s / 1e9, 1),
                              'peak': MI355X_HBM_TBS * 1000, 'unit': 'GB/s',
@@ -390,10 +485,10 @@ def main():
     if not args.no_gen:
         gen = gen_line(args.gen_dtype)
         if args.gen_dtype != 'fp32' and not args.no_gen_fp32:
-            gen_fp32 = gen_line('fp32')       # parity-grade numerics (bit-replay tests)
+            gen_fp32 = gen_line('fp32')       # the reference's precision (bit-replay tests)
         if not args.no_gen_e:
             # configs[4]: 4-tier + look-ahead conditioning (C = 86), 1024 utterances over 8
-            # GPUs = 128 per GPU (replicas), 188 cond rows x 256 = 48,128 samples each
+            # GPUs = 128 per GPU, 188 cond rows x 256 = 48,128 samples each
             gen_e = gen_line(args.gen_dtype, (16, 4, 4), 86, 188,
                              '4-tier dim1024 FS=[16,4,4] look-ahead')
 
@@ -402,19 +497,20 @@ def main():
         cpu = cpu_baseline()
 
     if D.rank() == 0:
-        line = {'metric': METRIC, 'value': round(value, 1), 'unit': 'samples/s',
+        line = {'metric': METRIC, 'value': summ['value'], 'unit': 'samples/s',
                 'n_gpus': N, 'steps': args.steps, 'warmup': args.warmup,
-                'ms_per_step': round(ms, 3), 'higher_is_better': True, 'scaling': 'weak',
+                'ms_per_step': summ['ms_per_step'], 'higher_is_better': True,
+                'scaling': 'strong' if strong else 'weak',
                 'vs_baseline': None, 'dtype': args.dtype, 'data': 'synthetic',
-                'config': {'workload': 'TBPTT step, 3-tier SampleRNN dim1024 FS=[16,4] n_rnn=1 '
-                                       'cond 43 spk 6, T=1024, B=%d rows/GPU, fwd+bwd+clip+Adam'
-                                       % rows,
-                           'global_batch': N * rows, 'seq_len': 1024,
-                           'parallelism': 'dp%d' % N},
-                'tbptt_steps_per_s': round(args.steps / dt, 3),
-                'roofline': roof, 'cpu_baseline': cpu, 'gen': gen, 'gen_fp32': gen_fp32,
+                'config': {'workload': label, 'global_batch': N * rows, 'seq_len': T_SEQ,
+                           'rows_per_gpu': rows, 'parallelism': 'dp%d' % N},
+                'tbptt_steps_per_s': summ['tbptt_steps_per_s'],
+                'host_enqueue_ms_per_step': summ['host_enqueue_ms_per_step'],
+                'roofline': roof, 'kernels': ks, 'step_mfma': summ['step_mfma'],
+                'cpu_baseline': cpu, 'gen': gen, 'gen_fp32': gen_fp32,
                 'gen_config_e': gen_e, 'gru_sweep': gru,
-                'final_loss': round(losses[-1], 4)}
+                'final_loss': summ['final_loss']}
+        line.update(extra)
         print(json.dumps(line), flush=True)
     D.barrier()
 

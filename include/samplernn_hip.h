@@ -92,9 +92,10 @@ int srnn_gru_cell_bwd(int dtype, int B, int D, const float* dy, int64_t lddy,
  * work: >= (64 * ceil(B/32) + 1) ints (zeroed by the call; the last word is an error flag
  * raised if a workgroup gave up waiting).  srnn_gru_seq_supported returns 1 / 0.       */
 int srnn_gru_seq_supported(int dtype, int B, int D);
-/* Whole-sequence GRU forward of one layer as ONE persistent launch with row groups of 16
- * placed per XCD (gru_xcd.hip): W_hh resident in VGPRs, h hand-offs as data-tagged granules
- * in the XCD's L2.  Same operands and outputs as srnn_gru_seq_fwd (torch.nn.GRU recurrence,
+/* Whole-sequence GRU forward of one layer as ONE persistent launch with row groups placed per
+ * XCD (gru_xcd.hip): W_hh resident in VGPRs, h hand-offs as data-tagged granules in the XCD's
+ * L2.  Any B: up to 4 tiles of 16 rows per group (512 rows per launch at D = 1024; more rows run
+ * as consecutive launches over row chunks, rows being independent).  Same operands and outputs as srnn_gru_seq_fwd (torch.nn.GRU recurrence,
  * model.py:148-165 / 244), gi includes b_ih; work = srnn_gru_xcd_work_bytes(dtype, B, D) bytes
  * (0 = shape or device not supported; zeroed by the call).  srnn_gru_xcd_error(work)
  * synchronises and returns nonzero if a hand-off was given up (bounded spin). */
@@ -140,6 +141,13 @@ int srnn_persistent_error_take(void);
  * flag |= (src > 0).  The flag rides in a gradient bucket so every rank agrees.           */
 int srnn_persistent_flag_to_f32(float* dst, void* stream);
 int srnn_persistent_flag_or_f32(const float* src, void* stream);
+/* Stream-ordered 4-byte copy of the flag into pinned host memory `dst`: the Trainer's lagged
+ * per-iteration check reads step n's copy after enqueuing step n+1 (trainer/__init__.py:116-117
+ * without a device synchronisation per iteration). */
+int srnn_persistent_flag_snapshot(int* dst, void* stream);
+/* dtype (fp32 / bf16) forms of srnn_persistent_flag_to_f32 / _or_f32 (bf16 gradient buckets) */
+int srnn_persistent_flag_to(void* dst, int dtype, void* stream);
+int srnn_persistent_flag_or(const void* src, int dtype, void* stream);
 int srnn_gru_seq_fwd(int dtype, int B, int D, int Fr, const float* gi, int64_t ldgi,
                      int64_t sgi, const float* h0, const void* h0_lp, const void* whh,
                      const float* bhh, float* out, void* out_lp, int64_t ldo, int64_t so,
@@ -247,6 +255,19 @@ int srnn_adam_clip_multi(int ntensors, float* const* p, float* const* g, float* 
                          float* const* v, void* const* p_bf16, const int64_t* n, float clip_lo,
                          float clip_hi, double lr, double beta1, double beta2, double eps,
                          int64_t step, void* stream);
+/* srnn_adam_clip_multi over gradients of dtype gdtype (fp32, or bf16 from bf16 gradient
+ * buckets) scaled by gscale before the clamp: under data parallelism the SUM-reduced buckets
+ * are read in place with gscale = 1 / world (the mean before the clip, optim.py:11-13 applied
+ * to the full-batch gradient).  fp32 gradients are written back clamped, bf16 ones only read. */
+int srnn_adam_clip_multi2(int ntensors, float* const* p, void* const* g, int gdtype, float gscale,
+                          float* const* m, float* const* v, void* const* p_bf16, const int64_t* n,
+                          float clip_lo, float clip_hi, double lr, double beta1, double beta2,
+                          double eps, int64_t step, void* stream);
+/* Data-parallel gradient bucket packing: src[i] (fp32, n[i] elements, NULL = zeros) ->
+ * flat + dst_off[i] in dtype (fp32 / bf16), all tensors in one launch.  The reference has no
+ * distributed step; this feeds distributed.GradAllReduce's RCCL all-reduce.   */
+int srnn_pack_grads(int ntensors, const float* const* src, const int64_t* n,
+                    const int64_t* dst_off, void* flat, int dtype, void* stream);
 
 /* ---- autoregressive generation (Generator.__call__, model.py:445-520) --------------- */
 typedef struct SrnnTier {
@@ -294,6 +315,13 @@ int srnn_gen_workspace_size(const SrnnModel* m, int n_seqs, size_t* bytes);
 int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const float* cond,
                   const float* row_bias, const float* noise, uint64_t seed, int64_t* seq,
                   float* logp, void* workspace, size_t workspace_bytes, int flags, void* stream);
+/* srnn_generate for rows [row0, row0 + n_seqs) of a larger batch (rank-sharded generation,
+ * SURVEY §8e, generate.py:241-253 run per rank): the Philox noise of local row b is that of
+ * global row row0 + b, so the shards together draw exactly the single-process stream.    */
+int srnn_generate2(const SrnnModel* m, int n_seqs, int n_cond, const float* cond,
+                   const float* row_bias, const float* noise, uint64_t seed, int row0,
+                   int64_t* seq, float* logp, void* workspace, size_t workspace_bytes, int flags,
+                   void* stream);
 
 #ifdef __cplusplus
 }

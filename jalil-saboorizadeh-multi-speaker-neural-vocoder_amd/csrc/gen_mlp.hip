@@ -484,7 +484,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             floatx4 lq = floatx4{0.f, 0.f, 0.f, 0.f};
             if (valid)
                 lq = a.lq ? *reinterpret_cast<const floatx4*>(a.lq + ((int64_t)s * B + b) * Q + 4 * lane)
-                          : log_noise(sample_noise(a.noise, a.seed, B, b, i - a.L, lane));
+                          : log_noise(sample_noise(a.noise, a.seed, B, b, i - a.L, lane, a.row0));
             if (!zcheck()) {
                 int spins = 0;
                 for (;;) {
@@ -562,7 +562,8 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
 
 // log q of the draws of nsteps generation steps, one wave per (step, row)
 __global__ __launch_bounds__(256) void gen_noise_kernel(const float* __restrict__ noise,
-                                                        uint64_t seed, const int* __restrict__ base,
+                                                        uint64_t seed, int row0,
+                                                        const int* __restrict__ base,
                                                         int off, int nsteps, int L, int B,
                                                         float* __restrict__ lq) {
     const int idx = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -570,14 +571,14 @@ __global__ __launch_bounds__(256) void gen_noise_kernel(const float* __restrict_
     const int s = idx / B, b = idx - s * B;
     const int i = *base + off + s;
     *reinterpret_cast<floatx4*>(lq + ((int64_t)s * B + b) * gm::Q + 4 * lane) =
-        log_noise(sample_noise(noise, seed, B, b, i - L, lane));
+        log_noise(sample_noise(noise, seed, B, b, i - L, lane, row0));
 }
 
-int gen_noise_launch(const float* noise, uint64_t seed, const int* base, int off, int nsteps,
-                     int L, int B, float* lq, hipStream_t s) {
+int gen_noise_launch(const float* noise, uint64_t seed, int row0, const int* base, int off,
+                     int nsteps, int L, int B, float* lq, hipStream_t s) {
     if (nsteps <= 0 || B <= 0) return 0;
     hipLaunchKernelGGL(gen_noise_kernel, dim3(cdiv((int64_t)nsteps * B, 4)), dim3(256), 0, s,
-                       noise, seed, base, off, nsteps, L, B, lq);
+                       noise, seed, row0, base, off, nsteps, L, B, lq);
     SRNN_LAUNCH_CHECK();
     return 0;
 }

@@ -22,6 +22,7 @@ int srnn_mlp_l1_impl(int dtype, const void* tab, const int64_t* x, int64_t ldx, 
                      const int* base, int B, int Tlen, int upper_dtype, const void* upper,
                      int64_t ldu, void* out, int64_t ldo, int D, int FS0, int Q, hipStream_t s);
 int srnn_sample_impl(const float* z, int64_t ldz, int B, const float* noise, uint64_t seed,
+                     int row0,
                      const int* base, int off, int L, int64_t* seq, int64_t ldseq,
                      float* logp_out, hipStream_t s);
 int srnn_gru_cell_impl(int dtype, int B, int D, int Din, const void* x, int64_t ldx,
@@ -80,6 +81,7 @@ __global__ __launch_bounds__(256) void tier_input_kernel(
 struct NoiseJob {
     const float* noise;      // (T, B, Q) Exp(1) draws, or null -> Philox(seed)
     uint64_t seed;
+    int row0;                // global index of row 0 (Philox counters)
     int nsteps;              // 0: no noise work
     float* lq;               // (nsteps, B, Q)
 };
@@ -94,7 +96,7 @@ __device__ __forceinline__ void noise_plane(const NoiseJob& nz, const int* base,
     const int st = idx / B, b = idx - st * B;
     const int i = *base + off + st;
     *reinterpret_cast<floatx4*>(nz.lq + ((int64_t)st * B + b) * 256 + 4 * lane) =
-        log_noise(sample_noise(nz.noise, nz.seed, B, b, i - L, lane));
+        log_noise(sample_noise(nz.noise, nz.seed, B, b, i - L, lane, nz.row0));
 }
 
 constexpr int TI_RB = 8, TI_OB = 64;
@@ -447,6 +449,7 @@ struct Ctx {
     const float* row_bias;
     const float* noise;
     uint64_t seed;
+    int row0 = 0;             // global index of row 0 (rank-sharded generation)
     int64_t* seq;
     int64_t ldseq;
     float* logp;
@@ -474,7 +477,7 @@ int tier_tick(Ctx& c, int k, int off, int par) {
         // then [up | gh'] = h [W_up; W_hh]^T + [b_up; b_hh]
         const SrnnTier& u = m->tier[1];
         const int fi = (off / t.n_frame_samples) % u.frame_size;
-        const NoiseJob nz{c.noise, c.seed, 0, nullptr};    // (the upper tick drew them)
+        const NoiseJob nz{c.noise, c.seed, c.row0, 0, nullptr};    // (the upper tick drew them)
         const dim3 g2(cdiv(D, 256), cdiv(B, FG_RB));
         const int planes = 1;
         const int64_t fs0d = (int64_t)t.frame_size * D;
@@ -496,7 +499,7 @@ int tier_tick(Ctx& c, int k, int off, int par) {
     if (k == 1 && c.b.fold_top) {
         // folded top tick: a (+ the period's noise) -> gi = a Min1^T + P1, gh1 carried ->
         // [G | gh1'] = h [Wfold; W_hh1]^T + [bfold; b_hh1]
-        NoiseJob nz{c.noise, c.seed, 0, nullptr};
+        NoiseJob nz{c.noise, c.seed, c.row0, 0, nullptr};
         const int gx = cdiv(B, 2);
         int planes = 1;
         if (c.pl && c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
@@ -543,7 +546,7 @@ int tier_tick(Ctx& c, int k, int off, int par) {
                     hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
                 attr[ai] = true;
             }
-            NoiseJob nz{c.noise, c.seed, 0, nullptr};
+            NoiseJob nz{c.noise, c.seed, c.row0, 0, nullptr};
             int planes = 1;
             if (k == (c.b.fold ? 1 : 0) && c.pl && c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
                 nz.nsteps = c.b.lq_steps;             // the persistent launches after this tick
@@ -613,7 +616,7 @@ int mlp_step(Ctx& c, int off) {
     RET(linear_fwd(dt, dt, B, D, D, c.b.a1, D, m->w_hid, D, m->b_hid, c.b.a2, D, 1, c.s));
     RET(linear_fwd(dt, SRNN_F32, B, Q, D, c.b.a2, D, m->w_out, D, m->b_out, c.b.logits, Q, 0,
                    c.s));
-    RET(srnn_sample_impl(c.b.logits, Q, B, c.noise, c.seed, c.b.base, off, c.L, c.seq, c.ldseq,
+    RET(srnn_sample_impl(c.b.logits, Q, B, c.noise, c.seed, c.row0, c.b.base, off, c.L, c.seq, c.ldseq,
                          c.logp, c.s));
     return 0;
 }
@@ -640,7 +643,7 @@ int run_block(Ctx& c, int periods) {
             a.tab = m->tab; a.w_hid = m->w_hid; a.b_hid = m->b_hid;
             a.w_out = m->w_out; a.b_out = m->b_out;
             a.up0 = c.b.up[0]; a.ldup = c.b.ldup0;
-            a.noise = c.noise; a.seed = c.seed;
+            a.noise = c.noise; a.seed = c.seed; a.row0 = c.row0;
             a.seq = c.seq; a.ldseq = c.ldseq; a.logp = c.logp;
             a.base = c.b.base; a.off = off; a.nsteps = m->tier[0].frame_size; a.L = c.L;
             a.B = c.B; a.D = m->dim; a.FS0 = m->tier[0].frame_size;
@@ -649,7 +652,7 @@ int run_block(Ctx& c, int periods) {
             if (c.b.lq && env_flag("SRNN_GEN_NOISE_AHEAD", 1)) {
                 // drawn ahead by a tick's input launch, else by a launch here
                 if (off < c.noise_beg || off + a.nsteps > c.noise_end) {
-                    RET(gen_noise_launch(c.noise, c.seed, c.b.base, off, a.nsteps, c.L, c.B,
+                    RET(gen_noise_launch(c.noise, c.seed, c.row0, c.b.base, off, a.nsteps, c.L, c.B,
                                          c.b.lq, c.s));
                     c.noise_beg = off;
                     c.noise_end = off + a.nsteps;
@@ -698,10 +701,24 @@ extern "C" int srnn_gen_workspace_size(const SrnnModel* m, int n_seqs, size_t* b
     return 0;
 }
 
+extern "C" int srnn_generate2(const SrnnModel* m, int n_seqs, int n_cond, const float* cond,
+                              const float* row_bias, const float* noise, uint64_t seed,
+                              int row0, int64_t* seq, float* logp, void* workspace,
+                              size_t workspace_bytes, int flags, void* stream);
+
 extern "C" int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const float* cond,
                              const float* row_bias, const float* noise, uint64_t seed,
                              int64_t* seq, float* logp, void* workspace, size_t workspace_bytes,
                              int flags, void* stream) {
+    return srnn_generate2(m, n_seqs, n_cond, cond, row_bias, noise, seed, 0, seq, logp,
+                          workspace, workspace_bytes, flags, stream);
+}
+
+extern "C" int srnn_generate2(const SrnnModel* m, int n_seqs, int n_cond, const float* cond,
+                              const float* row_bias, const float* noise, uint64_t seed,
+                              int row0, int64_t* seq, float* logp, void* workspace,
+                              size_t workspace_bytes, int flags, void* stream) {
+    SRNN_REQUIRE(row0 >= 0, "generate: negative row offset");
     SRNN_REQUIRE(m && n_seqs > 0 && n_cond > 0 && seq && workspace, "generate: bad args");
     SRNN_REQUIRE(m->n_tiers >= 1 && m->n_tiers <= SRNN_MAX_TIERS, "generate: n_tiers");
     SRNN_REQUIRE(m->n_rnn >= 1 && m->n_rnn <= SRNN_MAX_RNN, "generate: n_rnn");
@@ -721,6 +738,7 @@ extern "C" int srnn_generate(const SrnnModel* m, int n_seqs, int n_cond, const f
     c.row_bias = row_bias;
     c.noise = noise;
     c.seed = seed;
+    c.row0 = row0;
     c.seq = seq;
     c.ldseq = (int64_t)c.L * (n_cond + 1);
     c.logp = logp;

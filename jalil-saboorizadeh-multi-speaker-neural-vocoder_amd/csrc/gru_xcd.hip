@@ -27,6 +27,10 @@ constexpr int CU = 32;                 // units per workgroup
 constexpr int NT = 6;                  // n tiles: 3 gates x 2 x 16 units
 constexpr int UK = 32;                 // k per bf16 MFMA unit
 constexpr int MAXMT = 4;               // row tiles per group (B up to 512 rows at D = 1024)
+// cross-wave reduction buffer: component planes of PS floats, [buf][kw][tile][e][PS]; a
+// reader half-wave takes component e of 16 lanes of two adjacent tiles, 4 PS = 16 (mod 32)
+// banks apart: conflict-free ds_read_b32 (the lane-major floatx4 layout was 4-way)
+constexpr int PS = 68;
 // work header: [0] error word, ints [16, HDR / 4) the placement-check slots ([G][P])
 constexpr int HDR = 2048;
 }  // namespace gx
@@ -62,6 +66,8 @@ struct GruXArgs {
     int B, D, Fr, G, P, RV;
     int poll_sleep;                                 // s_sleep 1 repeats between polls
     unsigned long long* diag;                       // optional phase timestamps (timing only)
+    int exp;                                        // timing experiments (SRNN_GX_EXP, results
+                                                    // invalid): 1 no output stores, 2 no gi loads
 };
 
 template <int UPW, int MT>
@@ -71,8 +77,9 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int D = a.D, B = a.B, RV = a.RV;
     const int NU = D / UK, KW = NW < NU ? NW : NU;
-    floatx4* red = (floatx4*)smem;                              // [KW][NT][64]
-    int* gsh = (int*)(smem + (size_t)KW * NT * 64 * sizeof(floatx4));
+    // double-buffered by the (step, tile) parity: one barrier per (step, tile)
+    float* red = (float*)smem;                                  // [2][KW][NT][4][PS]
+    int* gsh = (int*)(smem + (size_t)2 * KW * NT * 4 * PS * sizeof(float));
     // static map (handoff.hpp): group g = block % G, member p = block / G; the placement
     // check runs while the weights load
     const int g = blockIdx.x % a.G, p = blockIdx.x / a.G;
@@ -117,7 +124,11 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     const int r = tid >> 5, uu = tid & 31;
     const bool rv = r < RV;
     const int unit = u0 + uu;
-    auto row_of = [&](int m) { return (g * MT + m) * RV + r; };
+    // row_of's lane part is re-made opaque every trip of the step loop (rop below), so the
+    // compiler recomputes the per-tile row addresses instead of keeping MT sets of 64-bit
+    // pointers live across the loop (at MT = 4 they spilled)
+    int rop = r;
+    auto row_of = [&](int m) { return (g * MT + m) * RV + rop; };
     const float bhr = a.bhh[unit], bhz = a.bhh[D + unit], bhn = a.bhh[2 * D + unit];
     float hprev[MT];
 #pragma unroll
@@ -153,6 +164,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
         ga = Gi{gp0[unit], gp0[D + unit], gp0[2 * D + unit]};
     }
     auto fetch_gi = [&](int t, int m, Gi& nx) {     // operands of the (step, tile) after (t, m)
+        if (a.exp & 2) return;
         int tn = t, mn = m + 1;
         if (mn == MT) { mn = 0; tn = min(t + 1, a.Fr - 1); }
         const float* gp = a.gi + (int64_t)min(row_of(mn), B - 1) * a.ldgi + (int64_t)tn * a.sgi;
@@ -206,8 +218,11 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     #pragma unroll
                     for (int i = 0; i < NT; ++i) Mma<bf16>::run(acc[i], af, wf[j][i]);
                 }
+                float* rb = red + (size_t)(((t * MT + m) & 1) * KW + wave) * NT * 4 * PS + lane;
     #pragma unroll
-                for (int i = 0; i < NT; ++i) red[(wave * NT + i) * 64 + lane] = acc[i];
+                for (int i = 0; i < NT; ++i)
+    #pragma unroll
+                    for (int e = 0; e < 4; ++e) rb[(i * 4 + e) * PS] = acc[i][e];
             }
             GX_STAMP();
             __syncthreads();
@@ -215,6 +230,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
             float gh[3];
             {
                 const int ln = (r >> 2) * 16 + (uu & 15), ii = r & 3;
+                const float* rb = red + (size_t)((t * MT + m) & 1) * KW * NT * 4 * PS + ii * PS + ln;
     #pragma unroll
                 for (int gt = 0; gt < 3; ++gt) {
                     const int tile = 2 * gt + (uu >> 4);
@@ -222,7 +238,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
                     float pr[NW];
                     #pragma unroll
                     for (int kw = 0; kw < NW; ++kw)
-                        pr[kw] = red[(min(kw, KW - 1) * NT + tile) * 64 + ln][ii];
+                        pr[kw] = rb[(min(kw, KW - 1) * NT + tile) * 4 * PS];
                     #pragma unroll
                     for (int kw = 0; kw < NW; ++kw) v += kw < KW ? pr[kw] : 0.f;
                     gh[gt] = v;
@@ -237,7 +253,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
             publish(t, m, hn);
             GX_STAMP();
             const int row = row_of(m);
-            if (rv && row < B) {
+            if (rv && row < B && !(a.exp & 1)) {
                 const int64_t o = (int64_t)row * a.ldo + (int64_t)t * a.so + unit;
                 a.out[o] = hn;
                 a.out_lp[o] = __float2bfloat16(hn);
@@ -245,13 +261,15 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
                 float* gt = a.gates + (int64_t)row * a.ldg + (int64_t)t * a.sg;
                 gt[unit] = rr; gt[D + unit] = zz; gt[2 * D + unit] = nn; gt[3 * D + unit] = ghn;
             }
-            __syncthreads();                       // red is rewritten next (step, tile)
+            // (no barrier: the next (step, tile) writes the other red buffer, and this one is
+            //  rewritten only after every wave passed the next (step, tile)'s barrier)
             GX_STAMP();
     };
     // (step, tile) sequence, unrolled by two for the alternating operand sets (MT = 1: two
     // steps per trip; MT even: the tiles of one step)
     constexpr int TU = MT == 1 ? 2 : 1;
     for (int t0 = 0; t0 < a.Fr; t0 += TU) {
+        if (MT > 1) asm volatile("" : "+v"(rop));
 #pragma unroll
         for (int q = 0; q < TU * MT; ++q) {
             const int t = t0 + q / MT, m = q % MT;
@@ -288,6 +306,7 @@ struct GruXBwdArgs {
     int spin_limit;
     int withhold;
     int B, D, Fr, G, P, RV;
+    int exp;                                        // timing experiments (as the forward)
 };
 
 template <int UPW, bool FULL, int MT>   // FULL: NU == UPW * NW (every unit of every wave in range)
@@ -298,8 +317,9 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
     const int D = a.D, B = a.B, K3 = 3 * D, RV = a.RV;
     const int NU = K3 / UK, KW = NW < NU ? NW : NU;
     constexpr int NTB = 2;                                      // 32 units = 2 n tiles
-    floatx4* red = (floatx4*)smem;                              // [KW][2][64]
-    int* gsh = (int*)(smem + (size_t)KW * NTB * 64 * sizeof(floatx4));
+    float* red = (float*)smem;                                  // [2][KW][NTB][4][PS]
+    const size_t red_bytes = (size_t)2 * KW * NTB * 4 * PS * sizeof(float);
+    int* gsh = (int*)(smem + red_bytes);
     // static map (handoff.hpp): group g = block % G, member p = block / G; the placement
     // check runs while the weights load
     const int g = blockIdx.x % a.G, p = blockIdx.x / a.G;
@@ -338,7 +358,8 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
     const int r = tid >> 5, uu = tid & 31;
     const bool rv = r < RV;
     const int unit = u0 + uu;
-    auto row_of = [&](int m) { return (g * MT + m) * RV + r; };
+    int rop = r;                                    // (opaque per step: see the forward)
+    auto row_of = [&](int m) { return (g * MT + m) * RV + rop; };
     const __amdgpu_buffer_rsrc_t rx = hx_rsrc(a.xg);
     const size_t bufw = (size_t)a.G * MT * RG * KG;
     const int lrow = lane & 15;
@@ -357,11 +378,12 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
     // at MT = 1, per-thread LDS slots above (the register file is full at D = 1024: W_hh^T
     // slice + poll buffer; the tile loop is not unrolled, so its index is not a constant)
     float ddir1 = 0.f, sar1 = 0.f, saz1 = 0.f, sghn1 = 0.f, san1 = 0.f;
-    float* sl = (float*)(smem + (size_t)KW * NTB * 64 * sizeof(floatx4) + 64);   // [MT][5][NTHR]
+    float* sl = (float*)(smem + red_bytes + 64);                 // [MT][5][NTHR]
     if (MT > 1)
         for (int k = 0; k < 5 * MT; ++k) sl[k * NTHR + tid] = 0.f;
     fetch(a.Fr - 1, 0, dyv, gr, gz, gn, gg, hp);
     for (int t = a.Fr - 1; t >= 0; --t) {
+    asm volatile("" : "+v"(rop));
 #pragma unroll 1
     for (int m = 0; m < MT; ++m) {
         const bool has_next = t + 1 < a.Fr;
@@ -412,17 +434,22 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
 #pragma unroll
                     for (int i = 0; i < NTB; ++i) Mma<bf16>::run(acc[i], af, wf[j][i]);
                 }
+                float* rb = red + (size_t)((((a.Fr - 1 - t) * MT + m) & 1) * KW + wave) * NTB * 4 * PS + lane;
 #pragma unroll
-                for (int i = 0; i < NTB; ++i) red[(wave * NTB + i) * 64 + lane] = acc[i];
+                for (int i = 0; i < NTB; ++i)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) rb[(i * 4 + e) * PS] = acc[i][e];
             }
             __syncthreads();
         }
         float s = 0.f;
         if (has_next) {
             const int ln = (r >> 2) * 16 + (uu & 15), ii = r & 3, tile = uu >> 4;
+            const float* rb = red + (size_t)(((a.Fr - 1 - t) * MT + m) & 1) * KW * NTB * 4 * PS +
+                              ii * PS + ln;
             float pr[NW];
 #pragma unroll
-            for (int kw = 0; kw < NW; ++kw) pr[kw] = red[(min(kw, KW - 1) * NTB + tile) * 64 + ln][ii];
+            for (int kw = 0; kw < NW; ++kw) pr[kw] = rb[(min(kw, KW - 1) * NTB + tile) * 4 * PS];
 #pragma unroll
             for (int kw = 0; kw < NW; ++kw) s += kw < KW ? pr[kw] : 0.f;
         }
@@ -444,10 +471,12 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
             }
         }
         const float cdar = o.dar, cdaz = o.daz, cdghn = o.dghn, cdan = o.dan;
-        if (m + 1 < MT) fetch(t, m + 1, dyv, gr, gz, gn, gg, hp);
-        else if (t > 0) fetch(t - 1, 0, dyv, gr, gz, gn, gg, hp);
+        if (!(a.exp & 2)) {
+            if (m + 1 < MT) fetch(t, m + 1, dyv, gr, gz, gn, gg, hp);
+            else if (t > 0) fetch(t - 1, 0, dyv, gr, gz, gn, gg, hp);
+        }
         const int row = row_of(m);
-        if (rv && row < B) {
+        if (rv && row < B && !(a.exp & 1)) {
             const int64_t ob = (int64_t)row * a.ldd + (int64_t)t * a.sd;
             if (a.dgh) {
                 float* dg = a.dgh + ob;
@@ -471,7 +500,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
             }
             if (t == 0) a.ddir0[(int64_t)row * D + unit] = o.ddir;
         }
-        __syncthreads();
+        // (no barrier: red is double-buffered by the (step, tile) parity, see the forward)
     }
     }
 #pragma unroll
@@ -604,6 +633,7 @@ extern "C" int srnn_gru_xcd_fwd2(int dtype, int B, int D, int Fr, const float* g
     a.B = B; a.D = D; a.Fr = Fr;
     a.diag = nullptr;
     a.poll_sleep = env_flag("SRNN_POLL_SLEEP", 1);
+    a.exp = env_flag("SRNN_GX_EXP", 0);
     {
         static unsigned long long* diag = nullptr;
         static int armed = -1;
@@ -620,7 +650,7 @@ extern "C" int srnn_gru_xcd_fwd2(int dtype, int B, int D, int Fr, const float* g
     a.RV = L.rv;
     const int NU = D / gx::UK;
     const int KW = NU < gx::NW ? NU : gx::NW;
-    const size_t lds = (size_t)KW * gx::NT * 64 * 16 + 16;
+    const size_t lds = (size_t)2 * KW * gx::NT * 4 * gx::PS * 4 + 16;
     const int upw = cdiv(NU, gx::NW);
     const int ui = upw <= 1 ? 0 : upw <= 2 ? 1 : 2;
     const int mi = L.mt == 1 ? 0 : L.mt == 2 ? 1 : 2;
@@ -633,7 +663,8 @@ extern "C" int srnn_gru_xcd_fwd2(int dtype, int B, int D, int Fr, const float* g
     static bool attr[3][3] = {};
     if (!attr[ui][mi]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 65536));
+                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           160 * 1024));
         attr[ui][mi] = true;
     }
     hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
@@ -707,12 +738,13 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
     a.census = env_flag("SRNN_GEN_LOCAL", 1) ? (int*)work + 16 : nullptr;
     a.xg = (u64*)((char*)work + gx::HDR);
     a.B = B; a.D = D; a.Fr = Fr;
+    a.exp = env_flag("SRNN_GX_EXP", 0);
     a.G = L.G;
     a.P = L.P;
     a.RV = L.rv;
     const int NU = 3 * D / gx::UK;
     const int KW = NU < gx::NW ? NU : gx::NW;
-    const size_t lds = (size_t)KW * 2 * 64 * 16 + 64 +
+    const size_t lds = (size_t)2 * KW * 2 * 4 * gx::PS * 4 + 64 +
                        (L.mt > 1 ? (size_t)L.mt * 5 * gx::NTHR * 4 : 0);
     const int upw = cdiv(NU, gx::NW);
     const int ui = upw <= 3 ? 0 : upw <= 6 ? 1 : 2;

@@ -1,3 +1,4 @@
+#include <type_traits>
 // Memory-bound support kernels of the hot path: mu-law quantize/dequantize (utils.py),
 // weight-norm forward/backward (torch weight_norm, model.py:119-131,177-178,303-306),
 // layout permutes for the folded weights, row gathers (nn.Embedding), column sums
@@ -852,23 +853,39 @@ __global__ void adam_clip_kernel(float* __restrict__ p, float* __restrict__ g,
 // descriptors travel in the kernel argument block).  A workgroup takes a 2048-element
 // chunk of the concatenated index space; the chunk's first tensor is found by a uniform
 // scan of the offsets, and a thread steps to the next tensor at a boundary.
+// GT: gradient element type (float, or bf16 for gradients reduced in bf16 buckets under data
+// parallelism); gscale multiplies the gradient before the clamp (the DP mean's 1 / N, so the
+// summed buckets need no separate scaling pass).  fp32 gradients are written back clamped
+// (hardtanh_ is in place in the reference, optim.py:13); bf16 ones are only read.
 #define ADAM_MT 64
 struct AdamMulti {
     int nt;
     int64_t off[ADAM_MT + 1];     // element offsets
     int boff[ADAM_MT + 1];        // first workgroup of each tensor
     float* p[ADAM_MT];
-    float* g[ADAM_MT];
+    void* g[ADAM_MT];
     float* m[ADAM_MT];
     float* v[ADAM_MT];
     bf16* plp[ADAM_MT];
 };
 
+__device__ __forceinline__ floatx4 adam_ld4(const float* g) {
+    return *reinterpret_cast<const floatx4*>(g);
+}
+__device__ __forceinline__ floatx4 adam_ld4(const bf16* g) {
+    const uint2 u = *reinterpret_cast<const uint2*>(g);
+    return floatx4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                   __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+}
+
+template <typename GT>
 __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float lo, float hi,
                                                               float w1, float b2, float omb2,
                                                               float step_size, float bc2s,
-                                                              float eps, const int* skip) {
+                                                              float eps, float gscale,
+                                                              const int* skip) {
     constexpr int CH = 2048;
+    constexpr bool WB = std::is_same<GT, float>::value;      // write the clamped grad back
     // a persistent sweep of this step gave up a hand-off (persist.hip): its gradients are
     // invalid, so neither the weights nor the Adam moments move (the host raises after)
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(skip, __ATOMIC_RELAXED,
@@ -881,7 +898,7 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
     t = __builtin_amdgcn_readfirstlane(t);
     const int64_t n = a.off[t + 1] - a.off[t];
     float* __restrict__ P = a.p[t];
-    float* __restrict__ G = a.g[t];
+    GT* __restrict__ G = (GT*)a.g[t];
     float* __restrict__ Mm = a.m[t];
     float* __restrict__ V = a.v[t];
     bf16* __restrict__ PL = a.plp[t];
@@ -889,7 +906,7 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
     // (a null gradient is an all-zero one: a parameter backward did not reach this
     //  step, e.g. the learned h0 on a carried chunk -- torch-0.4 zero_grad semantics)
     auto upd = [&](float g, float& p, float& m, float& v) {
-        const float gi = fminf(fmaxf(g, lo), hi);
+        const float gi = fminf(fmaxf(g * gscale, lo), hi);
         m = m + w1 * (gi - m);
         v = v * b2;
         v = v + omb2 * gi * gi;
@@ -897,13 +914,14 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
         p = p + (-step_size) * m / denom;
         return gi;
     };
-    // two 4-element chunks per thread (16-B accesses; every tensor is its own allocation,
-    // so chunk starts are 16-B aligned); the ragged end element by element
+    // two 4-element chunks per thread (16-B accesses; every tensor is its own allocation or a
+    // 64-element-aligned view, so chunk starts are 16-B aligned); the ragged end element by
+    // element
 #pragma unroll
     for (int c = 0; c < CH / 1024; ++c) {
         const int64_t j = j0 + c * 1024 + 4 * threadIdx.x;
         if (j + 4 <= n) {
-            floatx4 g4 = G ? *reinterpret_cast<const floatx4*>(G + j) : floatx4{0.f, 0.f, 0.f, 0.f};
+            floatx4 g4 = G ? adam_ld4(G + j) : floatx4{0.f, 0.f, 0.f, 0.f};
             floatx4 p4 = *reinterpret_cast<const floatx4*>(P + j);
             floatx4 m4 = *reinterpret_cast<const floatx4*>(Mm + j);
             floatx4 v4 = *reinterpret_cast<const floatx4*>(V + j);
@@ -913,7 +931,7 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
                 g4[e] = upd(g4[e], pe, me, ve);
                 p4[e] = pe; m4[e] = me; v4[e] = ve;
             }
-            if (G) *reinterpret_cast<floatx4*>(G + j) = g4;
+            if (WB && G) *reinterpret_cast<floatx4*>((float*)G + j) = g4;
             *reinterpret_cast<floatx4*>(Mm + j) = m4;
             *reinterpret_cast<floatx4*>(V + j) = v4;
             *reinterpret_cast<floatx4*>(P + j) = p4;
@@ -927,8 +945,8 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
         } else {
             for (int64_t k = j; k < n && k < j + 4; ++k) {
                 float pe = P[k], me = Mm[k], ve = V[k];
-                const float gi = upd(G ? G[k] : 0.f, pe, me, ve);
-                if (G) G[k] = gi;
+                const float gi = upd(G ? to_f(G[k]) : 0.f, pe, me, ve);
+                if (WB && G) ((float*)G)[k] = gi;
                 Mm[k] = me;
                 V[k] = ve;
                 P[k] = pe;
@@ -938,13 +956,14 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
     }
 }
 
-extern "C" int srnn_adam_clip_multi(int ntensors, float* const* p, float* const* g,
-                                    float* const* m, float* const* v, void* const* p_bf16,
-                                    const int64_t* n, float clip_lo, float clip_hi, double lr,
-                                    double beta1, double beta2, double eps, int64_t step,
-                                    void* stream) {
+extern "C" int srnn_adam_clip_multi2(int ntensors, float* const* p, void* const* g, int gdtype,
+                                     float gscale, float* const* m, float* const* v,
+                                     void* const* p_bf16, const int64_t* n, float clip_lo,
+                                     float clip_hi, double lr, double beta1, double beta2,
+                                     double eps, int64_t step, void* stream) {
     SRNN_REQUIRE(ntensors >= 0, "adam_multi: bad tensor count");
     SRNN_REQUIRE(step >= 1, "adam: step must be >= 1");
+    SRNN_REQUIRE(gdtype == SRNN_F32 || gdtype == SRNN_BF16, "adam_multi: gradient dtype");
     const double bc1 = 1.0 - pow(beta1, (double)step);
     const double bc2 = 1.0 - pow(beta2, (double)step);
     const float step_size = (float)(lr / bc1);
@@ -970,9 +989,80 @@ extern "C" int srnn_adam_clip_multi(int ntensors, float* const* p, float* const*
         t0 = t;
         if (a.nt == 0) continue;
         const int64_t nblk = a.boff[a.nt];
-        hipLaunchKernelGGL(adam_clip_multi_kernel, dim3((unsigned)nblk), dim3(256), 0,
-                           (hipStream_t)stream, a, clip_lo, clip_hi, (float)(1.0 - beta1),
-                           (float)beta2, (float)(1.0 - beta2), step_size, bc2s, (float)eps, skip);
+        if (gdtype == SRNN_F32)
+            hipLaunchKernelGGL(adam_clip_multi_kernel<float>, dim3((unsigned)nblk), dim3(256), 0,
+                               (hipStream_t)stream, a, clip_lo, clip_hi, (float)(1.0 - beta1),
+                               (float)beta2, (float)(1.0 - beta2), step_size, bc2s, (float)eps,
+                               gscale, skip);
+        else
+            hipLaunchKernelGGL(adam_clip_multi_kernel<bf16>, dim3((unsigned)nblk), dim3(256), 0,
+                               (hipStream_t)stream, a, clip_lo, clip_hi, (float)(1.0 - beta1),
+                               (float)beta2, (float)(1.0 - beta2), step_size, bc2s, (float)eps,
+                               gscale, skip);
+        SRNN_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
+extern "C" int srnn_adam_clip_multi(int ntensors, float* const* p, float* const* g,
+                                    float* const* m, float* const* v, void* const* p_bf16,
+                                    const int64_t* n, float clip_lo, float clip_hi, double lr,
+                                    double beta1, double beta2, double eps, int64_t step,
+                                    void* stream) {
+    return srnn_adam_clip_multi2(ntensors, p, (void* const*)g, SRNN_F32, 1.0f, m, v, p_bf16, n,
+                                 clip_lo, clip_hi, lr, beta1, beta2, eps, step, stream);
+}
+
+// ------------------------------------------------------------------ gradient buckets
+// Data-parallel gradient packing (distributed.py GradAllReduce): n gradient tensors (fp32,
+// or NULL = all zero) copied into one flat bucket at 64-element-aligned offsets, converted to
+// the bucket's dtype, in ONE launch (the per-parameter copy_ launches it replaces cost a
+// launch each); the reduced bucket is read in place by srnn_adam_clip_multi2.
+#define PACK_MT 64
+struct PackMulti {
+    int nt;
+    int boff[PACK_MT + 1];
+    const float* src[PACK_MT];
+    int64_t n[PACK_MT];
+    int64_t dst_off[PACK_MT];
+};
+
+template <typename TD>
+__global__ __launch_bounds__(256) void pack_grads_kernel(PackMulti a, TD* __restrict__ flat) {
+    int t = 0;
+    while (t + 1 < a.nt && a.boff[t + 1] <= (int)blockIdx.x) ++t;
+    t = __builtin_amdgcn_readfirstlane(t);
+    const float* __restrict__ src = a.src[t];
+    const int64_t n = a.n[t];
+    TD* __restrict__ dst = flat + a.dst_off[t];
+    const int64_t j0 = (int64_t)(blockIdx.x - a.boff[t]) * 2048;
+    for (int64_t j = j0 + threadIdx.x; j < n && j < j0 + 2048; j += 256)
+        dst[j] = from_f<TD>(src ? src[j] : 0.f);
+}
+
+extern "C" int srnn_pack_grads(int ntensors, const float* const* src, const int64_t* n,
+                               const int64_t* dst_off, void* flat, int dtype, void* stream) {
+    SRNN_REQUIRE(ntensors >= 0 && flat, "pack_grads: bad arguments");
+    SRNN_REQUIRE(dtype == SRNN_F32 || dtype == SRNN_BF16, "pack_grads: dtype");
+    for (int t0 = 0; t0 < ntensors;) {
+        PackMulti a;
+        a.nt = 0;
+        a.boff[0] = 0;
+        int t = t0;
+        for (; t < ntensors && a.nt < PACK_MT; ++t) {
+            if (n[t] <= 0) continue;
+            const int k = a.nt++;
+            a.src[k] = src[t]; a.n[k] = n[t]; a.dst_off[k] = dst_off[t];
+            a.boff[k + 1] = a.boff[k] + (int)((n[t] + 2047) / 2048);
+        }
+        t0 = t;
+        if (a.nt == 0) continue;
+        if (dtype == SRNN_F32)
+            hipLaunchKernelGGL(pack_grads_kernel<float>, dim3((unsigned)a.boff[a.nt]), dim3(256),
+                               0, (hipStream_t)stream, a, (float*)flat);
+        else
+            hipLaunchKernelGGL(pack_grads_kernel<bf16>, dim3((unsigned)a.boff[a.nt]), dim3(256),
+                               0, (hipStream_t)stream, a, (bf16*)flat);
         SRNN_LAUNCH_CHECK();
     }
     return 0;

@@ -555,25 +555,25 @@ extern "C" int srnn_nll_bwd(const int64_t* target, int64_t ldt, int Tlen, int64_
 // per-row math lives in sampler.hpp, shared with the persistent generation loop.
 __global__ __launch_bounds__(256) void sample_kernel(
     const float* __restrict__ z, int64_t ldz, int B, const float* __restrict__ noise,
-    uint64_t seed, const int* __restrict__ base, int off, int L, int64_t* __restrict__ seq,
-    int64_t ldseq, float* __restrict__ logp_out) {
+    uint64_t seed, int row0, const int* __restrict__ base, int off, int L,
+    int64_t* __restrict__ seq, int64_t ldseq, float* __restrict__ logp_out) {
     const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (b >= B) return;
     const int i = *base + off;        // absolute sample index being generated
     const int step = i - L;
     const floatx4 v = *reinterpret_cast<const floatx4*>(z + (int64_t)b * ldz + 4 * lane);
-    const floatx4 lq = log_noise(sample_noise(noise, seed, B, b, step, lane));
+    const floatx4 lq = log_noise(sample_noise(noise, seed, B, b, step, lane, row0));
     const int bi = sample_row(v, lq, logp_out ? logp_out + ((int64_t)step * B + b) * 256 : nullptr,
                               lane);
     if (lane == 0) seq[(int64_t)b * ldseq + i] = bi;
 }
 
 int srnn_sample_impl(const float* z, int64_t ldz, int B, const float* noise, uint64_t seed,
-                     const int* base, int off, int L, int64_t* seq, int64_t ldseq,
+                     int row0, const int* base, int off, int L, int64_t* seq, int64_t ldseq,
                      float* logp_out, hipStream_t s) {
     hipLaunchKernelGGL(sample_kernel, dim3(cdiv(B, 4)), dim3(256), 0, s, z, ldz, B, noise, seed,
-                       base, off, L, seq, ldseq, logp_out);
+                       row0, base, off, L, seq, ldseq, logp_out);
     SRNN_LAUNCH_CHECK();
     return 0;
 }

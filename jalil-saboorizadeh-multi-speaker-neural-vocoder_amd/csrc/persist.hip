@@ -73,3 +73,42 @@ extern "C" int srnn_persistent_error_take(void) {
         return -1;
     return v ? 1 : 0;
 }
+
+// Stream-ordered snapshot of the flag into `dst` (pinned host memory, 4 bytes): the host
+// reads it one step later, after that copy's event, with no device synchronisation
+// (samplernn_hip.PersistentErrorWatch: the Trainer's lagged per-iteration check).
+extern "C" int srnn_persistent_flag_snapshot(int* dst, void* stream) {
+    int* f = srnn_sticky_flag();
+    SRNN_REQUIRE(f && dst, "persistent_flag_snapshot: no flag / null destination");
+    SRNN_CHECK_HIP(hipMemcpyAsync(dst, f, sizeof(int), hipMemcpyDeviceToHost,
+                                  (hipStream_t)stream));
+    return 0;
+}
+
+// dtype forms of srnn_persistent_flag_to_f32 / _or_f32 for gradient buckets in bf16
+__global__ void flag_to_bf16_kernel(const int* flag, bf16* dst) {
+    if (threadIdx.x == 0) *dst = __float2bfloat16(*flag ? 1.f : 0.f);
+}
+__global__ void flag_or_bf16_kernel(int* flag, const bf16* src) {
+    if (threadIdx.x == 0 && __bfloat162float(*src) > 0.f) *flag = 1;
+}
+
+extern "C" int srnn_persistent_flag_to(void* dst, int dtype, void* stream) {
+    if (dtype == SRNN_F32) return srnn_persistent_flag_to_f32((float*)dst, stream);
+    int* f = srnn_sticky_flag();
+    SRNN_REQUIRE(f && dst && dtype == SRNN_BF16, "persistent_flag_to: bad arguments");
+    hipLaunchKernelGGL(flag_to_bf16_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, f,
+                       (bf16*)dst);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
+extern "C" int srnn_persistent_flag_or(const void* src, int dtype, void* stream) {
+    if (dtype == SRNN_F32) return srnn_persistent_flag_or_f32((const float*)src, stream);
+    int* f = srnn_sticky_flag();
+    SRNN_REQUIRE(f && src && dtype == SRNN_BF16, "persistent_flag_or: bad arguments");
+    hipLaunchKernelGGL(flag_or_bf16_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, f,
+                       (const bf16*)src);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}

@@ -83,12 +83,15 @@ __device__ __forceinline__ float exp1_from_u32(uint32_t x) {
     return -logf(u);
 }
 
-// Exp(1) noise of lane `lane` (q = 4 lane .. 4 lane + 3) for (row b, generation step `step`)
+// Exp(1) noise of lane `lane` (q = 4 lane .. 4 lane + 3) for (row b, generation step `step`).
+// Philox counters use the GLOBAL row row0 + b: a rank generating rows [row0, row0 + B) of a
+// larger batch (rank-sharded generation) draws exactly the single-process stream.
 __device__ __forceinline__ floatx4 sample_noise(const float* noise, uint64_t seed, int B, int b,
-                                                int step, int lane) {
+                                                int step, int lane, int row0 = 0) {
     if (noise)
         return *reinterpret_cast<const floatx4*>(noise + ((int64_t)step * B + b) * 256 + 4 * lane);
-    const uint4 rnd = philox4x32(make_uint4((uint32_t)lane, (uint32_t)b, (uint32_t)step, 0u),
+    const uint4 rnd = philox4x32(make_uint4((uint32_t)lane, (uint32_t)(row0 + b), (uint32_t)step,
+                                            0u),
                                  make_uint2((uint32_t)seed, (uint32_t)(seed >> 32)));
     return floatx4{exp1_from_u32(rnd.x), exp1_from_u32(rnd.y), exp1_from_u32(rnd.z),
                    exp1_from_u32(rnd.w)};

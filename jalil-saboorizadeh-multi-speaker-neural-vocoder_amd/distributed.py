@@ -87,12 +87,35 @@ def readiness_groups(model):
     return [g for g in groups if g]
 
 
+_ALIGN = 64          # bucket offsets in elements (16-B aligned views for the fused Adam)
+
+
+def _grad_dtype(name):
+    name = (name or os.environ.get('SRNN_DP_GRAD_DTYPE', 'fp32')).lower()
+    if name in ('fp32', 'float32'):
+        return torch.float32
+    if name in ('bf16', 'bfloat16'):
+        return torch.bfloat16
+    raise ValueError('gradient bucket dtype %r (fp32 / bf16)' % name)
+
+
 class GradAllReduce:
-    """Average gradients across ranks in flat buckets of ~bucket_mb, in place.
+    """Average gradients across ranks in flat buckets of ~bucket_mb, before the clamp.
 
     Used as `gradient_clipping(..., grad_sync=GradAllReduce())`: runs after the closure's
     backward and before the clamp + Adam.  Parameters without a grad contribute zeros
     (torch-0.4 zero_grad semantics), so every rank reduces identical bucket layouts.
+
+    Device path (the fused clip+Adam, optim.py): a bucket is packed by ONE multi-tensor launch
+    (srnn_pack_grads: every gradient of the bucket into the flat buffer at 64-element-aligned
+    offsets, converted to the bucket dtype) and SUM-reduced in place; the fused Adam then
+    reads the reduced bucket through views with a 1 / world scale (srnn_adam_clip_multi2) --
+    no per-parameter copy launches, no unpack, no separate mean pass, and the local gradients
+    are released once packed.  grad_dtype 'bf16' (or env SRNN_DP_GRAD_DTYPE=bf16) halves the
+    bytes on xGMI: each rank's gradient is rounded to bf16 before the reduction (the sum of
+    N bf16 terms accumulates in bf16 inside RCCL); the default fp32 keeps the reference's
+    full-batch gradient to fp32 rounding.  Host path (CPU / non-fused optimizers): the same
+    buckets, unpacked into p.grad.
 
     overlap_groups (e.g. readiness_groups(model)): parameter groups in the order backward
     completes them.  A post-accumulate-grad hook packs a group's bucket and starts its
@@ -100,20 +123,23 @@ class GradAllReduce:
     as soon as the group's last gradient lands, so the MLP's and the bottom tier's
     reductions run under the rest of the backward; __call__ then only waits.  Groups whose
     grads never arrive this step (h0 on non-reset chunks) are reduced at the sync point.
-    The reduced values are identical to the non-overlapped path (same buckets, same sums).
     A persistent GRU sweep enqueued while reductions are in flight first makes the stream
-    wait for them (_fence): RCCL kernels and a sweep never share the CUs.
+    wait for them (_fence): RCCL kernels and a sweep never share the CUs.  close() removes the
+    hooks and the fence.
     """
 
-    def __init__(self, bucket_mb=64, group=None, overlap_groups=None):
+    def __init__(self, bucket_mb=64, group=None, overlap_groups=None, grad_dtype=None):
         self.bucket_bytes = int(bucket_mb * (1 << 20))
         self.group = group
+        self.grad_dtype = _grad_dtype(grad_dtype)
         self._bufs = {}
         self._groups = None
         self._hooks = []
         self._pending = {}
         self._fenced = set()
         self._flag_buf = None
+        self._fence_ref = None
+        self.reduced = None         # fused path: ([(param, view)], dtype, scale) of the step
         if overlap_groups is not None and dist.is_available() and dist.is_initialized() and \
                 dist.get_world_size(group) > 1:
             self._install(overlap_groups)
@@ -121,8 +147,9 @@ class GradAllReduce:
     # ---- bucketing
     def _split(self, params):
         buckets, cur, size = [], [], 0
+        es = torch.tensor([], dtype=self.grad_dtype).element_size()
         for p in params:
-            nb = p.numel() * p.element_size()
+            nb = p.numel() * es
             if cur and size + nb > self.bucket_bytes:
                 buckets.append(cur)
                 cur, size = [], 0
@@ -132,49 +159,78 @@ class GradAllReduce:
             buckets.append(cur)
         return buckets
 
-    def _flat(self, key, bucket, extra=0):
-        total = sum(p.numel() for p in bucket) + extra
-        k = (key, total, bucket[0].dtype, bucket[0].device)
+    @staticmethod
+    def _offsets(bucket):
+        offs, off = [], 0
+        for p in bucket:
+            offs.append(off)
+            off += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
+        return offs, off
+
+    def _flat(self, key, bucket, flag):
+        offs, total = self._offsets(bucket)
+        dev = bucket[0].device
+        dtype = self.grad_dtype if dev.type == 'cuda' else torch.float32
+        k = (key, flag, total, dtype, dev)
         flat = self._bufs.get(k)
         if flat is None:
-            flat = torch.empty(total, dtype=bucket[0].dtype, device=bucket[0].device)
+            flat = torch.empty(total + (_ALIGN if flag else 0), dtype=dtype, device=dev)
             self._bufs[k] = flat
-        return flat
+        return flat, offs, total
 
     def _launch(self, key, bucket, async_op, flag=False):
         """Pack a bucket and start its SUM all-reduce.  flag: the bucket carries one extra
         element, this rank's persistent-sweep failure flag (0 / 1, persist.hip), so after the
         reduction every rank holds the same verdict."""
-        flat = self._flat((key, flag), bucket, 1 if flag else 0)
-        off = 0
-        for p in bucket:
-            k = p.numel()
-            if p.grad is None:
-                flat[off:off + k].zero_()
-            else:
-                flat[off:off + k].copy_(p.grad.reshape(-1))
-            off += k
-        if flag:
-            _flag_to(flat[off:])
+        flat, offs, total = self._flat(key, bucket, flag)
+        if flat.is_cuda:
+            import ctypes
+            import samplernn_hip as H
+            n = len(bucket)
+            srcs = []
+            for p in bucket:
+                g = p.grad
+                if g is not None and (g.dtype != torch.float32 or not g.is_contiguous()):
+                    g = g.float().contiguous()
+                    p.grad = g
+                srcs.append(g)
+            H.lib().call('srnn_pack_grads', n,
+                         (ctypes.c_void_p * n)(*[H.ptr(g) for g in srcs]),
+                         (ctypes.c_int64 * n)(*[p.numel() for p in bucket]),
+                         (ctypes.c_int64 * n)(*offs), H.ptr(flat), H.dcode(flat), H.stream())
+            if flag:
+                _flag_to(flat[total:total + 1])
+        else:
+            flat.zero_()
+            for p, o in zip(bucket, offs):
+                if p.grad is not None:
+                    flat[o:o + p.numel()].copy_(p.grad.reshape(-1))
         work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
-        return flat, work
+        return (flat, offs, total), work
 
-    def _unpack(self, bucket, flat, n):
+    def _finish(self, bucket, rec, n, fused, views):
+        flat, offs, total = rec
+        if flat.numel() > total:        # the carried failure flag: any rank's -> this rank's
+            _flag_from(flat[total:total + 1])
+        if fused:
+            for p, o in zip(bucket, offs):
+                views.append((p, flat[o:o + p.numel()].view(p.shape)))
+                p.grad = None           # the local gradient was packed: release it
+            return
         flat.mul_(1.0 / n)
-        off = 0
-        for p in bucket:
-            k = p.numel()
+        for p, o in zip(bucket, offs):
+            v = flat[o:o + p.numel()].view(p.shape)
             if p.grad is None:
                 p.grad = torch.zeros_like(p)
-            p.grad.copy_(flat[off:off + k].view_as(p.grad))
-            off += k
-        if flat.numel() > off:          # the carried failure flag: any rank's -> this rank's
-            _flag_from(flat[off:])
+            p.grad.copy_(v)
 
     # ---- overlapped mode
     def _install(self, groups):
+        import weakref
         import samplernn_hip as H
-        H.BEFORE_PERSISTENT.append(self._fence)
+        ref = weakref.WeakMethod(self._fence)
+        self._fence_ref = ref
+        H.BEFORE_PERSISTENT.append(ref)
         self._groups = []
         for gi, params in enumerate(groups):
             for bi, bucket in enumerate(self._split(params)):
@@ -184,15 +240,34 @@ class GradAllReduce:
             for p in bucket:
                 self._owner[id(p)] = idx
         self._ready = [0] * len(self._groups)
+        # the hooks hold this object weakly: parameters outlive a GradAllReduce that is dropped
+        me = weakref.ref(self)
+
+        def hook(p):
+            s = me()
+            if s is not None:
+                s._on_grad(p)
         for idx, (_, bucket) in enumerate(self._groups):
             for p in bucket:
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+                self._hooks.append(p.register_post_accumulate_grad_hook(hook))
+
+    def close(self):
+        """Remove the gradient hooks and the persistent-sweep fence (and drop the buckets)."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        if self._fence_ref is not None:
+            import samplernn_hip as H
+            H.BEFORE_PERSISTENT[:] = [f for f in H.BEFORE_PERSISTENT if f is not self._fence_ref]
+            self._fence_ref = None
+        self._bufs = {}
+        self._groups = None
 
     def _fence(self):
         """Before a persistent GRU sweep: the current stream waits for every all-reduce in
         flight (a stream-level wait under RCCL, no host synchronisation), so the sweep never
         shares the CUs with RCCL kernels (samplernn_hip.BEFORE_PERSISTENT)."""
-        for idx, (flat, work) in self._pending.items():
+        for idx, (rec, work) in self._pending.items():
             if idx not in self._fenced:
                 work.wait()
                 self._fenced.add(idx)
@@ -204,10 +279,15 @@ class GradAllReduce:
         if self._ready[idx] == len(bucket) and idx not in self._pending:
             self._pending[idx] = self._launch(key, bucket, True)
 
-    def __call__(self, optimizer):
+    def __call__(self, optimizer, fused=False):
+        """Reduce this step's gradients.  fused=True (the device clip+Adam): leave them in the
+        buckets and publish (param, view) pairs, the dtype and the 1 / world scale in
+        self.reduced; otherwise write the means back into p.grad."""
+        self.reduced = None
         if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
             return
         n = dist.get_world_size(self.group)
+        views = []
         if self._groups is not None:
             # every backward kernel is enqueued by now, so the failure flag read here covers
             # all persistent sweeps of the step: it rides in the last bucket launched here, or
@@ -226,35 +306,52 @@ class GradAllReduce:
                 solo = dist.all_reduce(self._flag_buf, op=dist.ReduceOp.SUM, group=self.group,
                                        async_op=True)
             for idx, (key, bucket) in enumerate(self._groups):
-                flat, work = self._pending[idx]
+                rec, work = self._pending[idx]
                 work.wait()
-                self._unpack(bucket, flat, n)
+                self._finish(bucket, rec, n, fused and dev, views)
             if solo is not None:
                 solo.wait()
                 _flag_from(self._flag_buf)
             self._pending = {}
             self._fenced = set()
             self._ready = [0] * len(self._groups)
-            return
-        params = [p for g in optimizer.param_groups for p in g['params'] if p.requires_grad]
-        buckets = self._split(params)
-        for bi, bucket in enumerate(buckets):
-            flat, _ = self._launch(bi, bucket, False,
-                                   flag=bucket[0].is_cuda and bi == len(buckets) - 1)
-            self._unpack(bucket, flat, n)
+        else:
+            params = [p for g in optimizer.param_groups for p in g['params'] if p.requires_grad]
+            buckets = self._split(params)
+            for bi, bucket in enumerate(buckets):
+                dev = bucket[0].is_cuda
+                rec, _ = self._launch(bi, bucket, False, flag=dev and bi == len(buckets) - 1)
+                self._finish(bucket, rec, n, fused and dev, views)
+        if views:
+            self.reduced = (views, views[0][1].dtype, 1.0 / n)
 
 
 def _flag_to(dst):
-    """dst (1-element fp32 device tensor) = this rank's persistent-sweep failure flag."""
+    """dst (1-element fp32 / bf16 device tensor) = this rank's persistent-sweep failure flag."""
     import samplernn_hip as H
-    H.lib().call('srnn_persistent_flag_to_f32', H.ptr(dst), H.stream())
+    H.lib().call('srnn_persistent_flag_to', H.ptr(dst), H.dcode(dst), H.stream())
 
 
 def _flag_from(src):
     """Raise this rank's failure flag if the reduced value says any rank failed: the fused
     clip+Adam then skips the update on every rank and every rank's Trainer raises."""
     import samplernn_hip as H
-    H.lib().call('srnn_persistent_flag_or_f32', H.ptr(src), H.stream())
+    H.lib().call('srnn_persistent_flag_or', H.ptr(src), H.dcode(src), H.stream())
+
+
+def gather_rows(local, total_rows):
+    """Concatenate every rank's contiguous row shard (host tensor (rows, ...)) in rank order;
+    identity for one process.  Over the process group's backend: RCCL (device tensors) under
+    nccl, the host under gloo."""
+    if not _active():
+        return local
+    dev = _coll_device()
+    t = local.to(dev).contiguous()
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    out = torch.cat(parts, 0).cpu()
+    assert out.shape[0] == total_rows
+    return out
 
 
 def barrier():

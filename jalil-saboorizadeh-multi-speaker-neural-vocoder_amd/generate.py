@@ -26,7 +26,7 @@ import numpy as np
 import torch
 
 from dataset import read_conditioners, write_wav
-from model import Generator, Predictor, SampleRNN
+from model import Generator, Predictor, SampleRNN, shard_generate
 
 default_params = {
     # model parameters
@@ -134,7 +134,12 @@ def build_model(params, spk_dim, use_cuda):
 
 
 def main(frame_sizes, **params):
+    import distributed as Dd
+    Dd.init()                   # torchrun: one process per GPU (no-op for a single process)
     use_cuda = torch.cuda.is_available()
+    if use_cuda:
+        torch.cuda.set_device(Dd.device_index())
+    rank, world = Dd.rank(), Dd.world()
     params = dict(default_params, frame_sizes=frame_sizes, **params)
     # parameters encoded in the experiment directory name (generate.py:122-126)
     parts = params['model'].split('/')
@@ -171,15 +176,27 @@ def main(frame_sizes, **params):
             rows[j * n:(j + 1) * n, :c.shape[0]] = c
             spks[j * n:(j + 1) * n] = jobs[j][1]
         gen = Generator(model, use_cuda)
-        out = gen(len(rows), params['sample_length'], rows, spks, sampler=params['sampler'],
-                  seed=params['seed']).numpy()
+        if world > 1:
+            # rank-sharded: contiguous row shards, Philox noise of the global
+            # rows, gathered at the end (rows padded to a multiple of the world size)
+            pad = (-len(rows)) % world
+            prow = np.concatenate([rows, np.zeros((pad,) + rows.shape[1:], rows.dtype)])
+            pspk = np.concatenate([spks, np.zeros(pad, spks.dtype)])
+            out = shard_generate(gen, len(prow), prow, pspk, params['seed']).numpy()[:len(rows)]
+        else:
+            out = gen(len(rows), params['sample_length'], rows, spks, sampler=params['sampler'],
+                      seed=params['seed']).numpy()
+        if rank != 0:
+            return
         L = model.lookback
         for j, (stem, sp, original) in enumerate(jobs):
             fname = output_name(params['model'], original, str(spk[sp]))
             for i in range(n):
                 write_wav(fname, out[j * n + i, :conds[j].shape[0] * L], sr=params['sample_rate'])
         return
-    for stem, speaker, original in jobs:
+    for j, (stem, speaker, original) in enumerate(jobs):
+        if j % world != rank:       # files are independent: round-robin over the ranks
+            continue
         cond = file_conditioning(stem, speaker, params)
         init_random_seed(params['seed'], use_cuda)
         model = build_model(params, spk_dim, use_cuda)

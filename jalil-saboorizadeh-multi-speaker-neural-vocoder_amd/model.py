@@ -286,10 +286,12 @@ class _TierFn(torch.autograd.Function):
                 work = torch.empty(xw, device=dev, dtype=torch.uint8)
                 hprevT = torch.empty((B, Fr, D), device=dev, dtype=T)
                 _STATS['gru_xcd_fwd'] += 1
+                ev = H.roof_begin()
                 H.lib().call('srnn_gru_xcd_fwd2', H.dcode(T), B, D, Fr, H.ptr(gi), Fr * 3 * D,
                              3 * D, H.ptr(hpf), H.ptr(Whh[l]), H.ptr(b_hh), H.ptr(out),
                              H.ptr(outT), Fr * D, D, H.ptr(gt), Fr * 4 * D, 4 * D,
                              H.ptr(hprevT), H.ptr(work), xw, H.stream())
+                H.roof_end('gru_xcd_fwd', ev, 2.0 * B * Fr * 3 * D * D)
             elif seq:
                 # whole sequence in one persistent launch (W_hh resident in LDS)
                 work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
@@ -408,11 +410,14 @@ class _TierFn(torch.autograd.Function):
                 work = torch.empty(xbw, device=dev, dtype=torch.uint8)
                 dOutc = dOut.contiguous()
                 _STATS['gru_xcd_bwd'] += 1
+                ev = H.roof_begin()
                 H.lib().call('srnn_gru_xcd_bwd2', H.dcode(T), B, D, Fr, H.ptr(dOutc), Fr * D, D,
                              H.ptr(gates[l]), Fr * 4 * D, 4 * D, H.ptr(outs[l]), Fr * D, D,
                              H.ptr(h_in[l]), H.ptr(WhhT), None, H.ptr(dGHT), None, H.ptr(dGIT),
                              H.ptr(bsum), Fr * 3 * D, 3 * D, H.ptr(ddir[0]), H.ptr(work), xbw,
                              st())
+                # (the dgh_{t+1} W_hh products of steps 1 .. F-1; step F-1 has none)
+                H.roof_end('gru_xcd_bwd', ev, 2.0 * B * (Fr - 1) * 3 * D * D)
             elif seq:
                 # the whole reverse sweep in one persistent launch (W_hh^T resident in LDS)
                 work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
@@ -585,14 +590,9 @@ class _MlpFn(torch.autograd.Function):
                          H.dcode(upper), H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
         W_hid = _wcast(mlp.hidden, T).reshape(D, D)
         W_out = _wcast(mlp.output, T).reshape(Q, D)
-        probe = H.ROOF_EVENTS
-        if probe is not None:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record()
+        ev = H.roof_begin()
         a2 = H.linear(a1, W_hid, bias=mlp.hidden.bias, relu=True, out_dtype=T, bits_out=m2)
-        if probe is not None:
-            ev[1].record()
-            probe.append(ev)
+        H.roof_end('mlp_hidden_gemm', ev, 2.0 * B * Tl * D * D)
         z = H.linear(a2, W_out, bias=mlp.output.bias)                    # (B*T, Q) fp32
         logp = torch.empty((B * Tl, Q), device=dev, dtype=torch.float32)
         H.lib().call('srnn_logsoftmax_nll', H.ptr(z), Q, None, 0, Tl, B * Tl, Q, None,
@@ -640,9 +640,14 @@ class _MlpFn(torch.autograd.Function):
         # gradient (its output is this layer's `upper`), handed over on the returned gradient
         colsum = torch.empty(FS0 * D, device=dev, dtype=torch.float32)
         done = ctypes.c_int(0)
+        ev = H.roof_begin()
         H.lib().call('srnn_mlp_dtab2', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.stride(0), 0, B,
                      Tl, H.ptr(dtabT), H.dcode(T), D, FS0, Q, H.ptr(work), work.numel() * 8,
                      H.ptr(colsum), ctypes.byref(done), st())
+        # algorithmic bytes: da1 and the index window read once, dTab^T and the column sums
+        # written once
+        H.roof_end('dtab_scatter', ev, B * Tl * D * da1.element_size() +
+                   B * (Tl + FS0 - 1) * 8 + Q * FS0 * D * dtabT.element_size() + FS0 * D * 4)
         dE = H.gemm(dtabT, Wp.reshape(FS0 * D, Q))                       # (Q, Q)
         # dWp[k] = dTab[:, k]^T E for every tap k at once: (FS0 D, Q) = dtabT^T . ET, one GEMM
         # (the (FS0, D, Q) result is the same memory as the per-tap batch)
@@ -816,7 +821,10 @@ class Generator(Runner):
         self.last_sequences = None
 
     def __call__(self, n_seqs, seq_len, cond, spk, sampler='torch', seed=0, noise=None,
-                 return_logp=False, use_graph=True, dtype=None, persistent=True):
+                 return_logp=False, use_graph=True, dtype=None, persistent=True, row_offset=0):
+        """row_offset: these n_seqs rows are rows [row_offset, row_offset + n_seqs) of a larger
+        batch (rank-sharded generation, see shard_generate): the Philox noise (sampler='philox')
+        is that of the global rows, so shards reproduce the single-process stream."""
         model = self.model
         self.reset_hidden_states()
         dev = next(model.parameters()).device
@@ -845,9 +853,9 @@ class Generator(Runner):
         sz = ctypes.c_size_t(0)
         H.lib().call('srnn_gen_workspace_size', ctypes.byref(m), n_seqs, ctypes.byref(sz))
         ws = torch.empty(sz.value, device=dev, dtype=torch.uint8)
-        H.lib().call('srnn_generate', ctypes.byref(m), n_seqs, num_cond, H.ptr(cond),
-                     H.ptr(row_bias), H.ptr(noise), int(seed) & ((1 << 64) - 1), H.ptr(seq),
-                     H.ptr(logp), H.ptr(ws), sz.value,
+        H.lib().call('srnn_generate2', ctypes.byref(m), n_seqs, num_cond, H.ptr(cond),
+                     H.ptr(row_bias), H.ptr(noise), int(seed) & ((1 << 64) - 1),
+                     int(row_offset), H.ptr(seq), H.ptr(logp), H.ptr(ws), sz.value,
                      (1 if use_graph else 0) | (0 if persistent else 2), H.stream())
         del keep
         self.last_sequences = seq
@@ -855,3 +863,25 @@ class Generator(Runner):
         if return_logp:
             return out, logp.permute(1, 0, 2).contiguous()
         return out
+
+
+def shard_generate(generator, n_seqs, cond, spk, seed, rank=None, world=None, **kw):
+    """Rank-sharded generation (the reference runs generate.py:241-253 per file on
+    one device): rank r generates the contiguous rows [r n / N, (r + 1) n / N) of an n_seqs batch
+    with replicated weights and no collective in the loop (Philox noise of the GLOBAL rows, so
+    the union equals the single-process output); the dequantized rows are gathered to every
+    rank at the end.  cond: (num_cond, C) shared or (n_seqs, num_cond, C) per row; spk: int or
+    (n_seqs,).  Returns the host float32 (n_seqs, num_cond * lookback) batch."""
+    import distributed as Dd
+    rank = Dd.rank() if rank is None else rank
+    world = Dd.world() if world is None else world
+    rows = Dd.shard_rows(n_seqs, rank, world)
+    c = torch.as_tensor(np.asarray(cond) if not torch.is_tensor(cond) else cond)
+    if c.dim() == 3:
+        c = c[rows]
+    s = torch.as_tensor(np.asarray(spk) if not torch.is_tensor(spk) else spk).reshape(-1)
+    if s.numel() > 1:
+        s = s[rows]
+    out = generator(rows.stop - rows.start, 0, c, s, sampler='philox', seed=seed,
+                    row_offset=rows.start, **kw)
+    return Dd.gather_rows(out, n_seqs)

@@ -15,10 +15,15 @@ import torch
 import samplernn_hip as H
 
 
-def _fused_adam_step(optimizer, lo, hi):
+def _fused_adam_step(optimizer, lo, hi, reduced=None):
     """All parameters of a group that share a step count go through ONE multi-tensor
-    launch (srnn_adam_clip_multi) instead of one launch per tensor."""
+    launch (srnn_adam_clip_multi2) instead of one launch per tensor.  reduced: the data-
+    parallel gradient buckets ((param, view) pairs, dtype, 1 / world scale; distributed.py)
+    read in place instead of p.grad."""
     import ctypes
+    rv = {id(p): v for p, v in reduced[0]} if reduced else None
+    gdt = reduced[1] if reduced else torch.float32
+    gscale = reduced[2] if reduced else 1.0
     for group in optimizer.param_groups:
         if group.get('weight_decay', 0) != 0 or group.get('amsgrad', False) or \
                 group.get('maximize', False):
@@ -34,8 +39,8 @@ def _fused_adam_step(optimizer, lo, hi):
                 st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
             # a None grad goes to the kernel as NULL = all-zero (no zero-fill launch)
-            if p.grad is not None and (not p.grad.is_contiguous() or
-                                       p.grad.dtype != torch.float32):
+            if rv is None and p.grad is not None and (not p.grad.is_contiguous() or
+                                                      p.grad.dtype != torch.float32):
                 p.grad = p.grad.float().contiguous()
             if not (p.is_contiguous() and p.dtype == torch.float32):
                 raise NotImplementedError('fused clip+Adam: contiguous fp32 parameters only')
@@ -48,13 +53,20 @@ def _fused_adam_step(optimizer, lo, hi):
             # parameters with a cached bf16 copy (samplernn_hip.cast_param) get it rewritten
             # by the same kernel, so the next forward needs no cast
             shadows = [H.shadow_of(p) for p, _ in items]
-            H.lib().call('srnn_adam_clip_multi', n, arr([p for p, _ in items]),
-                         arr([p.grad for p, _ in items]), arr([s['exp_avg'] for _, s in items]),
+            ev = H.roof_begin()
+            nel = sum(p.numel() for p, _ in items)
+            grads = [p.grad for p, _ in items] if rv is None else [rv.get(id(p)) for p, _ in items]
+            H.lib().call('srnn_adam_clip_multi2', n, arr([p for p, _ in items]), arr(grads),
+                         H.dcode(gdt), float(gscale), arr([s['exp_avg'] for _, s in items]),
                          arr([s['exp_avg_sq'] for _, s in items]),
                          arr(shadows) if any(t is not None for t in shadows) else None,
                          (ctypes.c_int64 * n)(*[p.numel() for p, _ in items]), float(lo),
                          float(hi), float(group['lr']), float(b1), float(b2),
                          float(group['eps']), step, H.stream())
+            # algorithmic bytes: p, m, v read + written, the gradient read + written back
+            # clamped (hardtanh_ in place, optim.py:13), the bf16 copies written
+            H.roof_end('adam_clip', ev, nel * 32 + 2 * sum(
+                p.numel() for (p, _), sh in zip(items, shadows) if sh is not None))
 
 
 def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
@@ -80,10 +92,15 @@ def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
             if self._fused():
                 with torch.enable_grad():
                     loss = closure()
+                reduced = None
                 if self.grad_sync is not None:
-                    self.grad_sync(optimizer)
+                    if hasattr(self.grad_sync, 'reduced'):      # distributed.GradAllReduce
+                        self.grad_sync(optimizer, fused=True)
+                        reduced = self.grad_sync.reduced
+                    else:
+                        self.grad_sync(optimizer)
                 with torch.no_grad():
-                    _fused_adam_step(optimizer, min, max)
+                    _fused_adam_step(optimizer, min, max, reduced)
                 return loss
 
             def closure_wrapper():
@@ -98,6 +115,16 @@ def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
                 return loss
 
             return optimizer.step(closure_wrapper)
+
+        def rollback_steps(self, k):
+            """Undo the Adam step-count increments of k steps whose update the device skipped
+            (a persistent sweep gave up a hand-off, samplernn_hip.PersistentErrorWatch): the
+            bias correction then matches the k fewer updates the moments hold."""
+            for group in optimizer.param_groups:
+                for p in group['params']:
+                    st = optimizer.state.get(p)
+                    if st and 'step' in st:
+                        st['step'] -= k
 
         def __getattr__(self, attr):
             return getattr(optimizer, attr)

@@ -9,6 +9,7 @@ import ctypes
 import sys
 import time
 import os
+import weakref
 
 import torch
 
@@ -82,8 +83,15 @@ _SIGS = {
     'srnn_convt_wn_bwd': [_P, _P, _P, _P, _P, _I, _I, _I, _P],
     'srnn_gen_workspace_size': [_P, _I, ctypes.POINTER(_SZ)],
     'srnn_generate': [_P, _I, _I, _P, _P, _P, _U64, _P, _P, _P, _SZ, _I, _P],
+    'srnn_generate2': [_P, _I, _I, _P, _P, _P, _U64, _I, _P, _P, _P, _SZ, _I, _P],
     'srnn_persistent_flag_to_f32': [_P, _P],
     'srnn_persistent_flag_or_f32': [_P, _P],
+    'srnn_persistent_flag_snapshot': [_P, _P],
+    'srnn_persistent_flag_to': [_P, _I, _P],
+    'srnn_persistent_flag_or': [_P, _I, _P],
+    'srnn_adam_clip_multi2': [_I, _P, _P, _I, _F, _P, _P, _P, _P, _F, _F, _D, _D, _D, _D, _L,
+                              _P],
+    'srnn_pack_grads': [_I, _P, _P, _P, _P, _I, _P],
 }
 
 
@@ -170,15 +178,46 @@ def exported_symbols():
 # the current stream wait for every gradient all-reduce already in flight.
 BEFORE_PERSISTENT = []
 
-# Measurement hook (bench.py): when a list, the sample-level MLP's hidden-layer GEMM -- the
-# bench's roofline kernel -- is bracketed by HIP events on its stream at every launch and the
-# (start, end) pairs are appended, so its duration is measured inside the timed TBPTT steps
+# Measurement hook (bench.py): when a dict, the step's heaviest launch sites (the GRU sweeps,
+# the dTab scatter, the MLP hidden-layer GEMM, the fused clip+Adam, ...) are bracketed by HIP
+# events on the stream they launch on, and site -> [(start, end, work)] collects them, so
+# their durations are measured inside the timed TBPTT steps (work = the launch's algorithmic
+# flop or bytes)
 ROOF_EVENTS = None
 
 
+def roof_begin():
+    """Start event of a probed launch site (None when probing is off)."""
+    if ROOF_EVENTS is None:
+        return None
+    ev = torch.cuda.Event(enable_timing=True)
+    ev.record()
+    return ev
+
+
+def roof_end(site, ev0, work):
+    if ev0 is None or ROOF_EVENTS is None:
+        return
+    ev1 = torch.cuda.Event(enable_timing=True)
+    ev1.record()
+    ROOF_EVENTS.setdefault(site, []).append((ev0, ev1, float(work)))
+
+
 def before_persistent_sweep():
+    """Run the registered callbacks (plain callables or weakref.WeakMethod references, whose
+    dead entries -- a GradAllReduce that is gone -- are dropped)."""
+    dead = []
     for f in BEFORE_PERSISTENT:
-        f()
+        if isinstance(f, weakref.WeakMethod):
+            m = f()
+            if m is None:
+                dead.append(f)
+                continue
+            m()
+        else:
+            f()
+    for f in dead:
+        BEFORE_PERSISTENT.remove(f)
 
 
 def check_persistent_errors():
@@ -193,6 +232,55 @@ def check_persistent_errors():
         raise RuntimeError('persistent GRU sweep gave up a hand-off (bounded spin) -- results of '
                            'this step are invalid' if v > 0 else
                            'srnn_persistent_error_take: HIP error')
+
+
+class PersistentErrorWatch:
+    """Lagged, synchronisation-free form of check_persistent_errors for the training loop
+    (trainer/__init__.py:116-117 checks once per iteration): after step n is enqueued a 4-byte
+    stream-ordered copy of the sticky flag goes to pinned host memory, and the copy of step
+    n - 1 is read -- waiting only on that copy's event, which the GPU has normally passed
+    while it runs step n.  The flag is sticky, so a failure in step n - 1 also made step n's
+    fused clip+Adam skip its update: `step()` then reports 2 skipped steps (the caller rolls
+    the Adam step counters back, optim.py) and raises.  flush() checks the last step with a
+    synchronisation (epoch end)."""
+
+    def __init__(self):
+        self._bufs = [torch.zeros(1, dtype=torch.int32).pin_memory() for _ in range(2)]
+        self._events = [None, None]
+        self._n = 0
+
+    def _snapshot(self):
+        slot = self._n % 2
+        lib().call('srnn_persistent_flag_snapshot', ptr(self._bufs[slot]), stream())
+        ev = torch.cuda.Event()
+        ev.record()
+        self._events[slot] = ev
+        self._n += 1
+
+    def _read(self, slot):
+        ev = self._events[slot]
+        if ev is None:
+            return 0
+        ev.synchronize()
+        self._events[slot] = None
+        return int(self._bufs[slot][0])
+
+    def step(self, on_skip=None):
+        """Call once per enqueued training step."""
+        self._snapshot()
+        if self._n >= 2 and self._read((self._n - 2) % 2):
+            self._fail(on_skip, 2)
+
+    def flush(self, on_skip=None):
+        if self._n and self._read((self._n - 1) % 2):
+            self._fail(on_skip, 1)
+
+    def _fail(self, on_skip, skipped):
+        for s in range(2):
+            self._events[s] = None
+        if on_skip is not None:
+            on_skip(skipped)
+        check_persistent_errors()       # synchronises, clears the flag and raises
 
 
 _GRU_XCD = {}
@@ -393,13 +481,15 @@ def cast_param(p, dtype):
     that becomes the cached copy."""
     if p.dtype == dtype:
         return p
-    import weakref
     key = id(p)
     e = _SHADOW.get(key)
     if e is not None and e[0]() is p and e[1].dtype == dtype and e[2] == p.data_ptr() and \
             e[3] == p._version:
         return e[1]
     c = cast(p.detach(), dtype)
+    if e is None or e[0]() is not p:
+        # evict the copy with its parameter (no bf16 copies of dead parameters stay allocated)
+        weakref.finalize(p, _SHADOW.pop, key, None)
     _SHADOW[key] = (weakref.ref(p), c, p.data_ptr(), p._version)
     return c
 

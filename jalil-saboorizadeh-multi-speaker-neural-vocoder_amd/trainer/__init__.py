@@ -6,8 +6,14 @@ TBPTT step itself is unchanged in structure -- reset flag, device copies, closur
 (forward, criterion, backward), optimizer.step(closure) -- and runs on the HIP model.
 zero_grad keeps torch-0.4 semantics (grads zero-filled, never None) so the reference's
 gradient_clipping never meets a None grad.
+
+The per-iteration check of the persistent sweeps' failure flag is lagged by one step and
+needs no device synchronisation (samplernn_hip.PersistentErrorWatch): the host keeps
+enqueuing while the GPU runs; a failure raises one iteration later (or at the epoch's end),
+after the Adam step counters of the skipped updates are rolled back.
 """
 import heapq
+import time
 
 import torch
 
@@ -33,6 +39,8 @@ class Trainer(object):
             'update': [],
         }
         self.writer = writer
+        self._watch = None
+        self.enqueue_s = 0.0        # host seconds spent enqueuing steps (bench.py)
 
     def register_plugin(self, plugin):
         plugin.register(self)
@@ -75,8 +83,16 @@ class Trainer(object):
         except TypeError:
             self.optimizer.zero_grad()
 
+    def _rollback(self, k):
+        fn = getattr(self.optimizer, 'rollback_steps', None)
+        if fn is not None:
+            fn(k)
+
     def train(self):
+        if self.cuda and self._watch is None:
+            self._watch = H.PersistentErrorWatch()
         for (self.iterations, data) in enumerate(self.dataset, self.iterations + 1):
+            t_enq = time.perf_counter()
             inputs = data[0]
             reset = data[1]
             batch_target = data[2]
@@ -113,8 +129,11 @@ class Trainer(object):
 
             self._zero_grad()
             self.optimizer.step(closure)
+            self.enqueue_s += time.perf_counter() - t_enq
             if self.cuda:
-                H.check_persistent_errors()
+                self._watch.step(self._rollback)
             self.call_plugins('iteration', self.iterations, batch_inputs, batch_target,
                               *plugin_data)
             self.call_plugins('update', self.iterations, self.model)
+        if self.cuda:
+            self._watch.flush(self._rollback)

@@ -214,8 +214,28 @@ class ValidationPlugin(Plugin):
         # under data parallelism each rank saw its row shard: sum (loss, rows) over ranks so
         # every rank -- and SaverPlugin's best-checkpoint choice -- sees the full-batch value
         import distributed
-        loss_sum, n_examples = distributed.sum_over_ranks([loss_sum, n_examples])
+        # a persistent sweep that gave up a hand-off during evaluation makes the loss invalid:
+        # its flag is summed with the loss over ranks, so every rank raises before the value
+        # is logged or SaverPlugin picks a checkpoint by it
+        flag = _persistent_flag() if self.trainer.cuda else 0.0
+        loss_sum, n_examples, flag = distributed.sum_over_ranks([loss_sum, n_examples, flag])
+        if flag > 0:
+            import samplernn_hip as H
+            try:
+                H.check_persistent_errors()          # clears this rank's flag
+            except RuntimeError:
+                pass
+            raise RuntimeError('persistent GRU sweep gave up a hand-off during evaluation -- '
+                               'the evaluation loss is invalid')
         return loss_sum / n_examples if n_examples else float('nan')
+
+
+def _persistent_flag():
+    """This rank's persistent-sweep failure flag as 0.0 / 1.0 (synchronises)."""
+    import samplernn_hip as H
+    t = torch.zeros(1, device='cuda')
+    H.lib().call('srnn_persistent_flag_to_f32', H.ptr(t), H.stream())
+    return float(t.item())
 
 
 class AbsoluteTimeMonitor(Monitor):

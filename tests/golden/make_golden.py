@@ -283,7 +283,37 @@ def generation_goldens(name, n_seqs, num_cond, seed, gen_seed):
     print('gen %s: T=%d n_seqs=%d min relative margin %.3g' % (name, T, n_seqs, margin))
     save('gen_' + name, cond=cond, spk=np.array(spk), n_seqs=np.array(n_seqs),
          weight_seed=np.array(seed), noise=q, idx=idx.astype(np.int64), samples=samples,
-         logp=logp, margin=np.array(margin))
+         logp=logp, margin=np.array(margin), gen_seed=np.array(gen_seed))
+
+
+def generation_seed_goldens(name, n_seqs, num_cond, seed, gen_seed):
+    """The default sampling path from a seed, as generate.py runs it (generate.py:200-235:
+    init_random_seed BEFORE the model is built, then load_state_dict, then the Generator):
+    torch.manual_seed(gen_seed) -> SampleRNN(...) (init consumes the RNG) -> weights loaded ->
+    Generator(n_seqs, 0, cond, spk) drawing its multinomials from the same generator.  Stores
+    the seed and the produced samples; the build's test repeats the sequence with its own
+    SampleRNN (same init RNG order, a13) and the default sampler='torch'."""
+    cfg = recipe.CONFIGS[name]
+    w = recipe.make_weights(cfg, seed)
+    cond = recipe.synth_cond((num_cond, cfg['cond_dim']), seed + 3)
+    spk = 2 % cfg['spk_dim']
+    torch.manual_seed(gen_seed)
+    m, _ = build_ref(cfg, w)
+    gen = ref_model.Generator(m, False)
+    devnull = open(os.devnull, 'w')
+    so = sys.stdout
+    sys.stdout = devnull
+    try:
+        with torch.no_grad():
+            samples = gen(n_seqs, 0, cond, spk).numpy()
+    finally:
+        sys.stdout = so
+    lut = ref_utils.udequantize(torch.arange(cfg['q_levels']), cfg['q_levels']).numpy()
+    idx = np.searchsorted(lut, samples).astype(np.int64)
+    assert np.array_equal(lut[idx], samples)
+    print('gen-from-seed %s: T=%d n_seqs=%d' % (name, samples.shape[1], n_seqs))
+    save('genseed_' + name, cond=cond, spk=np.array(spk), n_seqs=np.array(n_seqs),
+         weight_seed=np.array(seed), gen_seed=np.array(gen_seed), idx=idx, samples=samples)
 
 
 class _RowwisePredictor(torch.nn.Module):
@@ -419,6 +449,13 @@ def main():
         generation_goldens('t4la', n_seqs=2, num_cond=2, seed=23, gen_seed=7)
         generation_goldens('t3_20_4', n_seqs=2, num_cond=3, seed=24, gen_seed=8)
         generation_goldens('t3r2wn', n_seqs=2, num_cond=2, seed=25, gen_seed=9)
+    if want('genbig'):
+        # configs[2]'s model (3-tier, dim 1024, FS [16, 4], cond 43, 6 speakers): 2 rows x 2
+        # top-tier frames = 128 samples (8 bottom ticks, 2 top ticks)
+        generation_goldens('big', n_seqs=2, num_cond=2, seed=26, gen_seed=10)
+    if want('genseed'):
+        generation_seed_goldens('t3', n_seqs=3, num_cond=2, seed=27, gen_seed=11)
+        generation_seed_goldens('big', n_seqs=2, num_cond=1, seed=28, gen_seed=12)
     if want('tbptt'):
         tbptt_goldens('t3', B=2, T=128, n_steps=3, seed=31)
         tbptt_goldens('t3r2wn', B=2, T=64, n_steps=3, seed=32)

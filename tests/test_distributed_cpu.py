@@ -173,3 +173,47 @@ def test_dp_plugins_report_full_batch_losses():
     for _, val, tl in got:
         assert abs(val - full) < 1e-9
         assert abs(tl - full) < 1e-6
+
+
+class _Work:
+    def __init__(self):
+        self.waits = 0
+
+    def wait(self):
+        self.waits += 1
+
+
+def test_fence_waits_every_pending_reduction_and_unregisters():
+    """GradAllReduce._fence (registered in samplernn_hip.BEFORE_PERSISTENT through a weak
+    reference) makes a persistent sweep wait for EVERY all-reduce in flight, once each; close()
+    and garbage collection both take it off the list (no stale fences or buckets pile up)."""
+    import gc
+    import distributed as D
+    import samplernn_hip as H
+    before = list(H.BEFORE_PERSISTENT)
+    sync = D.GradAllReduce(bucket_mb=1)
+    sync._install([[torch.nn.Parameter(torch.zeros(3))], [torch.nn.Parameter(torch.zeros(2))]])
+    assert len(H.BEFORE_PERSISTENT) == len(before) + 1
+    w = [_Work(), _Work(), _Work()]
+    sync._pending = {0: (None, w[0]), 1: (None, w[1])}
+    H.before_persistent_sweep()
+    assert [x.waits for x in w] == [1, 1, 0]
+    sync._pending[2] = (None, w[2])
+    H.before_persistent_sweep()                  # only the newly launched one is waited for
+    assert [x.waits for x in w] == [1, 1, 1]
+    sync.close()
+    assert H.BEFORE_PERSISTENT == before
+    sync2 = D.GradAllReduce(bucket_mb=1)
+    sync2._install([[torch.nn.Parameter(torch.zeros(3))]])
+    assert len(H.BEFORE_PERSISTENT) == len(before) + 1
+    del sync2
+    gc.collect()
+    H.before_persistent_sweep()                  # the dead entry is dropped
+    assert H.BEFORE_PERSISTENT == before
+
+
+def test_bucket_offsets_aligned():
+    import distributed as D
+    ps = [torch.nn.Parameter(torch.zeros(n)) for n in (3, 64, 65, 1)]
+    offs, total = D.GradAllReduce._offsets(ps)
+    assert offs == [0, 64, 128, 256] and total == 320

@@ -76,6 +76,47 @@ def test_persistent_bf16_d1024(hip, B):
     assert err.mean().item() < 0.02, err.mean().item()
 
 
+def test_bf16_long_run_drift_d1024(hip):
+    """configs[2]'s full utterance length in bf16: 750 top-tier ticks (48,000 samples, 3 s)
+    through the persistent loop, then the fp32 teacher-forced Predictor (the reference's
+    precision, pinned to its goldens) re-runs the whole recurrence along the generated stream
+    in TBPTT chunks with the hidden state carried.  The bf16 loop's log-probs stay within the
+    bf16 tolerance of the fp32 ones over the whole run, and the error does not grow with time
+    (hidden-state drift): the last tenth's mean error is within 1.5x the first tenth's."""
+    import model as M
+    cfg = recipe.CONFIGS['big']
+    m, pred = build(cfg, 17, torch.bfloat16)
+    B, n_cond = 16, 750
+    cond = recipe.synth_cond((B, n_cond, cfg['cond_dim']), 8)
+    spk = np.arange(B) % cfg['spk_dim']
+    gen = M.Generator(m, True)
+    _, lp = gen(B, 0, cond, spk, sampler='philox', seed=77, return_logp=True)
+    seq = gen.last_sequences
+    L = m.lookback
+    T = n_cond * L
+    assert lp.shape == (B, T, 256) and torch.isfinite(lp).all()
+    m.compute_dtype = torch.float32
+    condt = torch.from_numpy(cond)
+    spkt = torch.from_numpy(spk).reshape(-1, 1)
+    Tc = 75 * L                                      # 4,800 samples per TBPTT chunk
+    emean, emax = [], []
+    with torch.no_grad():
+        for c in range(T // Tc):
+            tf = pred(seq[:, c * Tc: c * Tc + L + Tc - 1], c == 0,
+                      condt[:, c * Tc // L:(c + 1) * Tc // L], spkt)
+            d = (tf - lp[:, c * Tc:(c + 1) * Tc]).abs()
+            emean.append(d.mean(-1))                  # (B, Tc): mean over the 256 levels
+            emax.append(d.amax().item())
+    err = torch.cat(emean, 1)                         # (B, T)
+    tenth = T // 10
+    first, last = err[:, :tenth].mean().item(), err[:, -tenth:].mean().item()
+    print('bf16 vs fp32 teacher-forced over %d steps: max %.4f mean %.5f first tenth %.5f '
+          'last tenth %.5f' % (T, max(emax), err.mean().item(), first, last))
+    assert max(emax) < 0.25, max(emax)
+    assert err.mean().item() < 0.02, err.mean().item()
+    assert last <= 1.5 * first + 1e-3, (first, last)
+
+
 def test_config_e_bf16_d1024(hip):
     """configs[4] at full width: 4 tiers FS=[16,4,4], look-ahead conditioning (C = 86),
     D = 1024, 128 utterances (one GPU's share of 1024), bf16 persistent loop.  Same sampler

@@ -48,10 +48,12 @@ def test_forward_golden(hip, name):
                                            g['hidden_%d_tier%d' % (n, t)], atol=2e-5, rtol=0)
 
 
-@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn'])
+@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn', 'big'])
 @pytest.mark.parametrize('graph,persistent', [(True, True), (False, True), (True, False),
                                               (False, False)])
 def test_generation_golden(hip, name, graph, persistent):
+    """fp32 generation with the reference's replayed multinomial noise: index streams bit
+    for bit, log-probs 1e-4 ('big' = configs[2]'s dim-1024 model, 128 samples)."""
     import model as M
     g = golden('gen_' + name)
     cfg = recipe.CONFIGS[name]
@@ -64,6 +66,29 @@ def test_generation_golden(hip, name, graph, persistent):
     assert np.array_equal(idx, g['idx'])
     assert np.array_equal(out.numpy(), g['samples'])
     np.testing.assert_allclose(lp.cpu().numpy(), g['logp'], atol=1e-4, rtol=0)
+
+
+@pytest.mark.parametrize('name', ['t3', 'big'])
+def test_generation_default_sampler_from_seed(hip, name):
+    """The default path exactly as generate.py drives it (generate.py:200-253): seed, build
+    the model (its init consumes the CPU generator in the reference's order, a13), load the
+    weights, call the Generator with no noise= argument -- sampler='torch' draws the
+    multinomials' Exp(1) noise from torch's CPU generator in the reference's consumption
+    order.  The index stream equals the one the reference produced from the same seed."""
+    import model as M
+    g = golden('genseed_' + name)
+    cfg = recipe.CONFIGS[name]
+    torch.manual_seed(int(g['gen_seed']))
+    m = M.SampleRNN(cfg['frame_sizes'], cfg['n_rnn'], cfg['dim'], cfg['learn_h0'],
+                    cfg['q_levels'], True, cfg['weight_norm'], cfg['cond_dim'], cfg['spk_dim'])
+    pred = M.Predictor(m)
+    w = recipe.make_weights(cfg, int(g['weight_seed']))
+    pred.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in w.items()}, strict=True)
+    m = m.to(DEV)
+    gen = M.Generator(m, True)
+    out = gen(int(g['n_seqs']), 0, g['cond'], int(g['spk']))
+    assert np.array_equal(gen.last_sequences[:, m.lookback:].cpu().numpy(), g['idx'])
+    assert np.array_equal(out.numpy(), g['samples'])
 
 
 class _GradCapture:

@@ -75,7 +75,7 @@ def test_oracle_forward(name):
                                            atol=2e-6, rtol=0)
 
 
-@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn'])
+@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn', 'big'])
 def test_oracle_generation(name):
     g = golden('gen_' + name)
     cfg = recipe.CONFIGS[name]
@@ -111,3 +111,40 @@ def test_oracle_tbptt(name):
                                    rtol=0, err_msg=k)
     for t in range(len(cfg['frame_sizes'])):
         np.testing.assert_allclose(m.hidden[t].numpy(), g['hidden_final_tier%d' % t], atol=1e-5)
+
+
+@pytest.mark.parametrize('name', ['t3', 'big'])
+def test_oracle_generation_from_seed(name):
+    """The seed-driven default path (generate.py:200-253) on the CPU: seed -> the drop-in
+    SampleRNN's init (same RNG consumption as the reference's, a13) -> bulk Exp(1) draw of the
+    whole run's multinomial noise (what model.Generator's sampler='torch' does) -> the
+    oracle's argmax(p / q) loop reproduces the reference's stream from that seed.  Pins the
+    init RNG order and the bulk-draw == per-step-multinomial equivalence together."""
+    import model as M
+    g = golden('genseed_' + name)
+    cfg = recipe.CONFIGS[name]
+    torch.manual_seed(int(g['gen_seed']))
+    M.SampleRNN(cfg['frame_sizes'], cfg['n_rnn'], cfg['dim'], cfg['learn_h0'], cfg['q_levels'],
+                True, cfg['weight_norm'], cfg['cond_dim'], cfg['spk_dim'])
+    n = int(g['n_seqs'])
+    L = recipe.lookback(cfg)
+    T = g['cond'].shape[0] * L
+    noise = torch.empty(T, n, cfg['q_levels']).exponential_(1)
+    m = O.from_state_dict(cfg, recipe.make_weights(cfg, int(g['weight_seed'])))
+    seq = m.generate(n, g['cond'], int(g['spk']), noise)
+    assert np.array_equal(seq[:, L:].numpy(), g['idx'])
+
+
+@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn', 'big'])
+def test_log_space_draw_equals_ratio_draw_on_goldens(name):
+    """The device sampler draws argmax_j (z_j - log q_j) (sampler.hpp), the reference
+    argmax_j p_j / q_j (multinomial, model.py:514-517).  On every recorded step of every
+    generation golden (reference log-probs + replayed noise) both give the reference's index:
+    near-tie divergence rate 0 over these fixtures (min relative margins 2e-4 .. 5e-3)."""
+    g = golden('gen_' + name)
+    lp = g['logp'].astype(np.float32).transpose(1, 0, 2)         # (T, n, Q)
+    q = g['noise'].astype(np.float32)
+    ratio = np.argmax(np.exp(lp) / q, axis=-1).T
+    logsp = np.argmax(lp - np.log(q), axis=-1).T
+    assert np.array_equal(ratio, g['idx'])
+    assert np.array_equal(logsp, g['idx'])

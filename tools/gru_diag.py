@@ -8,7 +8,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'jalil-saboorizadeh-multi-speaker-neural-vocoder_amd'))
 import samplernn_hip as H  # noqa: E402
 
-B, D, Fr = 128, 1024, 64
+B, D, Fr = int(sys.argv[1]) if len(sys.argv) > 1 else 128, 1024, 64
 dev = 'cuda'
 T = torch.bfloat16
 whh = (torch.randn(3 * D, D) * 0.03).to(dev, T)
