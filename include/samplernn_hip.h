@@ -196,6 +196,13 @@ int srnn_nll_fwd(const float* logp, int64_t ldl, const int64_t* target, int64_t 
                  int64_t rows, float* loss_row, void* stream);
 int srnn_nll_bwd(const int64_t* target, int64_t ldt, int Tlen, int64_t rows, int Q,
                  float* dlogp, int64_t ldd, float gscale, const float* gmul, void* stream);
+/* Fused backward of sequence_nll_loss_bits (nn.py:66-70) through the MLP's log_softmax
+ * (model.py:324-325): dz = c (exp(logp) - onehot(target)), c = gscale * (*gmul), in dz_dtype
+ * (fp32 / bf16) -- srnn_nll_bwd + srnn_logsoftmax_bwd in one pass, bit-identical to them,
+ * without the dense fp32 dlogp. */
+int srnn_nll_logsoftmax_bwd(const int64_t* target, int64_t ldt, int Tlen, int64_t rows, int Q,
+                            const float* logp, int64_t ldl, float gscale, const float* gmul,
+                            void* dz, int dz_dtype, int64_t ldd, void* stream);
 /* (gmul: optional device scalar the scale is multiplied by -- the incoming loss gradient,
  *  read on the device so the backward never synchronises with the host)                 */
 int srnn_logsoftmax_nll(const float* z, int64_t ldz, const int64_t* target, int64_t ldt,

@@ -30,6 +30,8 @@ struct Gemm2Args {
     const void* mask;
     int64_t lda, ldb, ldc, ldcin, ldmask;
     int M, N, K, ksplit;
+    float* part;          // split-K partial tiles [ksplit][M][N] (deterministic ordered sum),
+                          // or null: fp32 atomics into C
     float alpha, beta;
     int bias_mode, relu;
 };
@@ -196,7 +198,10 @@ __global__ __launch_bounds__(256, 1) void gemm2_kernel(Gemm2Args g) {
                 const int row = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + e;
                 float v = g.alpha * acc[i][j][e];
                 if (g.ksplit > 1) {
-                    atomicAdd(reinterpret_cast<float*>(Cp) + (int64_t)row * g.ldc + col, v);
+                    if (g.part)
+                        g.part[((int64_t)blockIdx.z * g.M + row) * g.N + col] = v;
+                    else
+                        atomicAdd(reinterpret_cast<float*>(Cp) + (int64_t)row * g.ldc + col, v);
                     continue;
                 }
                 if (g.beta != 0.f) v += g.beta * g.Cin[(int64_t)row * g.ldcin + col];
@@ -261,6 +266,19 @@ int srnn_gemm2_try(int dtype, int out_dtype, int transA, int transB, int M, int 
         while (tiles * ks < 512 && (K / (ks * 2)) % KB == 0 && K / (ks * 2) >= 8 * KB) ks *= 2;
     }
     g.ksplit = ks;
+    g.part = nullptr;
+    // split K deterministically (partials + ordered sum, as gemm3) where C allows the float4
+    // sum; fp32 atomics otherwise (SRNN_G3_SPLITK_PART=0 forces them)
+    const bool det = ks > 1 && env_flag("SRNN_G3_SPLITK_PART", 1) && ldc % 4 == 0 &&
+                     (uintptr_t)C % 16 == 0;
+    if (det) {
+        g.part = srnn_splitk_scratch((size_t)ks * M * N * sizeof(float));
+        SRNN_REQUIRE(g.part, "gemm2: split-K scratch allocation failed");
+        const int rc = dtype == SRNN_F32 ? launch2_layout<float, float>(g, !transA, transB, s)
+                                         : launch2_layout<bf16, float>(g, !transA, transB, s);
+        if (rc) return rc;
+        return srnn_splitk_sum(g.part, (float*)C, ldc, M, N, ks, s);
+    }
     if (ks > 1) {
         if (ldc == N) {
             SRNN_CHECK_HIP(hipMemsetAsync(C, 0, (size_t)M * N * 4, s));

@@ -406,6 +406,27 @@ __global__ __launch_bounds__(256) void g3_splitk_sum_kernel(const float* __restr
     *reinterpret_cast<floatx4*>(C + (int64_t)m * ldc + n) = s;
 }
 
+float* srnn_splitk_scratch(size_t bytes) {
+    static float* scratch = nullptr;
+    static size_t have = 0;
+    if (bytes > have) {
+        if (scratch && hipFree(scratch) != hipSuccess) return nullptr;
+        scratch = nullptr;
+        have = 0;
+        if (hipMalloc((void**)&scratch, bytes) != hipSuccess) return nullptr;
+        have = bytes;
+    }
+    return scratch;
+}
+
+int srnn_splitk_sum(const float* part, float* C, int64_t ldc, int M, int N, int ks, hipStream_t s) {
+    const int64_t nq = (int64_t)M * N / 4;
+    hipLaunchKernelGGL(g3_splitk_sum_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, s,
+                       part, C, ldc, M, N, ks);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
 // Persistent: workgroup w owns work units w, w + G, ... (unit = output tile x k-slice);
 // the k-stages of all its units form ONE stream through the ring, so the DMA of the next
 // tile's first stages runs under the current tile's last MFMAs and epilogue.
@@ -1193,17 +1214,8 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
                      ldc % 4 == 0 && (uintptr_t)C % 16 == 0;
     if (ks > 1 && det) {
         // partial tiles in a grow-only scratch, then one ordered sum (no memset, no atomics)
-        static float* scratch = nullptr;
-        static size_t bytes = 0;
-        const size_t need = (size_t)ks * M * N * sizeof(float);
-        if (need > bytes) {
-            if (scratch) SRNN_CHECK_HIP(hipFree(scratch));
-            scratch = nullptr;
-            bytes = 0;
-            SRNN_CHECK_HIP(hipMalloc((void**)&scratch, need));
-            bytes = need;
-        }
-        g.part = scratch;
+        g.part = srnn_splitk_scratch((size_t)ks * M * N * sizeof(float));
+        SRNN_REQUIRE(g.part, "gemm3: split-K scratch allocation failed");
     } else if (ks > 1) {
         if (ldc == N) {
             SRNN_CHECK_HIP(hipMemsetAsync(C, 0, (size_t)M * N * 4, s));
@@ -1215,11 +1227,7 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     if (ks > 1) {
         const int rc = launch3_layout<float, false>(g, kca, kcb, s);
         if (rc || !g.part) return rc;
-        const int64_t nq = (int64_t)M * N / 4;
-        hipLaunchKernelGGL(g3_splitk_sum_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0,
-                           s, (const float*)g.part, (float*)C, ldc, M, N, ks);
-        SRNN_LAUNCH_CHECK();
-        return 0;
+        return srnn_splitk_sum((const float*)g.part, (float*)C, ldc, M, N, ks, s);
     }
     if (out_dtype == SRNN_F32) return launch3_layout<float, true>(g, kca, kcb, s);
     return launch3_layout<bf16, true>(g, kca, kcb, s);

@@ -485,6 +485,53 @@ extern "C" int srnn_logsoftmax_bwd(const float* dlogp, int64_t lddl, const float
     return 0;
 }
 
+// Fused NLL-in-bits + log-softmax backward (nn.py:66-70 then model.py:324-325): the loss
+// gradient w.r.t. the log-probs is -c onehot(target), c = g log2(e) / N, so the logits'
+// gradient is dz = dlogp - exp(logp) sum(dlogp) = c (exp(logp) - onehot), written straight
+// in the GEMM operand dtype -- the dense (rows, Q) fp32 dlogp of the two-kernel path is
+// never materialised nor re-read.  The arithmetic is the two-kernel path's, value for value
+// (g_q = -c or 0, s = -c exactly, dz = g_q - exp(logp) s), so the results are identical.
+template <typename TG>
+__global__ __launch_bounds__(256) void nll_logsoftmax_bwd_kernel(
+    const int64_t* __restrict__ target, int64_t ldt, int Tlen, int64_t rows,
+    const float* __restrict__ lp, int64_t ldl, float gscale, const float* __restrict__ gmul,
+    TG* __restrict__ dz, int64_t ldd) {
+    const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= rows) return;
+    if (gmul) gscale *= *gmul;
+    const int64_t b = r / Tlen, t = r - b * Tlen;
+    const int tq = (int)target[b * ldt + t];
+    float g[4], p[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        g[j] = (lane + 64 * j == tq) ? -gscale : 0.f;
+        p[j] = lp[r * ldl + lane + 64 * j];
+    }
+    const float s = wave_sum(g[0] + g[1] + g[2] + g[3]);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dz[r * ldd + lane + 64 * j] = from_f<TG>(g[j] - expf(p[j]) * s);
+}
+
+extern "C" int srnn_nll_logsoftmax_bwd(const int64_t* target, int64_t ldt, int Tlen,
+                                       int64_t rows, int Q, const float* logp, int64_t ldl,
+                                       float gscale, const float* gmul, void* dz, int dz_dtype,
+                                       int64_t ldd, void* stream) {
+    SRNN_REQUIRE(Q == 256, "nll_logsoftmax_bwd: q_levels must be 256");
+    if (rows <= 0) return 0;
+    dim3 grid(cdiv(rows, 4));
+    if (dz_dtype == SRNN_BF16)
+        hipLaunchKernelGGL((nll_logsoftmax_bwd_kernel<bf16>), grid, dim3(256), 0,
+                           (hipStream_t)stream, target, ldt, Tlen, rows, logp, ldl, gscale, gmul,
+                           (bf16*)dz, ldd);
+    else
+        hipLaunchKernelGGL((nll_logsoftmax_bwd_kernel<float>), grid, dim3(256), 0,
+                           (hipStream_t)stream, target, ldt, Tlen, rows, logp, ldl, gscale, gmul,
+                           (float*)dz, ldd);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
 __global__ void nll_fwd_kernel(const float* __restrict__ lp, int64_t ldl,
                                const int64_t* __restrict__ target, int64_t ldt, int Tlen,
                                int64_t rows, float* __restrict__ loss_row) {

@@ -33,3 +33,10 @@ static inline int env_flag(const char* name, int dflt) {
 // SRNN_PERSIST_FORCE_FAIL test switch is set)
 int* srnn_sticky_flag();
 int srnn_persist_spin_limit(int dflt);
+
+// gemm3.hip: deterministic split-K support.  srnn_splitk_scratch returns a grow-only device
+// buffer of at least `bytes` (null on a HIP error; allocated on first use, i.e. outside graph
+// captures); srnn_splitk_sum writes C[m][n] = sum_z part[z][m][n] in z order (float4 columns:
+// N % 4 == 0, C 16-B aligned, ldc % 4 == 0).
+float* srnn_splitk_scratch(size_t bytes);
+int srnn_splitk_sum(const float* part, float* C, int64_t ldc, int M, int N, int ks, hipStream_t s);

@@ -603,7 +603,11 @@ class _MlpFn(torch.autograd.Function):
         ctx.dims = (B, Tl, D, Q, FS0)
         ctx.save_for_backward(x, a1, a2, logp, Wp, ET, W_hid, W_out)
         ctx.bits = (m1, m2)
-        return logp.reshape(B, Tl, Q)
+        out = logp.reshape(B, Tl, Q)
+        # (nn.sequence_nll_loss_bits on this output hands its gradient back in closed form)
+        ctx.tok = nn.FusedNllToken()
+        out._srnn_nll_token = ctx.tok
+        return out
 
     @staticmethod
     def backward(ctx, dlogp):
@@ -614,10 +618,22 @@ class _MlpFn(torch.autograd.Function):
         dev = logp.device
         st = H.stream
         M = B * Tl
-        dl = dlogp.reshape(M, Q).float().contiguous()
         dz = torch.empty((M, Q), device=dev, dtype=T)
-        H.lib().call('srnn_logsoftmax_bwd', H.ptr(dl), Q, H.ptr(logp), Q, M, Q, H.ptr(dz),
-                     H.dcode(T), Q, st())
+        nll = getattr(dlogp, '_srnn_nll', None)
+        if nll is not None:
+            # loss gradient in closed form (nn._NllBitsFn): fused NLL + log-softmax backward,
+            # dz = c (exp(logp) - onehot) straight into the GEMM operand dtype
+            tg, Tt, gscale, gd = nll
+            H.lib().call('srnn_nll_logsoftmax_bwd', H.ptr(tg), Tt, Tt, M, Q, H.ptr(logp), Q,
+                         gscale, H.ptr(gd), H.ptr(dz), H.dcode(T), Q, st())
+        else:
+            if ctx.tok.emitted:
+                raise RuntimeError('the fused NLL gradient of the MLP log-probs was combined '
+                                   'with another gradient (log-probs used twice); run with '
+                                   'SRNN_FUSED_NLL=0')
+            dl = dlogp.reshape(M, Q).float().contiguous()
+            H.lib().call('srnn_logsoftmax_bwd', H.ptr(dl), Q, H.ptr(logp), Q, M, Q, H.ptr(dz),
+                         H.dcode(T), Q, st())
         dW_out = H.gemm(dz, a2, transA=True)                             # (Q, D)
         db_out = H.colsum(dz, M, Q)
         m1, m2 = ctx.bits

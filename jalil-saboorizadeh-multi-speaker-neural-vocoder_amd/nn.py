@@ -6,6 +6,7 @@ GEMM; sequence_nll_loss_bits runs the HIP NLL kernels.  The init helpers are the
 reference's recipes (they only touch host tensors at construction time).
 """
 import math
+import os
 
 import torch
 from torch import nn
@@ -155,6 +156,21 @@ def concat_init(tensor, inits):
         tensor[i * fan_in: (i + 1) * fan_in, :] = chunk
 
 
+class FusedNllToken:
+    """Marks the SampleLevelMLP's log-prob output (model._MlpFn) so the NLL backward can hand
+    the MLP its loss gradient in closed form instead of a dense (B, T, Q) fp32 tensor:
+    `emitted` records that it did, so the MLP backward can tell a placeholder that autograd
+    summed with another gradient (logp used twice) from a plain dense gradient, and refuse
+    it instead of computing a wrong result."""
+    __slots__ = ('emitted',)
+
+    def __init__(self):
+        self.emitted = False
+
+
+FUSED_NLL = os.environ.get('SRNN_FUSED_NLL', '1') != '0'
+
+
 class _NllBitsFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logp, target):
@@ -166,16 +182,25 @@ class _NllBitsFn(torch.autograd.Function):
         loss = H.colsum(rows, B * T, 1, alpha=LOG2E / (B * T))
         ctx.save_for_backward(tg)
         ctx.shape = (B, T, Q)
+        tok = getattr(logp, '_srnn_nll_token', None)
+        ctx.tok = tok if (FUSED_NLL and isinstance(tok, FusedNllToken) and Q == 256) else None
         return loss.reshape(())
 
     @staticmethod
     def backward(ctx, g):
         (tg,) = ctx.saved_tensors
         B, T, Q = ctx.shape
-        d = torch.empty((B, T, Q), device=tg.device, dtype=torch.float32)
         # gscale = g * log2(e) / N  (mean reduction); g (0-d device tensor) is read on the
         # device: no host synchronisation inside backward
         gd = g.detach().float().reshape(1).contiguous()
+        if ctx.tok is not None:
+            # the MLP computes dz = c (exp(logp) - onehot) itself (srnn_nll_logsoftmax_bwd):
+            # hand it the target and c instead of the dense -c onehot gradient
+            d = torch.zeros((), device=tg.device, dtype=torch.float32).expand(B, T, Q)
+            d._srnn_nll = (tg, T, LOG2E / (B * T), gd)
+            ctx.tok.emitted = True
+            return d, None
+        d = torch.empty((B, T, Q), device=tg.device, dtype=torch.float32)
         H.lib().call('srnn_nll_bwd', H.ptr(tg), T, T, B * T, Q, H.ptr(d), Q, LOG2E / (B * T),
                      H.ptr(gd), H.stream())
         return d, None

@@ -1114,3 +1114,41 @@ def test_gemm_mask_bits(hip, M, N, K, tB, tile):
     y0 = hip.gemm(A, W, transB=tB, bias=bias, relu=True, out_dtype=bf, tile=tile)
     assert torch.equal(y, y0)
     assert torch.equal(bo, _bits_ref(y))
+
+
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_fused_nll_logsoftmax_backward_bit_identical(hip, monkeypatch, dtype):
+    """sequence_nll_loss_bits on the MLP's log-probs hands the MLP its gradient in closed form
+    (srnn_nll_logsoftmax_bwd: dz = c (exp(logp) - onehot)); every gradient equals the
+    two-kernel path's (dense fp32 dlogp + log-softmax backward) bit for bit.  Using the
+    log-probs twice (another gradient summed onto the placeholder) raises instead of
+    returning a wrong gradient."""
+    import model as M
+    import nn as snn
+    torch.manual_seed(4)
+    m = M.SampleRNN([16, 4], 1, 256, True, 256, True, False, 43, 6)
+    m.compute_dtype = dtype
+    pred = M.Predictor(m).to(DEV)
+    B, T, L = 3, 256, 64
+    g = torch.Generator().manual_seed(5)
+    x = torch.randint(0, 256, (B, L + T), generator=g).to(DEV)
+    cond = torch.rand(B, T // L, 43, generator=g).to(DEV)
+    spk = (torch.arange(B) % 6).reshape(-1, 1).to(DEV)
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(snn, 'FUSED_NLL', fused)
+        for p in pred.parameters():
+            p.grad = None
+        loss = snn.sequence_nll_loss_bits(pred(x[:, :-1], True, cond, spk), x[:, L:])
+        loss.backward()
+        res.append((float(loss), {k: p.grad.clone() for k, p in pred.named_parameters()
+                                  if p.grad is not None}))
+    assert res[0][0] == res[1][0]
+    assert res[0][1].keys() == res[1][1].keys()
+    for k in res[0][1]:
+        assert torch.equal(res[0][1][k], res[1][1][k]), k
+    monkeypatch.setattr(snn, 'FUSED_NLL', True)
+    lp = pred(x[:, :-1], True, cond, spk)
+    loss = snn.sequence_nll_loss_bits(lp, x[:, L:]) + lp.sum() * 0.0
+    with pytest.raises(RuntimeError, match='used twice'):
+        loss.backward()
