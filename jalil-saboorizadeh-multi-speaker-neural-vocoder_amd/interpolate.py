@@ -15,7 +15,8 @@ outputs and quirks as the reference:
     (interpolate.py:85-87; kept, documented).
 
 The per-frame state machine is replaced by a run-length pass over the voiced mask, so a
-file is O(runs) numpy slices instead of a Python loop over every frame.
+file is O(runs) numpy slices instead of a Python loop over every frame.  The reference file
+is MIT-licensed (c) 2016 Santi Dsp (interpolate.py:1-22); see THIRD_PARTY_NOTICES.md.
 """
 import argparse
 import os
@@ -70,49 +71,62 @@ def interpolation(signal, unvoiced_symbol):
     return isignal, uv
 
 
+# unvoiced thresholds of the two Ahocoder streams (interpolate.py:97-105): log-F0 frames at
+# or below -1e10, maximum-voiced-frequency frames at or below 1e3
+THRESHOLDS = {'f0': -10000000000, 'vf': 1e3}
+
+
+def _outputs(path):
+    """(interpolation file, u/v file) next to `path`: <stem>.i<ext> and <stem>.uv."""
+    folder, name = os.path.split(path.rstrip())
+    stem, ext = os.path.splitext(name)
+    return os.path.join(folder, stem + '.i' + ext), os.path.join(folder, stem + '.uv')
+
+
 def process_file(filename, unvoiced_symbol, gen_uv):
-    """interpolate.py:77-87."""
-    dire, fullname = os.path.split(filename.rstrip())
-    basename, ext = os.path.splitext(fullname)
-    raw = np.loadtxt(filename)
-    interp, uv = interpolation(raw, unvoiced_symbol)
-    out_interp_file = os.path.join(dire, basename + '.i' + ext)
-    print('Writing interpolation to {}'.format(out_interp_file))
-    np.savetxt(out_interp_file, interp)
-    if gen_uv:
-        out_uv_file = os.path.join(dire, basename + '.uv')
-        print('Writing u/v mask to {}'.format(out_uv_file))
-        np.savetxt(out_interp_file, uv)      # reference quirk: overwrites the .i file
+    """interpolate.py:77-87: <stem>.i<ext> <- interpolated frames; with gen_uv the mask is
+    announced as <stem>.uv but, as in the reference, written over the .i file."""
+    interp_path, uv_path = _outputs(filename)
+    interp, uv = interpolation(np.loadtxt(filename), unvoiced_symbol)
+    print('Writing interpolation to {}'.format(interp_path))
+    np.savetxt(interp_path, interp)
+    if not gen_uv:
+        return
+    print('Writing u/v mask to {}'.format(uv_path))
+    np.savetxt(interp_path, uv)             # the reference's destination (documented quirk)
 
 
 def process_guia(guia_file, unvoiced_symbol, gen_uv):
-    """interpolate.py:90-94."""
+    """interpolate.py:90-94: every path listed (one per line) in a guide file."""
     with open(guia_file) as fh:
-        for filename in fh:
-            process_file(filename.rstrip(), unvoiced_symbol, gen_uv)
+        paths = [line.rstrip() for line in fh]
+    for path in paths:
+        process_file(path, unvoiced_symbol, gen_uv)
 
 
 def main(opts):
-    """interpolate.py:97-105."""
-    if opts.f0_file:
-        process_file(opts.f0_file, -10000000000, opts.gen_uv)
-    if opts.f0_guia:
-        process_guia(opts.f0_guia, -10000000000, opts.gen_uv)
-    if opts.vf_file:
-        process_file(opts.vf_file, 1e3, opts.gen_uv)
-    if opts.vf_guia:
-        process_guia(opts.vf_guia, 1e3, opts.gen_uv)
+    """interpolate.py:97-105: single files first, then guide files, f0 before vf."""
+    jobs = ((opts.f0_file, process_file, 'f0'), (opts.f0_guia, process_guia, 'f0'),
+            (opts.vf_file, process_file, 'vf'), (opts.vf_guia, process_guia, 'vf'))
+    for target, run, stream in jobs:
+        if target:
+            run(target, THRESHOLDS[stream], opts.gen_uv)
+
+
+def build_parser():
+    """The reference's command line (interpolate.py:108-127): --f0_file / --f0_guia /
+    --vf_file / --vf_guia and --no-uv."""
+    p = argparse.ArgumentParser('Here are the main options to interpolate Ahocoder features')
+    for stream, what in (('f0', 'lf0'), ('vf', 'vf')):
+        p.add_argument('--%s_guia' % stream, type=str, default=None,
+                       help='guide file listing the %s files to interpolate' % what)
+        p.add_argument('--%s_file' % stream, type=str, default=None,
+                       help='a single %s file to interpolate' % what)
+    p.add_argument('--no-uv', dest='gen_uv', action='store_false',
+                   help='do not generate the U/V masks')
+    p.set_defaults(gen_uv=True)
+    return p
 
 
 if __name__ == '__main__':
-    parser = argparse.ArgumentParser('Here are the main options to interpolate Ahocoder features')
-    parser.add_argument('--f0_guia', type=str, default=None,
-                        help='Guia file containing pointers to the lf0 files to interpolate.')
-    parser.add_argument('--f0_file', type=str, default=None, help='Filename of a single F0 file')
-    parser.add_argument('--vf_guia', type=str, default=None,
-                        help='Guia file containing pointers to the vf files to interpolate.')
-    parser.add_argument('--vf_file', type=str, default=None, help='Filename of a single VF file')
-    parser.add_argument('--no-uv', dest='gen_uv', action='store_false',
-                        help='U/V masks are NOT generated.')
-    parser.set_defaults(gen_uv=True)
-    main(parser.parse_args())
+    main(build_parser().parse_args())

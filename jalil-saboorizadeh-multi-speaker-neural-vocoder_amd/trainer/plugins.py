@@ -11,6 +11,10 @@ HIP Predictor, loss read with .item() -- the reference's `loss.data[0]`, plugins
 fails on torch >= 0.5), AbsoluteTimeMonitor, SaverPlugin (ep{E}-it{I} / best-ep{E}-it{I}
 state_dict checkpoints), GeneratorPlugin (device generation + WAV), StatsPlugin (stats.pkl +
 svg plots), CometPlugin.
+
+The reference plugins are samplernn-pytorch's (MIT, (c) 2017 Piotr Kozakowski); their names,
+checkpoint naming, log-line format and pickle layout are the drop-in contract, restated here
+(THIRD_PARTY_NOTICES.md).
 """
 import os
 import pickle
