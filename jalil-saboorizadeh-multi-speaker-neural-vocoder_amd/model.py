@@ -5,13 +5,16 @@ Same classes, constructor signatures, attributes, state_dict keys and init recip
 Runner, Predictor, Generator -- so train.py / generate.py bind unchanged.  Every
 forward/backward runs on the hand-written HIP kernels of libsamplernn_hip.so:
 
-  * FrameLevelRNN  -> _TierFn: input/cond/speaker projections (MFMA GEMMs with fused
-    bias + upper-tier add), GRU input projection for all frames in one GEMM, one fused
-    MFMA+gate kernel per time step, LearnedUpsampling1d as one GEMM; backward mirrors it.
-  * SampleLevelMLP -> _MlpFn: embedding . conv folded into a per-tap table, L1 as a
-    gather-sum, hidden/output GEMMs with fused bias/ReLU, log-softmax kernel.
-  * Generator      -> srnn_generate: the whole autoregressive loop on the device,
-    captured as a hipGraph (no per-sample host round trip).
+  * FrameLevelRNN  -> srnn::tier_fwd / tier_bwd (custom_ops.py; tier_forward /
+    tier_backward here): input / cond / speaker projections (MFMA GEMMs with fused bias +
+    upper-tier add), the GRU input projection for all frames in one GEMM, the recurrence as
+    one persistent sweep per layer (gru_xcd.hip) or per-step kernels, LearnedUpsampling1d as
+    one GEMM; the backward mirrors it.
+  * SampleLevelMLP -> srnn::mlp_fwd / mlp_bwd (mlp_forward / mlp_backward): embedding . conv
+    folded into a per-tap table, L1 as a gather-sum, hidden / output GEMMs with fused bias /
+    ReLU, log-softmax kernel; with sequence_nll_loss_bits the loss backward is fused in.
+  * Generator      -> srnn::generate: the whole autoregressive loop on the device (persistent
+    sample loop + tier ticks, captured as a hipGraph; no per-sample host round trip).
 
 Numerics: fp32 by default (parity mode, logits within 1e-4 of the reference);
 `SampleRNN.compute_dtype = torch.bfloat16` (or env SRNN_COMPUTE_DTYPE=bf16) runs the
@@ -24,6 +27,7 @@ import numpy as np
 import torch
 from torch.nn import init
 
+import custom_ops
 import nn
 import utils
 import samplernn_hip as H
@@ -151,7 +155,7 @@ class FrameLevelRNN(torch.nn.Module):
         # always weight-normed: model.py:177 tests the imported function, not the flag
         nn.apply_weight_norm(self.upsampling.conv_t)
 
-    # parameter tensors in the order _TierFn consumes them
+    # parameter tensors in the order tier_forward consumes them (srnn::tier_fwd's params)
     def _param_list(self):
         ps = []
         ps += nn.weight_params(self.input_expand) + [self.input_expand.bias]
@@ -176,11 +180,12 @@ class FrameLevelRNN(torch.nn.Module):
             spk = spk.to(dev).long()
         h0 = self.h0
         ps = self._param_list()
-        out, h = _TierFn.apply(self, prev_samples.float().contiguous(),
-                               None if upper_tier_conditioning is None
-                               else upper_tier_conditioning.contiguous(),
-                               cond, spk, None if hidden is None else hidden.contiguous(),
-                               h0, *ps)
+        # the registered op srnn::tier_fwd (custom_ops.py; autograd: srnn::tier_bwd)
+        out, h = custom_ops.tier(prev_samples.float().contiguous(),
+                                 None if upper_tier_conditioning is None
+                                 else upper_tier_conditioning.contiguous(),
+                                 cond, spk, None if hidden is None else hidden.contiguous(),
+                                 h0, ps, tier_meta(self))
         return out, h
 
 
@@ -193,316 +198,396 @@ def _wcast(mod, T):
 
 
 def _dt(mod):
+    T = mod.__dict__.get('T')
+    if T is not None:
+        return T
     root = mod.__dict__.get('_root')
     return root.compute_dtype if root is not None else torch.float32
 
 
-class _TierFn(torch.autograd.Function):
+class _Conv:
+    """A conv's parameters as the weight helpers of nn.py see them: `weight`, or
+    `weight_g` / `weight_v` under weight norm."""
 
-    @staticmethod
-    def forward(ctx, mod, prev, upper, cond, spk, hidden, h0, *ps):
-        T = _dt(mod)
-        B, Fr, nfs = prev.shape
-        D = mod.dim
-        L = mod.n_rnn
-        dev = prev.device
+    def __init__(self, ts):
+        if len(ts) == 2:
+            self.weight_g, self.weight_v = ts
+        else:
+            self.weight = ts[0]
+
+
+class TierSpec:
+    """Static description of one FrameLevelRNN for the srnn::tier_* ops: the meta ints
+    (tier_meta) plus the parameter list in FrameLevelRNN._param_list order."""
+
+    def __init__(self, meta, ps):
+        (self.dim, self.n_frame_samples, self.frame_size, self.n_rnn, is_cond, feeds, dt,
+         wn_ie, wn_c, wn_s, wn_up) = [int(v) for v in meta[:11]]
+        self.is_cond = bool(is_cond)
+        self.T = torch.bfloat16 if dt else torch.float32
+        self._feeds_mlp = bool(feeds)
         it = iter(ps)
 
-        def take_w(m):
-            return [next(it) for _ in nn.weight_params(m)]
+        def take(wn):
+            return _Conv([next(it) for _ in range(2 if wn else 1)])
+        self.input_expand = take(wn_ie)
+        next(it)
+        if self.is_cond:
+            self.cond_expand = take(wn_c)
+            next(it)
+            next(it)
+            self.spk_expand = take(wn_s)
+            next(it)
+        for _ in range(4 * self.n_rnn):
+            next(it)
+        self.upsampling = _Conv([])
+        self.upsampling.conv_t = take(wn_up)
 
-        ie_p = take_w(mod.input_expand)
-        ie_b = next(it)
-        W_ie = _wcast(mod.input_expand, T).reshape(D, nfs)
-        prevT = H.cast(prev.reshape(B * Fr, nfs), T)
-        lp = T != torch.float32
-        # In the low-precision mode only the compute-dtype copy of the first GRU layer's input
-        # is ever read, so the last projection writes it directly (no fp32 x0, no cast); the
-        # fp32 (parity) mode keeps the reference's summation order.
-        x0 = H.linear(prevT, W_ie, bias=ie_b,
-                      cin=None if upper is None else upper.reshape(B * Fr, D),
-                      beta=0.0 if upper is None else 1.0,
-                      out_dtype=T if lp and not mod.is_cond else torch.float32)
-        condT = spk_embT = W_c = W_s = None
-        if mod.is_cond:
-            take_w(mod.cond_expand)
-            c_b = next(it)
-            E_s = next(it)
-            take_w(mod.spk_expand)
-            s_b = next(it)
-            C = cond.shape[-1]
-            W_c = _wcast(mod.cond_expand, T).reshape(D, C)
-            condT = H.cast(cond.reshape(B * Fr, C).float().contiguous(), T)
-            S = E_s.shape[1]
-            spk_flat = spk.reshape(B).contiguous()
-            spk_emb = torch.empty((B, S), device=dev, dtype=torch.float32)
-            H.lib().call('srnn_gather_rows', H.ptr(E_s), S, H.ptr(spk_flat), B, S, H.ptr(spk_emb),
-                         H.F32, S, H.stream())
-            spk_embT = H.cast(spk_emb, T)
-            W_s = _wcast(mod.spk_expand, T).reshape(D, S)
-            spk_proj = H.linear(spk_embT, W_s, bias=s_b)
-            if lp:
-                H.lib().call('srnn_add_bcast_rows', H.ptr(x0), H.ptr(spk_proj), B, Fr, D, D,
-                             H.stream())
-                x0 = H.linear(condT, W_c, bias=c_b, cin=x0, beta=1.0, out_dtype=T)
-            else:
-                H.linear(condT, W_c, bias=c_b, cin=x0, beta=1.0, out=x0)
-                H.lib().call('srnn_add_bcast_rows', H.ptr(x0), H.ptr(spk_proj), B, Fr, D, D,
-                             H.stream())
-        else:
-            spk_flat = None
-        reset = hidden is None
-        if reset:   # model.py:224-228
-            h_in = h0.detach().reshape(L, 1, D).expand(L, B, D).contiguous()
-        else:
-            h_in = hidden.float().contiguous()
-        Wih, Whh, WhhF, bih, bhh = [], [], [], [], []
-        xs, outs, outsT, gates, hprevs = [], [], [], [], []
-        X = x0
-        for l in range(L):
-            wih, whh, b_ih, b_hh = next(it), next(it), next(it), next(it)
-            Wih.append(H.cast_param(wih, T))
-            Whh.append(H.cast_param(whh, T))
-            WhhF.append(whh)
-            bih.append(b_ih)
-            bhh.append(b_hh)
-            XT = H.cast(X, T)
-            gi = H.linear(XT, Wih[l], bias=b_ih)                      # (B*F, 3D)
-            out = torch.empty((B, Fr, D), device=dev, dtype=torch.float32)
-            outT = torch.empty((B, Fr, D), device=dev, dtype=T) if lp else out
-            gt = torch.empty((B, Fr, 4 * D), device=dev, dtype=torch.float32)
-            hpf = h_in[l]
-            xw = H.gru_xcd_work_bytes(T, B, D) if lp else 0
-            # (the XCD sweep reads the fp32 state itself; the other paths take a T copy)
-            hpT = H.cast(hpf, T) if xw == 0 else None
-            seq = lp and (xw > 0 or H.gru_seq_supported(T, B, D))
-            if seq:
-                H.before_persistent_sweep()
-            hprevT = None
-            if xw > 0:
-                # whole sequence in one persistent launch, row groups per XCD, W_hh in VGPRs;
-                # it also writes the previous-state sequence [h0, h_0 .. h_{F-2}] in bf16 for
-                # the backward's W_hh gradient
-                work = torch.empty(xw, device=dev, dtype=torch.uint8)
-                hprevT = torch.empty((B, Fr, D), device=dev, dtype=T)
-                _STATS['gru_xcd_fwd'] += 1
-                ev = H.roof_begin()
-                H.lib().call('srnn_gru_xcd_fwd2', H.dcode(T), B, D, Fr, H.ptr(gi), Fr * 3 * D,
-                             3 * D, H.ptr(hpf), H.ptr(Whh[l]), H.ptr(b_hh), H.ptr(out),
-                             H.ptr(outT), Fr * D, D, H.ptr(gt), Fr * 4 * D, 4 * D,
-                             H.ptr(hprevT), H.ptr(work), xw, H.stream())
-                H.roof_end('gru_xcd_fwd', ev, 2.0 * B * Fr * 3 * D * D)
-            elif seq:
-                # whole sequence in one persistent launch (W_hh resident in LDS)
-                work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
-                _STATS['gru_seq'] += 1
-                H.lib().call('srnn_gru_seq_fwd', H.dcode(T), B, D, Fr, H.ptr(gi), Fr * 3 * D,
-                             3 * D, H.ptr(hpf), H.ptr(hpT), H.ptr(Whh[l]), H.ptr(b_hh),
-                             H.ptr(out), H.ptr(outT), Fr * D, D, H.ptr(gt), Fr * 4 * D, 4 * D,
-                             H.ptr(work), work.numel() * 4, H.stream())
-            _STATS['gru_cell_steps'] += 0 if seq else Fr
-            for t in range(0 if not seq else Fr, Fr):
-                if t == 0:
-                    hp_t, hp_f, ldh = hpT, hpf, D
-                else:
-                    hp_t, hp_f, ldh = outT[:, t - 1], out[:, t - 1], Fr * D
-                H.lib().call('srnn_gru_cell', H.dcode(T), B, D, D, None, 0, None, None,
-                             H.ptr(gi[t:]), Fr * 3 * D, H.ptr(hp_t), ldh, H.ptr(hp_f), ldh,
-                             H.ptr(Whh[l]), H.ptr(b_hh), H.ptr(out[:, t]), Fr * D,
-                             H.ptr(outT[:, t]) if lp else None, Fr * D, H.ptr(gt[:, t]),
-                             Fr * 4 * D, H.stream())
-            xs.append(XT)
-            hprevs.append(hprevT)
-            outs.append(out)
-            outsT.append(outT)
-            gates.append(gt)
-            X = out.reshape(B * Fr, D)
-        up_p = take_w(mod.upsampling.conv_t)
-        up_b = next(it)
-        k = mod.frame_size
-        W_up = nn.convt_operand(mod.upsampling.conv_t, T)                        # (k, D, D)
-        b_up = H.permute3(up_b.reshape(1, D, k), (0, 2, 1)).reshape(k * D)
-        # the bottom tier feeds the MLP's gather directly: its upsampled output (and so the
-        # gradient coming back) is in the compute dtype; upper tiers stay fp32 (Cin input)
-        y_dt = T if mod.__dict__.get('_feeds_mlp') else torch.float32
-        Y = H.linear(outsT[-1].reshape(B * Fr, D), W_up.reshape(k * D, D), bias=b_up,
-                     out_dtype=y_dt)
-        h_new = torch.stack([o[:, -1] for o in outs], 0)
-        ctx.mod = mod
-        ctx.reset = reset
-        ctx.has_upper = upper is not None
-        ctx.dims = (B, Fr, nfs, D, L, k)
-        ctx.T = T
-        ctx.save_for_backward(prevT, condT, spk_embT, spk_flat, h_in, W_ie, W_c, W_s, W_up,
-                              *Wih, *Whh, *xs, *outs, *outsT, *gates, *WhhF, *hprevs)
-        ctx.mark_non_differentiable(h_new)
-        return Y.reshape(B, Fr * k, D), h_new
 
-    @staticmethod
-    def backward(ctx, dY, dh_new):
-        mod = ctx.mod
-        B, Fr, nfs, D, L, k = ctx.dims
-        T = ctx.T
-        lp = T != torch.float32
-        sv = ctx.saved_tensors
-        prevT, condT, spk_embT, spk_flat, h_in, W_ie, W_c, W_s, W_up = sv[:9]
-        r = sv[9:]
-        Wih, Whh = r[:L], r[L:2 * L]
-        xs, outs, outsT, gates = r[2 * L:3 * L], r[3 * L:4 * L], r[4 * L:5 * L], r[5 * L:6 * L]
-        WhhF = r[6 * L:7 * L]                     # the fp32 parameters W_hh
-        hprevs = r[7 * L:8 * L]                   # [h_in, out[:, :F-1]] in T, or None
-        dev = dY.device
-        st = H.stream
-        M = B * Fr
-        # --- upsampling (nn.py:33-43)
-        if dY.dtype == T:
-            dY2 = dYT = dY.reshape(M, k * D).contiguous()
+def tier_meta(mod):
+    """The meta ints of TierSpec for a FrameLevelRNN."""
+    wn = lambda m: int(hasattr(m, 'weight_g'))  # noqa: E731
+    return [mod.dim, mod.n_frame_samples, mod.frame_size, mod.n_rnn, int(mod.is_cond),
+            int(bool(mod.__dict__.get('_feeds_mlp'))), H.dcode(_dt(mod)),
+            wn(mod.input_expand), wn(mod.cond_expand) if mod.is_cond else 0,
+            wn(mod.spk_expand) if mod.is_cond else 0, wn(mod.upsampling.conv_t)]
+
+
+class MlpSpec:
+    """Static description of the SampleLevelMLP for the srnn::mlp_* ops (mlp_meta + the
+    parameter list in SampleLevelMLP._param_list order)."""
+
+    def __init__(self, meta, ps):
+        self.q_levels, self.dim, self.frame_size, dt, wn = [int(v) for v in meta[:5]]
+        self.T = torch.bfloat16 if dt else torch.float32
+        it = iter(ps)
+
+        def take():
+            return _Conv([next(it) for _ in range(2 if wn else 1)])
+        self.embedding = _Conv([next(it)])
+        self.input = take()
+        self.hidden = take()
+        self.hidden.bias = next(it)
+        self.output = take()
+        self.output.bias = next(it)
+
+
+def mlp_meta(mlp):
+    return [mlp.q_levels, mlp.dim, mlp.frame_size, H.dcode(_dt(mlp)),
+            int(hasattr(mlp.hidden, 'weight_g'))]
+
+
+class _State:
+    """What a tier / MLP forward keeps for its backward (custom_ops stash)."""
+
+
+def tier_forward(mod, prev, upper, cond, spk, hidden, h0, ps):
+    """FrameLevelRNN forward (model.py:180-263) on the HIP kernels: returns (Y, h_new, state)
+    with state what tier_backward needs (srnn::tier_fwd, custom_ops.py)."""
+    T = _dt(mod)
+    B, Fr, nfs = prev.shape
+    D = mod.dim
+    L = mod.n_rnn
+    dev = prev.device
+    it = iter(ps)
+
+    def take_w(m):
+        return [next(it) for _ in nn.weight_params(m)]
+
+    ie_p = take_w(mod.input_expand)
+    ie_b = next(it)
+    W_ie = _wcast(mod.input_expand, T).reshape(D, nfs)
+    prevT = H.cast(prev.reshape(B * Fr, nfs), T)
+    lp = T != torch.float32
+    # In the low-precision mode only the compute-dtype copy of the first GRU layer's input
+    # is ever read, so the last projection writes it directly (no fp32 x0, no cast); the
+    # fp32 (parity) mode keeps the reference's summation order.
+    x0 = H.linear(prevT, W_ie, bias=ie_b,
+                  cin=None if upper is None else upper.reshape(B * Fr, D),
+                  beta=0.0 if upper is None else 1.0,
+                  out_dtype=T if lp and not mod.is_cond else torch.float32)
+    condT = spk_embT = W_c = W_s = None
+    if mod.is_cond:
+        take_w(mod.cond_expand)
+        c_b = next(it)
+        E_s = next(it)
+        take_w(mod.spk_expand)
+        s_b = next(it)
+        C = cond.shape[-1]
+        W_c = _wcast(mod.cond_expand, T).reshape(D, C)
+        condT = H.cast(cond.reshape(B * Fr, C).float().contiguous(), T)
+        S = E_s.shape[1]
+        spk_flat = spk.reshape(B).contiguous()
+        spk_emb = torch.empty((B, S), device=dev, dtype=torch.float32)
+        H.lib().call('srnn_gather_rows', H.ptr(E_s), S, H.ptr(spk_flat), B, S, H.ptr(spk_emb),
+                     H.F32, S, H.stream())
+        spk_embT = H.cast(spk_emb, T)
+        W_s = _wcast(mod.spk_expand, T).reshape(D, S)
+        spk_proj = H.linear(spk_embT, W_s, bias=s_b)
+        if lp:
+            H.lib().call('srnn_add_bcast_rows', H.ptr(x0), H.ptr(spk_proj), B, Fr, D, D,
+                         H.stream())
+            x0 = H.linear(condT, W_c, bias=c_b, cin=x0, beta=1.0, out_dtype=T)
         else:
-            dY2 = dY.reshape(M, k * D).float().contiguous()
-            # the tier below already cast this gradient (its dx0) to the compute dtype
-            lpc = getattr(dY, '_srnn_lp', None)
-            if lpc is not None and lpc[1] == dY._version and lpc[0].dtype == T and \
-                    lpc[0].numel() == dY2.numel() and dY2.data_ptr() == dY.data_ptr():
-                dYT = lpc[0].reshape(M, k * D)
-                _STATS['fused_lp'] += 1
+            H.linear(condT, W_c, bias=c_b, cin=x0, beta=1.0, out=x0)
+            H.lib().call('srnn_add_bcast_rows', H.ptr(x0), H.ptr(spk_proj), B, Fr, D, D,
+                         H.stream())
+    else:
+        spk_flat = None
+    reset = hidden is None
+    if reset:   # model.py:224-228
+        h_in = h0.detach().reshape(L, 1, D).expand(L, B, D).contiguous()
+    else:
+        h_in = hidden.float().contiguous()
+    Wih, Whh, WhhF, bih, bhh = [], [], [], [], []
+    xs, outs, outsT, gates, hprevs = [], [], [], [], []
+    X = x0
+    for l in range(L):
+        wih, whh, b_ih, b_hh = next(it), next(it), next(it), next(it)
+        Wih.append(H.cast_param(wih, T))
+        Whh.append(H.cast_param(whh, T))
+        WhhF.append(whh)
+        bih.append(b_ih)
+        bhh.append(b_hh)
+        XT = H.cast(X, T)
+        gi = H.linear(XT, Wih[l], bias=b_ih)                      # (B*F, 3D)
+        out = torch.empty((B, Fr, D), device=dev, dtype=torch.float32)
+        outT = torch.empty((B, Fr, D), device=dev, dtype=T) if lp else out
+        gt = torch.empty((B, Fr, 4 * D), device=dev, dtype=torch.float32)
+        hpf = h_in[l]
+        xw = H.gru_xcd_work_bytes(T, B, D) if lp else 0
+        # (the XCD sweep reads the fp32 state itself; the other paths take a T copy)
+        hpT = H.cast(hpf, T) if xw == 0 else None
+        seq = lp and (xw > 0 or H.gru_seq_supported(T, B, D))
+        if seq:
+            H.before_persistent_sweep()
+        hprevT = None
+        if xw > 0:
+            # whole sequence in one persistent launch, row groups per XCD, W_hh in VGPRs;
+            # it also writes the previous-state sequence [h0, h_0 .. h_{F-2}] in bf16 for
+            # the backward's W_hh gradient
+            work = torch.empty(xw, device=dev, dtype=torch.uint8)
+            hprevT = torch.empty((B, Fr, D), device=dev, dtype=T)
+            _STATS['gru_xcd_fwd'] += 1
+            ev = H.roof_begin()
+            H.lib().call('srnn_gru_xcd_fwd2', H.dcode(T), B, D, Fr, H.ptr(gi), Fr * 3 * D,
+                         3 * D, H.ptr(hpf), H.ptr(Whh[l]), H.ptr(b_hh), H.ptr(out),
+                         H.ptr(outT), Fr * D, D, H.ptr(gt), Fr * 4 * D, 4 * D,
+                         H.ptr(hprevT), H.ptr(work), xw, H.stream())
+            H.roof_end('gru_xcd_fwd', ev, 2.0 * B * Fr * 3 * D * D)
+        elif seq:
+            # whole sequence in one persistent launch (W_hh resident in LDS)
+            work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
+            _STATS['gru_seq'] += 1
+            H.lib().call('srnn_gru_seq_fwd', H.dcode(T), B, D, Fr, H.ptr(gi), Fr * 3 * D,
+                         3 * D, H.ptr(hpf), H.ptr(hpT), H.ptr(Whh[l]), H.ptr(b_hh),
+                         H.ptr(out), H.ptr(outT), Fr * D, D, H.ptr(gt), Fr * 4 * D, 4 * D,
+                         H.ptr(work), work.numel() * 4, H.stream())
+        _STATS['gru_cell_steps'] += 0 if seq else Fr
+        for t in range(0 if not seq else Fr, Fr):
+            if t == 0:
+                hp_t, hp_f, ldh = hpT, hpf, D
             else:
-                dYT = H.cast(dY2, T)
-        # weight gradient transposed, [i][j*D + o]: one row per input channel for the
-        # per-channel weight-norm backward (no permute of the 16 x D x D gradient)
-        dWupT = H.gemm(outsT[-1].reshape(M, D), dYT, transA=True)         # (D, k*D)
-        # bias gradient: summed by the MLP's dTab pass when dY is its untouched d(upper)
-        cs = getattr(dY, '_srnn_colsum', None)
-        if cs is not None and cs[1] == dY._version and cs[2] == k and cs[0].numel() == k * D:
-            db_up = cs[0]
-            _STATS['fused_colsum'] += 1
+                hp_t, hp_f, ldh = outT[:, t - 1], out[:, t - 1], Fr * D
+            H.lib().call('srnn_gru_cell', H.dcode(T), B, D, D, None, 0, None, None,
+                         H.ptr(gi[t:]), Fr * 3 * D, H.ptr(hp_t), ldh, H.ptr(hp_f), ldh,
+                         H.ptr(Whh[l]), H.ptr(b_hh), H.ptr(out[:, t]), Fr * D,
+                         H.ptr(outT[:, t]) if lp else None, Fr * D, H.ptr(gt[:, t]),
+                         Fr * 4 * D, H.stream())
+        xs.append(XT)
+        hprevs.append(hprevT)
+        outs.append(out)
+        outsT.append(outT)
+        gates.append(gt)
+        X = out.reshape(B * Fr, D)
+    up_p = take_w(mod.upsampling.conv_t)
+    up_b = next(it)
+    k = mod.frame_size
+    W_up = nn.convt_operand(mod.upsampling.conv_t, T)                        # (k, D, D)
+    b_up = H.permute3(up_b.reshape(1, D, k), (0, 2, 1)).reshape(k * D)
+    # the bottom tier feeds the MLP's gather directly: its upsampled output (and so the
+    # gradient coming back) is in the compute dtype; upper tiers stay fp32 (Cin input)
+    y_dt = T if mod.__dict__.get('_feeds_mlp') else torch.float32
+    Y = H.linear(outsT[-1].reshape(B * Fr, D), W_up.reshape(k * D, D), bias=b_up,
+                 out_dtype=y_dt)
+    h_new = torch.stack([o[:, -1] for o in outs], 0)
+    ctx = _State()
+    ctx.mod = mod
+    ctx.reset = reset
+    ctx.has_upper = upper is not None
+    ctx.dims = (B, Fr, nfs, D, L, k)
+    ctx.T = T
+    ctx.saved_tensors = (prevT, condT, spk_embT, spk_flat, h_in, W_ie, W_c, W_s, W_up,
+                         *Wih, *Whh, *xs, *outs, *outsT, *gates, *WhhF, *hprevs)
+    return Y.reshape(B, Fr * k, D), h_new, ctx
+
+
+def tier_backward(ctx, dY, need_h0):
+    """Backward of tier_forward: (d_upper or None, dh0 or None, [parameter gradients in
+    _param_list order])."""
+    mod = ctx.mod
+    B, Fr, nfs, D, L, k = ctx.dims
+    T = ctx.T
+    lp = T != torch.float32
+    sv = ctx.saved_tensors
+    prevT, condT, spk_embT, spk_flat, h_in, W_ie, W_c, W_s, W_up = sv[:9]
+    r = sv[9:]
+    Wih, Whh = r[:L], r[L:2 * L]
+    xs, outs, outsT, gates = r[2 * L:3 * L], r[3 * L:4 * L], r[4 * L:5 * L], r[5 * L:6 * L]
+    WhhF = r[6 * L:7 * L]                     # the fp32 parameters W_hh
+    hprevs = r[7 * L:8 * L]                   # [h_in, out[:, :F-1]] in T, or None
+    dev = dY.device
+    st = H.stream
+    M = B * Fr
+    # --- upsampling (nn.py:33-43)
+    if dY.dtype == T:
+        dY2 = dYT = dY.reshape(M, k * D).contiguous()
+    else:
+        dY2 = dY.reshape(M, k * D).float().contiguous()
+        # the tier below already cast this gradient (its dx0) to the compute dtype
+        lpc = getattr(dY, '_srnn_lp', None)
+        if lpc is not None and lpc[1] == dY._version and lpc[0].dtype == T and \
+                lpc[0].numel() == dY2.numel() and dY2.data_ptr() == dY.data_ptr():
+            dYT = lpc[0].reshape(M, k * D)
+            _STATS['fused_lp'] += 1
         else:
-            db_up = H.colsum(dY2, M, k * D)
-        dX = H.gemm(dYT, W_up.reshape(k * D, D))                          # (M, D)
-        g_up = nn.convt_grad_to_params(mod.upsampling.conv_t, dWupT)
-        g_up_b = H.permute3(db_up.reshape(1, k, D), (0, 2, 1)).reshape(D, k)
-        # --- GRU layers, top layer first
-        g_rnn = [None] * L
-        dh_in = [None] * L
-        for l in reversed(range(L)):
-            dOut = dX.reshape(B, Fr, D)
-            # W_hh^T (D, 3D): k-contiguous operand for the deep-ring backward kernel, straight
-            # from the fp32 parameter (the same bf16 values as the forward's copy, no cast pass)
-            WhhT = H.permute3(WhhF[l].detach().reshape(1, 3 * D, D), (0, 2, 1), dtype=T)
-            xbw = H.gru_xcd_bwd_work_bytes(T, B, D) if lp else 0
-            seq = lp and (xbw > 0 or H.gru_seq_supported(T, B, D))
-            ddir = [torch.empty((B, D), device=dev, dtype=torch.float32) for _ in range(2)]
-            dGIT = bsum = None
-            if xbw > 0:
-                # the sweep writes bf16 dgh / dgi (the GEMM operands) and per-row bias sums;
-                # no fp32 copies of either
-                dGH = dGI = None
-                dGHT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T)
-                dGIT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T)
-                bsum = torch.empty((B, 4 * D), device=dev, dtype=torch.float32)
+            dYT = H.cast(dY2, T)
+    # weight gradient transposed, [i][j*D + o]: one row per input channel for the
+    # per-channel weight-norm backward (no permute of the 16 x D x D gradient)
+    dWupT = H.gemm(outsT[-1].reshape(M, D), dYT, transA=True)         # (D, k*D)
+    # bias gradient: summed by the MLP's dTab pass when dY is its untouched d(upper)
+    cs = getattr(dY, '_srnn_colsum', None)
+    if cs is not None and cs[1] == dY._version and cs[2] == k and cs[0].numel() == k * D:
+        db_up = cs[0]
+        _STATS['fused_colsum'] += 1
+    else:
+        db_up = H.colsum(dY2, M, k * D)
+    dX = H.gemm(dYT, W_up.reshape(k * D, D))                          # (M, D)
+    g_up = nn.convt_grad_to_params(mod.upsampling.conv_t, dWupT)
+    g_up_b = H.permute3(db_up.reshape(1, k, D), (0, 2, 1)).reshape(D, k)
+    # --- GRU layers, top layer first
+    g_rnn = [None] * L
+    dh_in = [None] * L
+    for l in reversed(range(L)):
+        dOut = dX.reshape(B, Fr, D)
+        # W_hh^T (D, 3D): k-contiguous operand for the deep-ring backward kernel, straight
+        # from the fp32 parameter (the same bf16 values as the forward's copy, no cast pass)
+        WhhT = H.permute3(WhhF[l].detach().reshape(1, 3 * D, D), (0, 2, 1), dtype=T)
+        xbw = H.gru_xcd_bwd_work_bytes(T, B, D) if lp else 0
+        seq = lp and (xbw > 0 or H.gru_seq_supported(T, B, D))
+        ddir = [torch.empty((B, D), device=dev, dtype=torch.float32) for _ in range(2)]
+        dGIT = bsum = None
+        if xbw > 0:
+            # the sweep writes bf16 dgh / dgi (the GEMM operands) and per-row bias sums;
+            # no fp32 copies of either
+            dGH = dGI = None
+            dGHT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T)
+            dGIT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T)
+            bsum = torch.empty((B, 4 * D), device=dev, dtype=torch.float32)
+        else:
+            dGH = torch.empty((B, Fr, 3 * D), device=dev, dtype=torch.float32)
+            dGHT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T) if lp else dGH
+            dGI = torch.empty((B, Fr, 3 * D), device=dev, dtype=torch.float32)
+        if seq:
+            H.before_persistent_sweep()   # (DP: in-flight all-reduces finish first)
+        if xbw > 0:
+            # reverse sweep in one persistent launch, row groups per XCD, W_hh^T in VGPRs
+            work = torch.empty(xbw, device=dev, dtype=torch.uint8)
+            dOutc = dOut.contiguous()
+            _STATS['gru_xcd_bwd'] += 1
+            ev = H.roof_begin()
+            H.lib().call('srnn_gru_xcd_bwd2', H.dcode(T), B, D, Fr, H.ptr(dOutc), Fr * D, D,
+                         H.ptr(gates[l]), Fr * 4 * D, 4 * D, H.ptr(outs[l]), Fr * D, D,
+                         H.ptr(h_in[l]), H.ptr(WhhT), None, H.ptr(dGHT), None, H.ptr(dGIT),
+                         H.ptr(bsum), Fr * 3 * D, 3 * D, H.ptr(ddir[0]), H.ptr(work), xbw,
+                         st())
+            # (the dgh_{t+1} W_hh products of steps 1 .. F-1; step F-1 has none)
+            H.roof_end('gru_xcd_bwd', ev, 2.0 * B * (Fr - 1) * 3 * D * D)
+        elif seq:
+            # the whole reverse sweep in one persistent launch (W_hh^T resident in LDS)
+            work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
+            dOutc = dOut.contiguous()
+            H.lib().call('srnn_gru_seq_bwd', H.dcode(T), B, D, Fr, H.ptr(dOutc), Fr * D, D,
+                         H.ptr(gates[l]), Fr * 4 * D, 4 * D, H.ptr(outs[l]), Fr * D, D,
+                         H.ptr(h_in[l]), H.ptr(WhhT), H.ptr(dGH), H.ptr(dGHT), H.ptr(dGI),
+                         Fr * 3 * D, 3 * D, H.ptr(ddir[0]), H.ptr(work), work.numel() * 4,
+                         st())
+        _STATS['gru_cell_bwd_steps'] += 0 if seq else Fr
+        for t in reversed(range(Fr)) if not seq else ():
+            nxt = t + 1 < Fr
+            if t > 0:
+                hp, ldhp = outs[l][:, t - 1], Fr * D
             else:
-                dGH = torch.empty((B, Fr, 3 * D), device=dev, dtype=torch.float32)
-                dGHT = torch.empty((B, Fr, 3 * D), device=dev, dtype=T) if lp else dGH
-                dGI = torch.empty((B, Fr, 3 * D), device=dev, dtype=torch.float32)
-            if seq:
-                H.before_persistent_sweep()   # (DP: in-flight all-reduces finish first)
-            if xbw > 0:
-                # reverse sweep in one persistent launch, row groups per XCD, W_hh^T in VGPRs
-                work = torch.empty(xbw, device=dev, dtype=torch.uint8)
-                dOutc = dOut.contiguous()
-                _STATS['gru_xcd_bwd'] += 1
-                ev = H.roof_begin()
-                H.lib().call('srnn_gru_xcd_bwd2', H.dcode(T), B, D, Fr, H.ptr(dOutc), Fr * D, D,
-                             H.ptr(gates[l]), Fr * 4 * D, 4 * D, H.ptr(outs[l]), Fr * D, D,
-                             H.ptr(h_in[l]), H.ptr(WhhT), None, H.ptr(dGHT), None, H.ptr(dGIT),
-                             H.ptr(bsum), Fr * 3 * D, 3 * D, H.ptr(ddir[0]), H.ptr(work), xbw,
-                             st())
-                # (the dgh_{t+1} W_hh products of steps 1 .. F-1; step F-1 has none)
-                H.roof_end('gru_xcd_bwd', ev, 2.0 * B * (Fr - 1) * 3 * D * D)
-            elif seq:
-                # the whole reverse sweep in one persistent launch (W_hh^T resident in LDS)
-                work = torch.empty(64 * ((B + 31) // 32) + 1, device=dev, dtype=torch.int32)
-                dOutc = dOut.contiguous()
-                H.lib().call('srnn_gru_seq_bwd', H.dcode(T), B, D, Fr, H.ptr(dOutc), Fr * D, D,
-                             H.ptr(gates[l]), Fr * 4 * D, 4 * D, H.ptr(outs[l]), Fr * D, D,
-                             H.ptr(h_in[l]), H.ptr(WhhT), H.ptr(dGH), H.ptr(dGHT), H.ptr(dGI),
-                             Fr * 3 * D, 3 * D, H.ptr(ddir[0]), H.ptr(work), work.numel() * 4,
-                             st())
-            _STATS['gru_cell_bwd_steps'] += 0 if seq else Fr
-            for t in reversed(range(Fr)) if not seq else ():
-                nxt = t + 1 < Fr
-                if t > 0:
-                    hp, ldhp = outs[l][:, t - 1], Fr * D
-                else:
-                    hp, ldhp = h_in[l], D
-                H.lib().call('srnn_gru_cell_bwd', H.dcode(T), B, D, H.ptr(dOut[:, t]), Fr * D,
-                             H.ptr(dGHT[:, t + 1]) if nxt else None, Fr * 3 * D,
-                             H.ptr(ddir[(t + 1) % 2]) if nxt else None, H.ptr(Whh[l]),
-                             H.ptr(WhhT), H.ptr(gates[l][:, t]), Fr * 4 * D, H.ptr(hp), ldhp,
-                             H.ptr(dGH[:, t]), Fr * 3 * D,
-                             H.ptr(dGHT[:, t]) if lp else None, Fr * 3 * D,
-                             H.ptr(dGI[:, t]), Fr * 3 * D, H.ptr(ddir[t % 2]), st())
-            # dh_0 = dgh_0 . W_hh + dh_direct, as an NT product on W_hh^T (skinny ring path)
-            dh_in[l] = H.gemm(dGHT[:, 0], WhhT, transB=True, M=B, N=D, K=3 * D,
-                              lda=Fr * 3 * D, ldb=3 * D, cin=ddir[0], beta=1.0)
-            # previous hidden states of every step: [h_in, out[:, :F-1]] (written by the
-            # persistent forward sweep when it ran, else built here)
-            hprevT = hprevs[l]
-            if hprevT is None:
-                hprevT = torch.empty((B, Fr, D), device=dev, dtype=T)
-                H.lib().call('srnn_copy2d', H.F32, H.dcode(T), B, D, H.ptr(h_in[l]), D,
-                             H.ptr(hprevT), Fr * D, st())
-                if Fr > 1:
-                    H.lib().call('srnn_copy2d', H.dcode(T), H.dcode(T), B, (Fr - 1) * D,
-                                 H.ptr(outsT[l]), Fr * D, H.ptr(hprevT[:, 1:]), Fr * D, st())
-            dW_hh = H.gemm(dGHT.reshape(M, 3 * D), hprevT.reshape(M, D), transA=True)
-            if bsum is not None:
-                bs = H.colsum(bsum, B, 4 * D)               # sums of [dar | daz | dghn | dan]
-                db_hh = bs[:3 * D]
-                db_ih = torch.cat([bs[:2 * D], bs[3 * D:]])
-                dGIT = dGIT.reshape(M, 3 * D)
-            else:
-                dGH2, dGI2 = dGH.reshape(M, 3 * D), dGI.reshape(M, 3 * D)
-                db_hh = H.colsum(dGH2, M, 3 * D)
-                dGIT = H.cast(dGI2, T)
-                db_ih = H.colsum(dGI2, M, 3 * D)
-            dW_ih = H.gemm(dGIT, xs[l], transA=True)
-            dX = H.gemm(dGIT, Wih[l])                                     # (M, D)
-            g_rnn[l] = [dW_ih, dW_hh, db_ih, db_hh]
-        # --- input projections
-        dx0 = dX
-        dx0T = H.cast(dx0, T)
-        dW_ie = H.gemm(dx0T, prevT, transA=True)                         # (D, nfs)
-        g_ie = nn.weight_grad_to_params(mod.input_expand, dW_ie.reshape(D, nfs, 1))
-        g_ie_b = H.colsum(dx0, M, D)
-        d_upper = dx0.reshape(B, Fr, D) if ctx.has_upper else None
-        if d_upper is not None and dx0T is not dx0:
-            d_upper._srnn_lp = (dx0T, d_upper._version)     # (the upper tier's dY cast)
-        grads = g_ie + [g_ie_b]
-        if mod.is_cond:
-            C = condT.shape[1]
-            S = spk_embT.shape[1]
-            dW_c = H.gemm(dx0T, condT, transA=True)                      # (D, C)
-            grads += nn.weight_grad_to_params(mod.cond_expand, dW_c.reshape(D, C, 1))
-            grads += [g_ie_b.clone()]                                    # cond bias grad
-            dspk = torch.empty((B, D), device=dev, dtype=torch.float32)
-            H.lib().call('srnn_segsum', H.ptr(dx0), D, B, Fr, D, H.ptr(dspk), st())
-            dspkT = H.cast(dspk, T)
-            dW_s = H.gemm(dspkT, spk_embT, transA=True)                  # (D, S)
-            db_s = H.colsum(dspk, B, D)
-            demb = H.gemm(dspkT, W_s)                                    # (B, S)
-            dE = torch.zeros((S, S), device=dev, dtype=torch.float32)
-            H.lib().call('srnn_scatter_add_rows', H.ptr(dE), S, H.ptr(spk_flat), B, S,
-                         H.ptr(demb), S, st())
-            grads += [dE]
-            grads += nn.weight_grad_to_params(mod.spk_expand, dW_s.reshape(D, S, 1))
-            grads += [db_s]
-        for l in range(L):
-            grads += g_rnn[l]
-        grads += g_up + [g_up_b]
-        dh0 = None
-        if ctx.reset and ctx.needs_input_grad[6]:
-            dh0 = torch.stack([H.colsum(dh_in[l], B, D) for l in range(L)], 0)
-        return (None, None, d_upper, None, None, None, dh0) + tuple(grads)
+                hp, ldhp = h_in[l], D
+            H.lib().call('srnn_gru_cell_bwd', H.dcode(T), B, D, H.ptr(dOut[:, t]), Fr * D,
+                         H.ptr(dGHT[:, t + 1]) if nxt else None, Fr * 3 * D,
+                         H.ptr(ddir[(t + 1) % 2]) if nxt else None, H.ptr(Whh[l]),
+                         H.ptr(WhhT), H.ptr(gates[l][:, t]), Fr * 4 * D, H.ptr(hp), ldhp,
+                         H.ptr(dGH[:, t]), Fr * 3 * D,
+                         H.ptr(dGHT[:, t]) if lp else None, Fr * 3 * D,
+                         H.ptr(dGI[:, t]), Fr * 3 * D, H.ptr(ddir[t % 2]), st())
+        # dh_0 = dgh_0 . W_hh + dh_direct, as an NT product on W_hh^T (skinny ring path)
+        dh_in[l] = H.gemm(dGHT[:, 0], WhhT, transB=True, M=B, N=D, K=3 * D,
+                          lda=Fr * 3 * D, ldb=3 * D, cin=ddir[0], beta=1.0)
+        # previous hidden states of every step: [h_in, out[:, :F-1]] (written by the
+        # persistent forward sweep when it ran, else built here)
+        hprevT = hprevs[l]
+        if hprevT is None:
+            hprevT = torch.empty((B, Fr, D), device=dev, dtype=T)
+            H.lib().call('srnn_copy2d', H.F32, H.dcode(T), B, D, H.ptr(h_in[l]), D,
+                         H.ptr(hprevT), Fr * D, st())
+            if Fr > 1:
+                H.lib().call('srnn_copy2d', H.dcode(T), H.dcode(T), B, (Fr - 1) * D,
+                             H.ptr(outsT[l]), Fr * D, H.ptr(hprevT[:, 1:]), Fr * D, st())
+        dW_hh = H.gemm(dGHT.reshape(M, 3 * D), hprevT.reshape(M, D), transA=True)
+        if bsum is not None:
+            bs = H.colsum(bsum, B, 4 * D)               # sums of [dar | daz | dghn | dan]
+            db_hh = bs[:3 * D]
+            db_ih = torch.cat([bs[:2 * D], bs[3 * D:]])
+            dGIT = dGIT.reshape(M, 3 * D)
+        else:
+            dGH2, dGI2 = dGH.reshape(M, 3 * D), dGI.reshape(M, 3 * D)
+            db_hh = H.colsum(dGH2, M, 3 * D)
+            dGIT = H.cast(dGI2, T)
+            db_ih = H.colsum(dGI2, M, 3 * D)
+        dW_ih = H.gemm(dGIT, xs[l], transA=True)
+        dX = H.gemm(dGIT, Wih[l])                                     # (M, D)
+        g_rnn[l] = [dW_ih, dW_hh, db_ih, db_hh]
+    # --- input projections
+    dx0 = dX
+    dx0T = H.cast(dx0, T)
+    dW_ie = H.gemm(dx0T, prevT, transA=True)                         # (D, nfs)
+    g_ie = nn.weight_grad_to_params(mod.input_expand, dW_ie.reshape(D, nfs, 1))
+    g_ie_b = H.colsum(dx0, M, D)
+    d_upper = dx0.reshape(B, Fr, D) if ctx.has_upper else None
+    if d_upper is not None and dx0T is not dx0:
+        d_upper._srnn_lp = (dx0T, d_upper._version)     # (the upper tier's dY cast)
+    grads = g_ie + [g_ie_b]
+    if mod.is_cond:
+        C = condT.shape[1]
+        S = spk_embT.shape[1]
+        dW_c = H.gemm(dx0T, condT, transA=True)                      # (D, C)
+        grads += nn.weight_grad_to_params(mod.cond_expand, dW_c.reshape(D, C, 1))
+        grads += [g_ie_b.clone()]                                    # cond bias grad
+        dspk = torch.empty((B, D), device=dev, dtype=torch.float32)
+        H.lib().call('srnn_segsum', H.ptr(dx0), D, B, Fr, D, H.ptr(dspk), st())
+        dspkT = H.cast(dspk, T)
+        dW_s = H.gemm(dspkT, spk_embT, transA=True)                  # (D, S)
+        db_s = H.colsum(dspk, B, D)
+        demb = H.gemm(dspkT, W_s)                                    # (B, S)
+        dE = torch.zeros((S, S), device=dev, dtype=torch.float32)
+        H.lib().call('srnn_scatter_add_rows', H.ptr(dE), S, H.ptr(spk_flat), B, S,
+                     H.ptr(demb), S, st())
+        grads += [dE]
+        grads += nn.weight_grad_to_params(mod.spk_expand, dW_s.reshape(D, S, 1))
+        grads += [db_s]
+    for l in range(L):
+        grads += g_rnn[l]
+    grads += g_up + [g_up_b]
+    dh0 = None
+    if ctx.reset and need_h0:
+        dh0 = torch.stack([H.colsum(dh_in[l], B, D) for l in range(L)], 0)
+    return d_upper, dh0, grads
 
 
 class SampleLevelMLP(torch.nn.Module):
@@ -548,7 +633,8 @@ class SampleLevelMLP(torch.nn.Module):
         u = upper_tier_conditioning
         if u.dtype not in (torch.float32, _dt(self)):
             u = u.float()
-        return _MlpFn.apply(self, x, u.contiguous(), *self._param_list())
+        # the registered op srnn::mlp_fwd (custom_ops.py; autograd: srnn::mlp_bwd)
+        return custom_ops.mlp(x, u.contiguous(), self._param_list(), mlp_meta(self))
 
 
 def _build_tab(mlp, T):
@@ -562,122 +648,115 @@ def _build_tab(mlp, T):
     return tab, Wp, ET
 
 
-class _MlpFn(torch.autograd.Function):
+def mlp_forward(mlp, x, upper, ps):
+    """SampleLevelMLP forward (model.py:308-325): (log-probs, state) (srnn::mlp_fwd)."""
+    T = _dt(mlp)
+    B, Tl, D = upper.shape
+    Q, FS0 = mlp.q_levels, mlp.frame_size
+    dev = upper.device
+    tab, Wp, ET = _build_tab(mlp, T)
+    a1 = torch.empty((B * Tl, D), device=dev, dtype=T)
+    upper = upper.contiguous()
+    # SRNN_MASK_BITS=1 (bf16): the ReLU masks of a1 and a2 leave the forward as bits, 16x
+    # fewer bytes for the backward's masked GEMMs to read than the activations.  Off by
+    # default: measured (MI355X, B = 128) the two masked dgrads gain 27 us each, but the
+    # hidden GEMM's bit epilogue costs 26 us and the L1 gather's 2-B bit stores 87 us.
+    bits = T == torch.bfloat16 and upper.dtype == T and D % 64 == 0 and \
+        os.environ.get('SRNN_MASK_BITS', '0') != '0'
+    m1 = m2 = None
+    if bits:
+        m1, m2 = H.relu_bits(B * Tl, D, dev), H.relu_bits(B * Tl, D, dev)
+        H.lib().call('srnn_mlp_l1_bits', H.ptr(tab), H.ptr(x), x.stride(0), 0, B, Tl,
+                     H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.ptr(m1), m1.stride(0),
+                     H.stream())
+    else:
+        H.lib().call('srnn_mlp_l1', H.dcode(T), H.ptr(tab), H.ptr(x), x.stride(0), 0, B, Tl,
+                     H.dcode(upper), H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
+    W_hid = _wcast(mlp.hidden, T).reshape(D, D)
+    W_out = _wcast(mlp.output, T).reshape(Q, D)
+    ev = H.roof_begin()
+    a2 = H.linear(a1, W_hid, bias=mlp.hidden.bias, relu=True, out_dtype=T, bits_out=m2)
+    H.roof_end('mlp_hidden_gemm', ev, 2.0 * B * Tl * D * D)
+    z = H.linear(a2, W_out, bias=mlp.output.bias)                    # (B*T, Q) fp32
+    logp = torch.empty((B * Tl, Q), device=dev, dtype=torch.float32)
+    H.lib().call('srnn_logsoftmax_nll', H.ptr(z), Q, None, 0, Tl, B * Tl, Q, None,
+                 H.ptr(logp), Q, None, H.F32, 0, 0.0, H.stream())
+    ctx = _State()
+    ctx.mlp = mlp
+    ctx.T = T
+    ctx.udt = upper.dtype
+    ctx.dims = (B, Tl, D, Q, FS0)
+    ctx.saved_tensors = (x, a1, a2, logp, Wp, ET, W_hid, W_out)
+    ctx.bits = (m1, m2)
+    return logp.reshape(B, Tl, Q), ctx
 
-    @staticmethod
-    def forward(ctx, mlp, x, upper, *ps):
-        T = _dt(mlp)
-        B, Tl, D = upper.shape
-        Q, FS0 = mlp.q_levels, mlp.frame_size
-        dev = upper.device
-        tab, Wp, ET = _build_tab(mlp, T)
-        a1 = torch.empty((B * Tl, D), device=dev, dtype=T)
-        upper = upper.contiguous()
-        # SRNN_MASK_BITS=1 (bf16): the ReLU masks of a1 and a2 leave the forward as bits, 16x
-        # fewer bytes for the backward's masked GEMMs to read than the activations.  Off by
-        # default: measured (MI355X, B = 128) the two masked dgrads gain 27 us each, but the
-        # hidden GEMM's bit epilogue costs 26 us and the L1 gather's 2-B bit stores 87 us.
-        bits = T == torch.bfloat16 and upper.dtype == T and D % 64 == 0 and \
-            os.environ.get('SRNN_MASK_BITS', '0') != '0'
-        m1 = m2 = None
-        if bits:
-            m1, m2 = H.relu_bits(B * Tl, D, dev), H.relu_bits(B * Tl, D, dev)
-            H.lib().call('srnn_mlp_l1_bits', H.ptr(tab), H.ptr(x), x.stride(0), 0, B, Tl,
-                         H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.ptr(m1), m1.stride(0),
-                         H.stream())
-        else:
-            H.lib().call('srnn_mlp_l1', H.dcode(T), H.ptr(tab), H.ptr(x), x.stride(0), 0, B, Tl,
-                         H.dcode(upper), H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
-        W_hid = _wcast(mlp.hidden, T).reshape(D, D)
-        W_out = _wcast(mlp.output, T).reshape(Q, D)
-        ev = H.roof_begin()
-        a2 = H.linear(a1, W_hid, bias=mlp.hidden.bias, relu=True, out_dtype=T, bits_out=m2)
-        H.roof_end('mlp_hidden_gemm', ev, 2.0 * B * Tl * D * D)
-        z = H.linear(a2, W_out, bias=mlp.output.bias)                    # (B*T, Q) fp32
-        logp = torch.empty((B * Tl, Q), device=dev, dtype=torch.float32)
-        H.lib().call('srnn_logsoftmax_nll', H.ptr(z), Q, None, 0, Tl, B * Tl, Q, None,
-                     H.ptr(logp), Q, None, H.F32, 0, 0.0, H.stream())
-        ctx.mlp = mlp
-        ctx.T = T
-        ctx.udt = upper.dtype
-        ctx.dims = (B, Tl, D, Q, FS0)
-        ctx.save_for_backward(x, a1, a2, logp, Wp, ET, W_hid, W_out)
-        ctx.bits = (m1, m2)
-        out = logp.reshape(B, Tl, Q)
-        # (nn.sequence_nll_loss_bits on this output hands its gradient back in closed form)
-        ctx.tok = nn.FusedNllToken()
-        out._srnn_nll_token = ctx.tok
-        return out
 
-    @staticmethod
-    def backward(ctx, dlogp):
-        mlp = ctx.mlp
-        T = ctx.T
-        B, Tl, D, Q, FS0 = ctx.dims
-        x, a1, a2, logp, Wp, ET, W_hid, W_out = ctx.saved_tensors
-        dev = logp.device
-        st = H.stream
-        M = B * Tl
-        dz = torch.empty((M, Q), device=dev, dtype=T)
-        nll = getattr(dlogp, '_srnn_nll', None)
-        if nll is not None:
-            # loss gradient in closed form (nn._NllBitsFn): fused NLL + log-softmax backward,
-            # dz = c (exp(logp) - onehot) straight into the GEMM operand dtype
-            tg, Tt, gscale, gd = nll
-            H.lib().call('srnn_nll_logsoftmax_bwd', H.ptr(tg), Tt, Tt, M, Q, H.ptr(logp), Q,
-                         gscale, H.ptr(gd), H.ptr(dz), H.dcode(T), Q, st())
-        else:
-            if ctx.tok.emitted:
-                raise RuntimeError('the fused NLL gradient of the MLP log-probs was combined '
-                                   'with another gradient (log-probs used twice); run with '
-                                   'SRNN_FUSED_NLL=0')
-            dl = dlogp.reshape(M, Q).float().contiguous()
-            H.lib().call('srnn_logsoftmax_bwd', H.ptr(dl), Q, H.ptr(logp), Q, M, Q, H.ptr(dz),
-                         H.dcode(T), Q, st())
-        dW_out = H.gemm(dz, a2, transA=True)                             # (Q, D)
-        db_out = H.colsum(dz, M, Q)
-        m1, m2 = ctx.bits
-        ctx.bits = None
-        if m2 is not None:
-            da2 = H.gemm(dz, W_out, mask_bits=m2, out_dtype=T)           # (M, D)
-        else:
-            da2 = H.gemm(dz, W_out, mask=a2, out_dtype=T)                # (M, D)
-        dW_hid = H.gemm(da2, a1, transA=True)                            # (D, D)
-        db_hid = H.colsum(da2, M, D)
-        # d(upper) in upper's dtype: bf16 when the bottom tier hands the MLP a bf16 upper
-        if m1 is not None:
-            da1 = H.gemm(da2, W_hid, mask_bits=m1, out_dtype=ctx.udt)     # (M, D)
-        else:
-            da1 = H.gemm(da2, W_hid, mask=a1, out_dtype=ctx.udt)          # (M, D)
-        # folded embedding . conv backward: dTab[q][k][:] += da1[t] for x_{t+k} = q
-        dtabT = torch.empty((Q, FS0 * D), device=dev, dtype=T)
-        work = torch.empty(Q * FS0 * D, device=dev, dtype=torch.int64)
-        # the same pass sums da1 over rows t = j (mod FS0): the bottom tier's upsampling bias
-        # gradient (its output is this layer's `upper`), handed over on the returned gradient
-        colsum = torch.empty(FS0 * D, device=dev, dtype=torch.float32)
-        done = ctypes.c_int(0)
-        ev = H.roof_begin()
-        H.lib().call('srnn_mlp_dtab2', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.stride(0), 0, B,
-                     Tl, H.ptr(dtabT), H.dcode(T), D, FS0, Q, H.ptr(work), work.numel() * 8,
-                     H.ptr(colsum), ctypes.byref(done), st())
-        # algorithmic bytes: da1 and the index window read once, dTab^T and the column sums
-        # written once
-        H.roof_end('dtab_scatter', ev, B * Tl * D * da1.element_size() +
-                   B * (Tl + FS0 - 1) * 8 + Q * FS0 * D * dtabT.element_size() + FS0 * D * 4)
-        dE = H.gemm(dtabT, Wp.reshape(FS0 * D, Q))                       # (Q, Q)
-        # dWp[k] = dTab[:, k]^T E for every tap k at once: (FS0 D, Q) = dtabT^T . ET, one GEMM
-        # (the (FS0, D, Q) result is the same memory as the per-tap batch)
-        dWp = torch.empty((FS0, D, Q), device=dev, dtype=torch.float32)
-        H.gemm(dtabT, ET, transA=True, out=dWp, M=FS0 * D, N=Q, K=Q, lda=FS0 * D, ldb=Q, ldc=Q)
-        dW_in = H.permute3(dWp, (1, 2, 0))                               # (D, Q, FS0)
-        grads = [dE]
-        grads += nn.weight_grad_to_params(mlp.input, dW_in)
-        grads += nn.weight_grad_to_params(mlp.hidden, dW_hid.reshape(D, D, 1)) + [db_hid]
-        grads += nn.weight_grad_to_params(mlp.output, dW_out.reshape(Q, D, 1)) + [db_out]
-        d_upper = da1.reshape(B, Tl, D)
-        if done.value:
-            d_upper._srnn_colsum = (colsum, d_upper._version, FS0)
-        return (None, None, d_upper) + tuple(grads)
+def mlp_backward(ctx, dlogp, nll=None):
+    """Backward of mlp_forward: (d_upper, [parameter gradients]).  nll = (target, T,
+    gscale, g): the log-probs' gradient is sequence_nll_loss_bits' closed form (dlogp is then
+    not read)."""
+    mlp = ctx.mlp
+    T = ctx.T
+    B, Tl, D, Q, FS0 = ctx.dims
+    x, a1, a2, logp, Wp, ET, W_hid, W_out = ctx.saved_tensors
+    dev = logp.device
+    st = H.stream
+    M = B * Tl
+    dz = torch.empty((M, Q), device=dev, dtype=T)
+    if nll is not None:
+        # loss gradient in closed form (custom_ops nll_bits): fused NLL + log-softmax
+        # backward, dz = c (exp(logp) - onehot) straight into the GEMM operand dtype
+        tg, Tt, gscale, gd = nll
+        H.lib().call('srnn_nll_logsoftmax_bwd', H.ptr(tg), Tt, Tt, M, Q, H.ptr(logp), Q,
+                     gscale, H.ptr(gd), H.ptr(dz), H.dcode(T), Q, st())
+    else:
+        dl = dlogp.reshape(M, Q).float().contiguous()
+        H.lib().call('srnn_logsoftmax_bwd', H.ptr(dl), Q, H.ptr(logp), Q, M, Q, H.ptr(dz),
+                     H.dcode(T), Q, st())
+    dW_out = H.gemm(dz, a2, transA=True)                             # (Q, D)
+    db_out = H.colsum(dz, M, Q)
+    m1, m2 = ctx.bits
+    ctx.bits = None
+    if m2 is not None:
+        da2 = H.gemm(dz, W_out, mask_bits=m2, out_dtype=T)           # (M, D)
+    else:
+        da2 = H.gemm(dz, W_out, mask=a2, out_dtype=T)                # (M, D)
+    dW_hid = H.gemm(da2, a1, transA=True)                            # (D, D)
+    db_hid = H.colsum(da2, M, D)
+    # d(upper) in upper's dtype: bf16 when the bottom tier hands the MLP a bf16 upper
+    if m1 is not None:
+        da1 = H.gemm(da2, W_hid, mask_bits=m1, out_dtype=ctx.udt)     # (M, D)
+    else:
+        da1 = H.gemm(da2, W_hid, mask=a1, out_dtype=ctx.udt)          # (M, D)
+    # folded embedding . conv backward: dTab[q][k][:] += da1[t] for x_{t+k} = q
+    dtabT = torch.empty((Q, FS0 * D), device=dev, dtype=T)
+    work = torch.empty(Q * FS0 * D, device=dev, dtype=torch.int64)
+    # the same pass sums da1 over rows t = j (mod FS0): the bottom tier's upsampling bias
+    # gradient (its output is this layer's `upper`), handed over on the returned gradient
+    colsum = torch.empty(FS0 * D, device=dev, dtype=torch.float32)
+    done = ctypes.c_int(0)
+    ev = H.roof_begin()
+    H.lib().call('srnn_mlp_dtab2', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.stride(0), 0, B,
+                 Tl, H.ptr(dtabT), H.dcode(T), D, FS0, Q, H.ptr(work), work.numel() * 8,
+                 H.ptr(colsum), ctypes.byref(done), st())
+    # algorithmic bytes: da1 and the index window read once, dTab^T and the column sums
+    # written once
+    H.roof_end('dtab_scatter', ev, B * Tl * D * da1.element_size() +
+               B * (Tl + FS0 - 1) * 8 + Q * FS0 * D * dtabT.element_size() + FS0 * D * 4)
+    dE = H.gemm(dtabT, Wp.reshape(FS0 * D, Q))                       # (Q, Q)
+    # dWp[k] = dTab[:, k]^T E for every tap k at once: (FS0 D, Q) = dtabT^T . ET, one GEMM
+    # (the (FS0, D, Q) result is the same memory as the per-tap batch)
+    dWp = torch.empty((FS0, D, Q), device=dev, dtype=torch.float32)
+    H.gemm(dtabT, ET, transA=True, out=dWp, M=FS0 * D, N=Q, K=Q, lda=FS0 * D, ldb=Q, ldc=Q)
+    dW_in = H.permute3(dWp, (1, 2, 0))                               # (D, Q, FS0)
+    grads = [dE]
+    grads += nn.weight_grad_to_params(mlp.input, dW_in)
+    grads += nn.weight_grad_to_params(mlp.hidden, dW_hid.reshape(D, D, 1)) + [db_hid]
+    grads += nn.weight_grad_to_params(mlp.output, dW_out.reshape(Q, D, 1)) + [db_out]
+    d_upper = da1.reshape(B, Tl, D)
+    if done.value:
+        d_upper._srnn_colsum = (colsum, d_upper._version, FS0)
+    return d_upper, grads
 
 
 class Runner:
@@ -735,23 +814,16 @@ class Predictor(Runner, torch.nn.Module):
 
 
 def generation_weights(model, dtype=None):
-    """Folded, device-resident weight layouts for srnn_generate (weight-norm applied once)."""
+    """Folded, device-resident weight layouts for srnn::generate (weight-norm applied once):
+    (tensors, meta) -- srnn_model_struct(tensors, meta) rebuilds the C ABI's SrnnModel."""
     T = dtype or model.compute_dtype
     D = model.dim
-    keep = []
-    m = H.SrnnModel()
-    m.n_tiers = len(model.frame_level_rnns)
-    m.n_rnn = model.n_rnn
-    m.dim = D
-    m.q_levels = model.q_levels
-    m.cond_dim = model.cond_dim
-    m.dtype = H.dcode(T)
+    ws = []
+    meta = [len(model.frame_level_rnns), model.n_rnn, D, model.q_levels, model.cond_dim,
+            H.dcode(T)]
     with torch.no_grad():
         for k, rnn in enumerate(model.frame_level_rnns):
-            t = m.tier[k]
             nfs = rnn.n_frame_samples
-            t.frame_size = rnn.frame_size
-            t.n_frame_samples = nfs
             W_ie = nn.weight_of(rnn.input_expand).reshape(D, nfs)
             if rnn.is_cond:
                 C = model.cond_dim
@@ -761,39 +833,48 @@ def generation_weights(model, dtype=None):
                              nfs, H.ptr(w_in), nfs + C, H.stream())
                 H.lib().call('srnn_copy2d', H.F32, H.dcode(T), D, C, H.ptr(W_c.contiguous()), C,
                              H.ptr(w_in[:, nfs:]), nfs + C, H.stream())
-                t.in_dim = nfs + C
+                meta += [rnn.frame_size, nfs, nfs + C, 0]
+                ws.append(w_in)
             else:
-                w_in = H.cast(W_ie.contiguous(), T)
-                t.in_dim = nfs
-                b_in = rnn.input_expand.bias.detach().contiguous()
-                keep.append(b_in)
-                t.b_in = H.ptr(b_in)
-            keep.append(w_in)
-            t.w_in = H.ptr(w_in)
+                meta += [rnn.frame_size, nfs, nfs, 1]
+                ws += [H.cast(W_ie.contiguous(), T), rnn.input_expand.bias.detach().contiguous()]
             for l in range(model.n_rnn):
-                wih = H.cast(getattr(rnn.rnn, 'weight_ih_l%d' % l).detach().contiguous(), T)
-                whh = H.cast(getattr(rnn.rnn, 'weight_hh_l%d' % l).detach().contiguous(), T)
-                bih = getattr(rnn.rnn, 'bias_ih_l%d' % l).detach().contiguous()
-                bhh = getattr(rnn.rnn, 'bias_hh_l%d' % l).detach().contiguous()
-                keep += [wih, whh, bih, bhh]
-                t.w_ih[l], t.w_hh[l] = H.ptr(wih), H.ptr(whh)
-                t.b_ih[l], t.b_hh[l] = H.ptr(bih), H.ptr(bhh)
+                ws += [H.cast(getattr(rnn.rnn, 'weight_ih_l%d' % l).detach().contiguous(), T),
+                       H.cast(getattr(rnn.rnn, 'weight_hh_l%d' % l).detach().contiguous(), T),
+                       getattr(rnn.rnn, 'bias_ih_l%d' % l).detach().contiguous(),
+                       getattr(rnn.rnn, 'bias_hh_l%d' % l).detach().contiguous()]
             k_ = rnn.frame_size
-            w_up = nn.convt_operand(rnn.upsampling.conv_t, T)
-            b_up = H.permute3(rnn.upsampling.bias.detach().reshape(1, D, k_), (0, 2, 1))
-            h0 = rnn.h0.detach().float().contiguous()
-            keep += [w_up, b_up, h0]
-            t.w_up, t.b_up, t.h0 = H.ptr(w_up), H.ptr(b_up), H.ptr(h0)
+            ws += [nn.convt_operand(rnn.upsampling.conv_t, T),
+                   H.permute3(rnn.upsampling.bias.detach().reshape(1, D, k_), (0, 2, 1)),
+                   rnn.h0.detach().float().contiguous()]
         mlp = model.sample_level_mlp
-        tab = mlp.tab(T)
-        w_hid = H.cast(nn.weight_of(mlp.hidden).reshape(D, D).contiguous(), T)
-        w_out = H.cast(nn.weight_of(mlp.output).reshape(model.q_levels, D).contiguous(), T)
-        b_hid = mlp.hidden.bias.detach().contiguous()
-        b_out = mlp.output.bias.detach().contiguous()
-        keep += [tab, w_hid, w_out, b_hid, b_out]
-        m.tab, m.w_hid, m.w_out = H.ptr(tab), H.ptr(w_hid), H.ptr(w_out)
-        m.b_hid, m.b_out = H.ptr(b_hid), H.ptr(b_out)
-    return m, keep
+        ws += [mlp.tab(T), H.cast(nn.weight_of(mlp.hidden).reshape(D, D).contiguous(), T),
+               mlp.hidden.bias.detach().contiguous(),
+               H.cast(nn.weight_of(mlp.output).reshape(model.q_levels, D).contiguous(), T),
+               mlp.output.bias.detach().contiguous()]
+    meta.append(model.lookback)
+    return ws, meta
+
+
+def srnn_model_struct(ws, meta):
+    """The C ABI's SrnnModel (include/samplernn_hip.h) over generation_weights' tensors."""
+    m = H.SrnnModel()
+    m.n_tiers, m.n_rnn, m.dim, m.q_levels, m.cond_dim, m.dtype = [int(v) for v in meta[:6]]
+    it = iter(ws)
+    for k in range(m.n_tiers):
+        t = m.tier[k]
+        t.frame_size, t.n_frame_samples, t.in_dim, has_b = [int(v) for v in
+                                                            meta[6 + 4 * k: 10 + 4 * k]]
+        t.w_in = H.ptr(next(it))
+        if has_b:
+            t.b_in = H.ptr(next(it))
+        for l in range(m.n_rnn):
+            t.w_ih[l], t.w_hh[l] = H.ptr(next(it)), H.ptr(next(it))
+            t.b_ih[l], t.b_hh[l] = H.ptr(next(it)), H.ptr(next(it))
+        t.w_up, t.b_up, t.h0 = H.ptr(next(it)), H.ptr(next(it)), H.ptr(next(it))
+    m.tab, m.w_hid, m.b_hid = H.ptr(next(it)), H.ptr(next(it)), H.ptr(next(it))
+    m.w_out, m.b_out = H.ptr(next(it)), H.ptr(next(it))
+    return m
 
 
 def top_row_bias(model, spk):
@@ -857,23 +938,18 @@ class Generator(Runner):
         L = model.lookback
         T = num_cond * L
         Q = model.q_levels
-        m, keep = generation_weights(model, dtype)
+        weights, meta = generation_weights(model, dtype)
         row_bias = top_row_bias(model, spk)
-        seq = torch.full((n_seqs, L + T), utils.q_zero(Q), dtype=torch.long, device=dev)
         if noise is None and sampler == 'torch':
             noise = torch.empty(T, n_seqs, Q).exponential_(1)
         if noise is not None:
             noise = torch.as_tensor(noise).to(dev, torch.float32).contiguous()
             assert noise.shape == (T, n_seqs, Q), 'noise must be (T, n_seqs, Q)'
-        logp = torch.empty((T, n_seqs, Q), device=dev) if return_logp else None
-        sz = ctypes.c_size_t(0)
-        H.lib().call('srnn_gen_workspace_size', ctypes.byref(m), n_seqs, ctypes.byref(sz))
-        ws = torch.empty(sz.value, device=dev, dtype=torch.uint8)
-        H.lib().call('srnn_generate2', ctypes.byref(m), n_seqs, num_cond, H.ptr(cond),
-                     H.ptr(row_bias), H.ptr(noise), int(seed) & ((1 << 64) - 1),
-                     int(row_offset), H.ptr(seq), H.ptr(logp), H.ptr(ws), sz.value,
-                     (1 if use_graph else 0) | (0 if persistent else 2), H.stream())
-        del keep
+        # the registered op srnn::generate (custom_ops.py): the whole sample loop on the device
+        seq, logp = torch.ops.srnn.generate(
+            weights, meta, cond, row_bias, noise, int(seed) & ((1 << 63) - 1), int(row_offset),
+            (1 if use_graph else 0) | (0 if persistent else 2), bool(return_logp))
+        assert utils.q_zero(Q) == Q // 2
         self.last_sequences = seq
         out = model.dequantize(seq[:, L:], Q).cpu()
         if return_logp:

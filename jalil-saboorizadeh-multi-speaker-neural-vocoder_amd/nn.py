@@ -73,42 +73,51 @@ def apply_weight_norm(module, name='weight'):
     return module
 
 
-class _UpsampleFn(torch.autograd.Function):
-    """out[b, o, t*k + j] = sum_i x[b, i, t] W[i, o, j] + bias[o, j]  as one GEMM."""
+class _ConvT:
+    """conv_t's parameters as weight_of / weight_grad_to_params see them."""
 
-    @staticmethod
-    def forward(ctx, mod, x, *params):
-        B, Cin, Lx = x.shape
-        k = mod.conv_t.kernel_size[0]
-        Cout = mod.conv_t.out_channels
-        W = weight_of(mod.conv_t)                                  # (Cin, Cout, k)
-        Wg = H.permute3(W, (2, 1, 0))                              # (k*Cout, Cin)
-        xr = H.permute3(x.float(), (0, 2, 1)).reshape(B * Lx, Cin)  # (B*L, Cin)
-        bias = None
-        if mod.bias is not None:
-            bias = H.permute3(mod.bias.reshape(1, Cout, k), (0, 2, 1)).reshape(-1)
-        y = H.linear(xr, Wg.reshape(k * Cout, Cin), bias=bias)     # (B*L, k*Cout)
-        out = H.permute3(y.reshape(B, Lx * k, Cout), (0, 2, 1))     # (B, Cout, L*k)
-        ctx.mod = mod
-        ctx.save_for_backward(xr, Wg)
-        ctx.shape = (B, Cin, Lx, k, Cout)
-        return out
+    def __init__(self, ts):
+        if len(ts) == 2:
+            self.weight_g, self.weight_v = ts
+        else:
+            self.weight = ts[0]
 
-    @staticmethod
-    def backward(ctx, dout):
-        mod = ctx.mod
-        xr, Wg = ctx.saved_tensors
-        B, Cin, Lx, k, Cout = ctx.shape
-        dy = H.permute3(dout.float().contiguous(), (0, 2, 1)).reshape(B * Lx, k * Cout)
-        dWg = H.gemm(dy, xr, transA=True)                          # (k*Cout, Cin)
-        dx = H.gemm(dy, Wg.reshape(k * Cout, Cin))                 # (B*L, Cin)
-        dx = H.permute3(dx.reshape(B, Lx, Cin), (0, 2, 1))
-        dW = H.permute3(dWg.reshape(k, Cout, Cin), (2, 1, 0))      # (Cin, Cout, k)
-        grads = weight_grad_to_params(mod.conv_t, dW)
-        if mod.bias is not None:
-            db = H.colsum(dy, B * Lx, k * Cout)
-            grads.append(H.permute3(db.reshape(1, k, Cout), (0, 2, 1)).reshape(Cout, k))
-        return (None, dx) + tuple(grads)
+
+def upsample_forward(x, params, k, wn, has_bias):
+    """out[b, o, t*k + j] = sum_i x[b, i, t] W[i, o, j] + bias[o, j] as one GEMM (nn.py:33-43):
+    (out, state for upsample_backward) -- srnn::upsample."""
+    conv = _ConvT(params[:2] if wn else params[:1])
+    bias_p = params[-1] if has_bias else None
+    B, Cin, Lx = x.shape
+    W = weight_of(conv)                                        # (Cin, Cout, k)
+    Cout = W.shape[1]
+    Wg = H.permute3(W, (2, 1, 0))                              # (k*Cout, Cin)
+    xr = H.permute3(x.float(), (0, 2, 1)).reshape(B * Lx, Cin)  # (B*L, Cin)
+    bias = None
+    if bias_p is not None:
+        bias = H.permute3(bias_p.reshape(1, Cout, k), (0, 2, 1)).reshape(-1)
+    y = H.linear(xr, Wg.reshape(k * Cout, Cin), bias=bias)     # (B*L, k*Cout)
+    out = H.permute3(y.reshape(B, Lx * k, Cout), (0, 2, 1))     # (B, Cout, L*k)
+    st = _ConvT([])
+    st.conv, st.has_bias, st.xr, st.Wg = conv, has_bias, xr, Wg
+    st.shape = (B, Cin, Lx, k, Cout)
+    return out, st
+
+
+def upsample_backward(st, dout):
+    """(dx, [parameter gradients]) of upsample_forward -- srnn::upsample_bwd."""
+    xr, Wg = st.xr, st.Wg
+    B, Cin, Lx, k, Cout = st.shape
+    dy = H.permute3(dout.float().contiguous(), (0, 2, 1)).reshape(B * Lx, k * Cout)
+    dWg = H.gemm(dy, xr, transA=True)                          # (k*Cout, Cin)
+    dx = H.gemm(dy, Wg.reshape(k * Cout, Cin))                 # (B*L, Cin)
+    dx = H.permute3(dx.reshape(B, Lx, Cin), (0, 2, 1))
+    dW = H.permute3(dWg.reshape(k, Cout, Cin), (2, 1, 0))      # (Cin, Cout, k)
+    grads = weight_grad_to_params(st.conv, dW)
+    if st.has_bias:
+        db = H.colsum(dy, B * Lx, k * Cout)
+        grads.append(H.permute3(db.reshape(1, k, Cout), (0, 2, 1)).reshape(Cout, k))
+    return dx, grads
 
 
 class LearnedUpsampling1d(nn.Module):
@@ -133,7 +142,10 @@ class LearnedUpsampling1d(nn.Module):
     def forward(self, input):
         H.need_cuda(input)
         params = weight_params(self.conv_t) + ([self.bias] if self.bias is not None else [])
-        return _UpsampleFn.apply(self, input, *params)
+        import custom_ops
+        out, _ = torch.ops.srnn.upsample(input, params, self.conv_t.kernel_size[0],
+                                         hasattr(self.conv_t, 'weight_g'), self.bias is not None)
+        return out
 
 
 def lecun_uniform(tensor):
@@ -156,54 +168,9 @@ def concat_init(tensor, inits):
         tensor[i * fan_in: (i + 1) * fan_in, :] = chunk
 
 
-class FusedNllToken:
-    """Marks the SampleLevelMLP's log-prob output (model._MlpFn) so the NLL backward can hand
-    the MLP its loss gradient in closed form instead of a dense (B, T, Q) fp32 tensor:
-    `emitted` records that it did, so the MLP backward can tell a placeholder that autograd
-    summed with another gradient (logp used twice) from a plain dense gradient, and refuse
-    it instead of computing a wrong result."""
-    __slots__ = ('emitted',)
-
-    def __init__(self):
-        self.emitted = False
-
-
+# SRNN_FUSED_NLL=0 turns off the closed-form hand-over of the loss gradient to the MLP
+# (custom_ops: srnn::nll_bits_bwd + srnn::mlp_bwd's nll_* arguments)
 FUSED_NLL = os.environ.get('SRNN_FUSED_NLL', '1') != '0'
-
-
-class _NllBitsFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, logp, target):
-        B, T, Q = logp.shape
-        lp = logp.contiguous()
-        tg = target.reshape(B, T).contiguous()
-        rows = torch.empty(B * T, device=lp.device, dtype=torch.float32)
-        H.lib().call('srnn_nll_fwd', H.ptr(lp), Q, H.ptr(tg), T, T, B * T, H.ptr(rows), H.stream())
-        loss = H.colsum(rows, B * T, 1, alpha=LOG2E / (B * T))
-        ctx.save_for_backward(tg)
-        ctx.shape = (B, T, Q)
-        tok = getattr(logp, '_srnn_nll_token', None)
-        ctx.tok = tok if (FUSED_NLL and isinstance(tok, FusedNllToken) and Q == 256) else None
-        return loss.reshape(())
-
-    @staticmethod
-    def backward(ctx, g):
-        (tg,) = ctx.saved_tensors
-        B, T, Q = ctx.shape
-        # gscale = g * log2(e) / N  (mean reduction); g (0-d device tensor) is read on the
-        # device: no host synchronisation inside backward
-        gd = g.detach().float().reshape(1).contiguous()
-        if ctx.tok is not None:
-            # the MLP computes dz = c (exp(logp) - onehot) itself (srnn_nll_logsoftmax_bwd):
-            # hand it the target and c instead of the dense -c onehot gradient
-            d = torch.zeros((), device=tg.device, dtype=torch.float32).expand(B, T, Q)
-            d._srnn_nll = (tg, T, LOG2E / (B * T), gd)
-            ctx.tok.emitted = True
-            return d, None
-        d = torch.empty((B, T, Q), device=tg.device, dtype=torch.float32)
-        H.lib().call('srnn_nll_bwd', H.ptr(tg), T, T, B * T, Q, H.ptr(d), Q, LOG2E / (B * T),
-                     H.ptr(gd), H.stream())
-        return d, None
 
 
 def sequence_nll_loss_bits(input, target, *args, **kwargs):
@@ -211,4 +178,5 @@ def sequence_nll_loss_bits(input, target, *args, **kwargs):
     if args or kwargs:
         raise NotImplementedError('sequence_nll_loss_bits: extra nll_loss arguments')
     H.need_cuda(input, target)
-    return _NllBitsFn.apply(input, target)
+    import custom_ops
+    return custom_ops.nll_bits(input, target)          # the registered op srnn::nll_bits

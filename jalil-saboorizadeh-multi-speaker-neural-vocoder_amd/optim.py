@@ -20,9 +20,8 @@ def _fused_adam_step(optimizer, lo, hi, reduced=None):
     launch (srnn_adam_clip_multi2) instead of one launch per tensor.  reduced: the data-
     parallel gradient buckets ((param, view) pairs, dtype, 1 / world scale; distributed.py)
     read in place instead of p.grad."""
-    import ctypes
+    import custom_ops  # noqa: F401  (registers srnn::adam_clip_)
     rv = {id(p): v for p, v in reduced[0]} if reduced else None
-    gdt = reduced[1] if reduced else torch.float32
     gscale = reduced[2] if reduced else 1.0
     for group in optimizer.param_groups:
         if group.get('weight_decay', 0) != 0 or group.get('amsgrad', False) or \
@@ -47,22 +46,18 @@ def _fused_adam_step(optimizer, lo, hi, reduced=None):
             st['step'] += 1
             by_step.setdefault(int(st['step'].item()), []).append((p, st))
         for step, items in sorted(by_step.items()):
-            n = len(items)
-            arr = lambda ts: (ctypes.c_void_p * n)(  # noqa: E731
-                *[t.data_ptr() if t is not None else None for t in ts])
             # parameters with a cached bf16 copy (samplernn_hip.cast_param) get it rewritten
             # by the same kernel, so the next forward needs no cast
             shadows = [H.shadow_of(p) for p, _ in items]
             ev = H.roof_begin()
             nel = sum(p.numel() for p, _ in items)
             grads = [p.grad for p, _ in items] if rv is None else [rv.get(id(p)) for p, _ in items]
-            H.lib().call('srnn_adam_clip_multi2', n, arr([p for p, _ in items]), arr(grads),
-                         H.dcode(gdt), float(gscale), arr([s['exp_avg'] for _, s in items]),
-                         arr([s['exp_avg_sq'] for _, s in items]),
-                         arr(shadows) if any(t is not None for t in shadows) else None,
-                         (ctypes.c_int64 * n)(*[p.numel() for p, _ in items]), float(lo),
-                         float(hi), float(group['lr']), float(b1), float(b2),
-                         float(group['eps']), step, H.stream())
+            # the registered op srnn::adam_clip_ (custom_ops.py)
+            torch.ops.srnn.adam_clip_([p for p, _ in items], grads,
+                                      [s['exp_avg'] for _, s in items],
+                                      [s['exp_avg_sq'] for _, s in items], shadows,
+                                      float(gscale), float(lo), float(hi), float(group['lr']),
+                                      float(b1), float(b2), float(group['eps']), step)
             # algorithmic bytes: p, m, v read + written, the gradient read + written back
             # clamped (hardtanh_ in place, optim.py:13), the bf16 copies written
             H.roof_end('adam_clip', ev, nel * 32 + 2 * sum(

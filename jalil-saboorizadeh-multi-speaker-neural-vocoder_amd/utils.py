@@ -78,6 +78,12 @@ def uquantize(samples, q_levels):
 
 
 def _dequant(samples, q_levels, scale, mode=0):
+    """scale * dequantize(samples) on the device: the registered op srnn::dequant."""
+    import custom_ops  # noqa: F401  (registers the op)
+    return torch.ops.srnn.dequant(samples, q_levels, float(scale), mode)
+
+
+def _dequant_impl(samples, q_levels, scale, mode=0):
     if samples.is_cuda and samples.dtype == torch.long and samples.dim() == 2 and \
             samples.stride(1) == 1 and not samples.is_contiguous():
         # a window of the index stream: read in place (no copy of the slice first)

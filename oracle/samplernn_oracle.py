@@ -149,26 +149,15 @@ class OracleSampleRNN:
             x = x + s
         if h is None:                                          # model.py:224-228
             h = self.p[P + 'h0'].unsqueeze(1).expand(self.n_rnn, B, D)
-        hs = []
-        layer_in = x
-        for l in range(self.n_rnn):                            # torch.nn.GRU (model.py:148-153,244)
-            Wih = self.p[P + 'rnn.weight_ih_l%d' % l]
-            Whh = self.p[P + 'rnn.weight_hh_l%d' % l]
-            bih = self.p[P + 'rnn.bias_ih_l%d' % l]
-            bhh = self.p[P + 'rnn.bias_hh_l%d' % l]
-            gi = F.linear(layer_in, Wih, bih)                  # (B,F,3D)
-            hl = h[l]
-            outs = []
-            for t in range(Fr):
-                gh = F.linear(hl, Whh, bhh)
-                r = torch.sigmoid(gh[:, :D] + gi[:, t, :D])
-                z = torch.sigmoid(gh[:, D:2 * D] + gi[:, t, D:2 * D])
-                n = torch.tanh(gi[:, t, 2 * D:] + gh[:, 2 * D:] * r)
-                hl = (hl - n) * z + n
-                outs.append(hl)
-            layer_in = torch.stack(outs, 1)
-            hs.append(hl)
-        h_new = torch.stack(hs, 0)
+        # torch.nn.GRU (model.py:148-153, 244): the same fused ATen GRU the reference's module
+        # runs (gate order r | z | n: n = tanh(W_in x + b_in + r (W_hn h + b_hn)),
+        # h' = (1 - z) n + z h), called functionally on the state_dict tensors
+        flat = []
+        for l in range(self.n_rnn):
+            flat += [self.p[P + 'rnn.weight_ih_l%d' % l], self.p[P + 'rnn.weight_hh_l%d' % l],
+                     self.p[P + 'rnn.bias_ih_l%d' % l], self.p[P + 'rnn.bias_hh_l%d' % l]]
+        layer_in, h_new = torch._VF.gru(x, h.contiguous(), flat, True, self.n_rnn, 0.0,
+                                        torch.is_grad_enabled(), False, True)
         # LearnedUpsampling1d (nn.py:33-43): out[b,t*k+j,o] = sum_i y[b,t,i] W[i,o,j] + bias[o,j]
         W = weight_norm_w(self.p[P + 'upsampling.conv_t.weight_g'],
                           self.p[P + 'upsampling.conv_t.weight_v'])
@@ -218,7 +207,8 @@ class OracleSampleRNN:
 
         cond: (N,C) shared by all rows (reference) or (n_seqs,N,C) per row; spk: int or (n_seqs,).
         noise: (T, n_seqs, Q) Exp(1) draws, q_t consumed at step t exactly as
-        `multinomial(1)` does in torch>=2 CPU (p/q then argmax, first max).
+        `multinomial(1)` does in torch>=2 CPU (p/q then argmax, first max); None: drawn from
+        torch's CPU generator step by step, as the reference's multinomial does.
         Returns int64 sequences (n_seqs, L+T) (and logp (n_seqs,T,Q) if asked).
         """
         cond = torch.as_tensor(np.asarray(cond))
@@ -255,7 +245,8 @@ class OracleSampleRNN:
             upper = outs[0][:, i % fs0: i % fs0 + 1]         # model.py:511-513
             lp = self.mlp(seq[:, i - fs0: i], upper)[:, 0]   # model.py:504-516
             p = lp.exp()
-            seq[:, i] = torch.argmax(p / noise[i - L], dim=-1)   # model.py:517 (multinomial)
+            q = noise[i - L] if noise is not None else torch.empty(n_seqs, Q).exponential_(1)
+            seq[:, i] = torch.argmax(p / q, dim=-1)             # model.py:517 (multinomial)
             if return_logp:
                 logps.append(lp)
         if return_logp:
@@ -295,10 +286,11 @@ class OracleAdam:
             p.addcdiv_(m, denom, value=-step_size)
 
 
-def tbptt_step(model, opt, names, batch):
+def tbptt_step(model, opt, names, batch, return_grads=True):
     """Trainer.train body (trainer/__init__.py:62-117): forward, loss, backward, clip, Adam.
 
-    Returns (loss float, clipped grads list)."""
+    Returns (loss float, clipped grads list -- None without return_grads: the timed CPU
+    baseline does not pay for a copy the reference step does not make)."""
     inp, reset, tgt, cond, spk = batch
     params = [model.p[n] for n in names]
     for p in params:
@@ -308,7 +300,7 @@ def tbptt_step(model, opt, names, batch):
     loss = sequence_nll_loss_bits(logp, tgt)
     loss.backward()
     grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in params]
-    clipped = [g.clamp(-1, 1) for g in grads]
+    clipped = [g.clamp(-1, 1) for g in grads] if return_grads else None
     opt.step(grads)
     for p in params:
         p.grad = None

@@ -156,3 +156,35 @@ def test_trainer_control_flow_cpu():
     # grads clamped to [-0.5, 0.5] in place; never-used params got zero (not None) grads
     assert toy.w.grad.abs().max() <= 0.5
     assert toy.unused.grad is not None and float(toy.unused.grad.abs().sum()) == 0.0
+
+
+def test_custom_ops_registered_with_fake_kernels():
+    """Every HIP operator is a torch.library custom op (custom_ops.py) and its fake kernel
+    propagates shapes / dtypes without running HIP code (what torch.compile tracing uses)."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    import custom_ops
+    import model as M
+    for name in custom_ops.OPS:
+        assert hasattr(torch.ops.srnn, name), name
+    m = M.SampleRNN([16, 4], 1, 64, True, 256, True, True, 43, 6)
+    m.compute_dtype = torch.bfloat16
+    top, bot, mlp = m.frame_level_rnns[1], m.frame_level_rnns[0], m.sample_level_mlp
+    with FakeTensorMode(allow_non_fake_inputs=True):
+        B = 3
+        prev = torch.empty(B, 2, 64)
+        y, h, hd = torch.ops.srnn.tier_fwd(prev, None, torch.empty(B, 2, 43),
+                                           torch.zeros(B, 1, dtype=torch.long), None, top.h0,
+                                           top._param_list(), M.tier_meta(top))
+        assert tuple(y.shape) == (B, 8, 64) and y.dtype == torch.float32
+        assert tuple(h.shape) == (1, B, 64)
+        y2, _, _ = torch.ops.srnn.tier_fwd(torch.empty(B, 8, 16), y, None, None, None, bot.h0,
+                                           bot._param_list(), M.tier_meta(bot))
+        assert tuple(y2.shape) == (B, 128, 64) and y2.dtype == torch.bfloat16
+        lp, _ = torch.ops.srnn.mlp_fwd(torch.zeros(B, 143, dtype=torch.long), y2,
+                                       mlp._param_list(), M.mlp_meta(mlp))
+        assert tuple(lp.shape) == (B, 128, 256) and lp.dtype == torch.float32
+        loss = torch.ops.srnn.nll_bits(lp, torch.zeros(B, 128, dtype=torch.long))
+        assert loss.shape == ()
+        d = torch.ops.srnn.dequant(torch.zeros(B, 5, dtype=torch.long), 256, 2.0, 0)
+        assert d.dtype == torch.float32 and tuple(d.shape) == (B, 5)
