@@ -18,7 +18,7 @@ Every op has a fake (meta) kernel, so FakeTensor / torch.compile tracing sees sh
 running HIP code, and the differentiable ones have their autograd formula attached with
 torch.library.register_autograd (backward = the *_bwd op).
 
-Saved activations: a forward op returns, beside its outputs, a 1-element int64 host `handle`;
+Saved activations: a forward op returns, beside its outputs, a 0-element int64 host `handle`;
 the activations its backward needs (bf16 operand copies, GRU gates, MLP a1 / a2 / log-probs)
 stay in a per-call stash keyed by that handle and are released with the handle (when autograd
 frees the graph, or at once under no_grad).  The backward op takes the handle.  This keeps the
@@ -38,16 +38,19 @@ _NEXT = [1]
 
 
 def _stash(state):
+    """A 0-element int64 host tensor standing for `state` (its key rides as an attribute of
+    the tensor object, so the handle has no data: equal across runs for every comparison)."""
     key = _NEXT[0]
     _NEXT[0] += 1
     _STASH[key] = state
-    handle = torch.tensor([key], dtype=torch.int64)
+    handle = torch.empty(0, dtype=torch.int64)
+    handle._srnn_key = key
     weakref.finalize(handle, _STASH.pop, key, None)
     return handle
 
 
 def _take(handle):
-    st = _STASH.get(int(handle[0]))
+    st = _STASH.get(getattr(handle, '_srnn_key', None))
     if st is None:
         raise RuntimeError('srnn: saved state of this forward is gone (backward run twice '
                            'without retain_graph, or the handle was dropped)')
@@ -80,22 +83,27 @@ def _(prev, upper, cond, spk, hidden, h0, params, meta):
     ydt = torch.bfloat16 if (feeds and dt) else torch.float32
     return (prev.new_empty((B, Fr * k, D), dtype=ydt),
             prev.new_empty((L, B, D), dtype=torch.float32),
-            torch.empty(1, dtype=torch.int64, device='cpu'))
+            torch.empty(0, dtype=torch.int64, device='cpu'))
 
 
 @torch.library.custom_op('srnn::tier_bwd', mutates_args=())
-def tier_bwd(dy: Tensor, handle: Tensor, params: list[Tensor], need_h0: bool) -> list[Tensor]:
-    """[d_upper | empty, dh0 | empty, *parameter gradients (_param_list order)]."""
+def tier_bwd(dy: Tensor, handle: Tensor, params: list[Tensor], meta: list[int], need_h0: bool,
+             has_upper: bool) -> list[Tensor]:
+    """[d_upper (B, F, D) fp32 | empty, dh0 (n_rnn, D) | empty, *parameter gradients
+    (_param_list order)]."""
     import model
     d_upper, dh0, grads = model.tier_backward(_take(handle), dy, need_h0)
-    return [d_upper if d_upper is not None else _empty(), dh0 if dh0 is not None else _empty()] \
-        + list(grads)
+    return [d_upper if has_upper else _empty().to(dy.device),
+            dh0 if need_h0 else _empty().to(dy.device)] + list(grads)
 
 
 @tier_bwd.register_fake
-def _(dy, handle, params, need_h0):
-    B = dy.shape[0]
-    return [dy.new_empty((B, 0, 0)), dy.new_empty(0)] + [torch.empty_like(p) for p in params]
+def _(dy, handle, params, meta, need_h0, has_upper):
+    B, FK, D = dy.shape
+    k, L = meta[2], meta[3]
+    return [dy.new_empty((B, FK // k, D), dtype=torch.float32) if has_upper else dy.new_empty(0),
+            dy.new_empty((L, D), dtype=torch.float32) if need_h0 else dy.new_empty(0)] + \
+        [torch.empty_like(p) for p in params]
 
 
 def _tier_setup(ctx, inputs, output):
@@ -104,13 +112,15 @@ def _tier_setup(ctx, inputs, output):
     ctx.need_h0 = hidden is None and h0.requires_grad
     ctx.nparams = len(params)
     ctx.params = params
+    ctx.meta = meta
     ctx.save_for_backward(output[2])
     ctx.mark_non_differentiable(output[1], output[2])
 
 
 def _tier_backward(ctx, dy, dh_new, dhandle):
     (handle,) = ctx.saved_tensors
-    out = torch.ops.srnn.tier_bwd(dy.contiguous(), handle, ctx.params, ctx.need_h0)
+    out = torch.ops.srnn.tier_bwd(dy.contiguous(), handle, ctx.params, ctx.meta, ctx.need_h0,
+                                  ctx.has_upper)
     d_upper = out[0] if ctx.has_upper else None
     dh0 = out[1] if ctx.need_h0 else None
     return None, d_upper, None, None, None, dh0, list(out[2:]), None
@@ -138,12 +148,13 @@ def mlp_fwd(x: Tensor, upper: Tensor, params: list[Tensor],
 def _(x, upper, params, meta):
     B, Tl, _ = upper.shape
     return (upper.new_empty((B, Tl, meta[0]), dtype=torch.float32),
-            torch.empty(1, dtype=torch.int64, device='cpu'))
+            torch.empty(0, dtype=torch.int64, device='cpu'))
 
 
 @torch.library.custom_op('srnn::mlp_bwd', mutates_args=())
-def mlp_bwd(dlogp: Tensor, handle: Tensor, params: list[Tensor], nll_target: Optional[Tensor],
-            nll_scale: float, nll_g: Optional[Tensor]) -> list[Tensor]:
+def mlp_bwd(dlogp: Tensor, handle: Tensor, params: list[Tensor], meta: list[int],
+            upper_bf16: bool, nll_target: Optional[Tensor], nll_scale: float,
+            nll_g: Optional[Tensor]) -> list[Tensor]:
     """[d_upper, *parameter gradients].  nll_target given: the log-probs' gradient is
     sequence_nll_loss_bits' closed form -nll_scale * nll_g * onehot(target) (dlogp unread)."""
     import model
@@ -155,10 +166,10 @@ def mlp_bwd(dlogp: Tensor, handle: Tensor, params: list[Tensor], nll_target: Opt
 
 
 @mlp_bwd.register_fake
-def _(dlogp, handle, params, nll_target, nll_scale, nll_g):
-    st_dt = dlogp.dtype
+def _(dlogp, handle, params, meta, upper_bf16, nll_target, nll_scale, nll_g):
     B, Tl, _ = dlogp.shape
-    return [dlogp.new_empty((B, Tl, 0), dtype=st_dt)] + [torch.empty_like(p) for p in params]
+    udt = torch.bfloat16 if upper_bf16 else torch.float32
+    return [dlogp.new_empty((B, Tl, meta[1]), dtype=udt)] + [torch.empty_like(p) for p in params]
 
 
 class FusedNllToken:
@@ -175,6 +186,8 @@ class FusedNllToken:
 def _mlp_setup(ctx, inputs, output):
     x, upper, params, meta = inputs
     ctx.params = params
+    ctx.meta = meta
+    ctx.upper_bf16 = upper.dtype == torch.bfloat16
     ctx.save_for_backward(output[1])
     ctx.mark_non_differentiable(output[1])
     ctx.tok = FusedNllToken()
@@ -188,9 +201,11 @@ def _mlp_backward(ctx, dlogp, dhandle):
         raise RuntimeError('the fused NLL gradient of the MLP log-probs was combined with '
                            'another gradient (log-probs used twice); run with SRNN_FUSED_NLL=0')
     if nll is not None:
-        out = torch.ops.srnn.mlp_bwd(dlogp, handle, ctx.params, nll[0], nll[1], nll[2])
+        out = torch.ops.srnn.mlp_bwd(dlogp, handle, ctx.params, ctx.meta, ctx.upper_bf16,
+                                     nll[0], nll[1], nll[2])
     else:
-        out = torch.ops.srnn.mlp_bwd(dlogp, handle, ctx.params, None, 0.0, None)
+        out = torch.ops.srnn.mlp_bwd(dlogp, handle, ctx.params, ctx.meta, ctx.upper_bf16, None,
+                                     0.0, None)
     return None, out[0], list(out[1:]), None
 
 
@@ -280,30 +295,35 @@ def _(x, params, k, weight_norm, has_bias):
     B, Cin, Lx = x.shape
     v = params[1] if weight_norm else params[0]
     return (x.new_empty((B, v.shape[1], Lx * k), dtype=torch.float32),
-            torch.empty(1, dtype=torch.int64, device='cpu'))
+            torch.empty(0, dtype=torch.int64, device='cpu'))
 
 
 @torch.library.custom_op('srnn::upsample_bwd', mutates_args=())
-def upsample_bwd(dout: Tensor, handle: Tensor, params: list[Tensor]) -> list[Tensor]:
+def upsample_bwd(dout: Tensor, handle: Tensor, params: list[Tensor], k: int,
+                 weight_norm: bool) -> list[Tensor]:
     import nn
     dx, grads = nn.upsample_backward(_take(handle), dout)
     return [dx] + list(grads)
 
 
 @upsample_bwd.register_fake
-def _(dout, handle, params):
-    return [dout.new_empty((dout.shape[0], 0, 0))] + [torch.empty_like(p) for p in params]
+def _(dout, handle, params, k, weight_norm):
+    B, _, LK = dout.shape
+    cin = (params[1] if weight_norm else params[0]).shape[0]
+    return [dout.new_empty((B, cin, LK // k), dtype=torch.float32)] + \
+        [torch.empty_like(p) for p in params]
 
 
 def _up_setup(ctx, inputs, output):
     ctx.params = inputs[1]
+    ctx.k, ctx.wn = inputs[2], inputs[3]
     ctx.save_for_backward(output[1])
     ctx.mark_non_differentiable(output[1])
 
 
 def _up_backward(ctx, dout, dhandle):
     (handle,) = ctx.saved_tensors
-    out = torch.ops.srnn.upsample_bwd(dout.contiguous(), handle, ctx.params)
+    out = torch.ops.srnn.upsample_bwd(dout.contiguous(), handle, ctx.params, ctx.k, ctx.wn)
     return out[0], list(out[1:]), None, None, None
 
 

@@ -240,7 +240,7 @@ class TierSpec:
             next(it)
         for _ in range(4 * self.n_rnn):
             next(it)
-        self.upsampling = _Conv([])
+        self.upsampling = _State()
         self.upsampling.conv_t = take(wn_up)
 
 
@@ -946,9 +946,11 @@ class Generator(Runner):
             noise = torch.as_tensor(noise).to(dev, torch.float32).contiguous()
             assert noise.shape == (T, n_seqs, Q), 'noise must be (T, n_seqs, Q)'
         # the registered op srnn::generate (custom_ops.py): the whole sample loop on the device
-        seq, logp = torch.ops.srnn.generate(
-            weights, meta, cond, row_bias, noise, int(seed) & ((1 << 63) - 1), int(row_offset),
-            (1 if use_graph else 0) | (0 if persistent else 2), bool(return_logp))
+        with torch.no_grad():
+            seq, logp = torch.ops.srnn.generate(
+                weights, meta, cond, row_bias, noise, int(seed) & ((1 << 63) - 1),
+                int(row_offset), (1 if use_graph else 0) | (0 if persistent else 2),
+                bool(return_logp))
         assert utils.q_zero(Q) == Q // 2
         self.last_sequences = seq
         out = model.dequantize(seq[:, L:], Q).cpu()

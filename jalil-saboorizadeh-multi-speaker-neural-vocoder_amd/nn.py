@@ -98,7 +98,7 @@ def upsample_forward(x, params, k, wn, has_bias):
         bias = H.permute3(bias_p.reshape(1, Cout, k), (0, 2, 1)).reshape(-1)
     y = H.linear(xr, Wg.reshape(k * Cout, Cin), bias=bias)     # (B*L, k*Cout)
     out = H.permute3(y.reshape(B, Lx * k, Cout), (0, 2, 1))     # (B, Cout, L*k)
-    st = _ConvT([])
+    st = _ConvT([None])
     st.conv, st.has_bias, st.xr, st.Wg = conv, has_bias, xr, Wg
     st.shape = (B, Cin, Lx, k, Cout)
     return out, st

@@ -58,6 +58,9 @@ def _fused_adam_step(optimizer, lo, hi, reduced=None):
                                       [s['exp_avg_sq'] for _, s in items], shadows,
                                       float(gscale), float(lo), float(hi), float(group['lr']),
                                       float(b1), float(b2), float(group['eps']), step)
+            for (p, _), sh in zip(items, shadows):
+                if sh is not None:
+                    H.shadow_refreshed(p)
             # algorithmic bytes: p, m, v read + written, the gradient read + written back
             # clamped (hardtanh_ in place, optim.py:13), the bf16 copies written
             H.roof_end('adam_clip', ev, nel * 32 + 2 * sum(

@@ -495,6 +495,15 @@ def cast_param(p, dtype):
     return c
 
 
+def shadow_refreshed(p):
+    """The fused clip+Adam (srnn::adam_clip_, which declares its in-place writes and so bumps
+    the parameter's version counter) rewrote p and its bf16 copy together: keep the copy valid
+    at p's new version."""
+    e = _SHADOW.get(id(p))
+    if e is not None and e[0]() is p and e[2] == p.data_ptr():
+        _SHADOW[id(p)] = (e[0], e[1], p.data_ptr(), p._version)
+
+
 def shadow_of(p):
     """The valid bf16 copy of parameter p, or None (the fused Adam step refreshes it)."""
     e = _SHADOW.get(id(p))

@@ -80,7 +80,8 @@ def uquantize(samples, q_levels):
 def _dequant(samples, q_levels, scale, mode=0):
     """scale * dequantize(samples) on the device: the registered op srnn::dequant."""
     import custom_ops  # noqa: F401  (registers the op)
-    return torch.ops.srnn.dequant(samples, q_levels, float(scale), mode)
+    with torch.no_grad():           # (integer input: no gradient; keeps outputs grad-free)
+        return torch.ops.srnn.dequant(samples, q_levels, float(scale), mode)
 
 
 def _dequant_impl(samples, q_levels, scale, mode=0):

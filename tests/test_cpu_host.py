@@ -170,6 +170,14 @@ def test_custom_ops_registered_with_fake_kernels():
     m = M.SampleRNN([16, 4], 1, 64, True, 256, True, True, 43, 6)
     m.compute_dtype = torch.bfloat16
     top, bot, mlp = m.frame_level_rnns[1], m.frame_level_rnns[0], m.sample_level_mlp
+    # the op bodies' views of the modules are built from (meta, params) alone
+    for t in (top, bot):
+        spec = M.TierSpec(M.tier_meta(t), t._param_list())
+        assert spec.dim == 64 and spec.is_cond == t.is_cond and spec.T == torch.bfloat16
+        assert spec.upsampling.conv_t.weight_v is t.upsampling.conv_t.weight_v
+        assert (spec.input_expand.weight_g is t.input_expand.weight_g)
+    ms = M.MlpSpec(M.mlp_meta(mlp), mlp._param_list())
+    assert ms.hidden.bias is mlp.hidden.bias and ms.output.weight_v is mlp.output.weight_v
     with FakeTensorMode(allow_non_fake_inputs=True):
         B = 3
         prev = torch.empty(B, 2, 64)
