@@ -4,7 +4,10 @@ One JSON line (rank 0).  `value` = aggregate TBPTT training throughput (audio sa
 second = global batch x T / step time) of the drop-in Trainer.train (trainer/__init__.py:62-117,
 the product path: forward, NLL, backward, DP all-reduce, fused clip + Adam, lagged failure
 check) on a 3-tier SampleRNN, dim 1024, frame_sizes [16, 4], 6 speakers + 43-d Ahocoder
-conditioning, T = 1024, bf16 MFMA with fp32 master weights / recurrences.
+conditioning, T = 1024, bf16 MFMA with fp32 master weights / recurrences.  On one GPU the
+Trainer runs in graph mode: the warm-up chunks run the eager steps and capture the step, the
+timed chunks replay it (`graph_replays`; `eager_ms_per_step` = the same step enqueued kernel
+by kernel, measured right after).
 
 Default workload = configs[3]: global batch 512 stream rows sharded over the N ranks
 (512 / N rows per GPU, strong scaling; N = 1 is the whole 512-row batch on one GPU).  Beside
@@ -12,8 +15,9 @@ it the line carries
   * `config_b` (N = 1): configs[1], 128 rows on one GPU;
   * `weak_64`: 64 rows per GPU (weak scaling at configs[3]'s 8-GPU share);
   * `roofline`: the step's DOMINANT kernel (largest time per step among the probed launch
-    sites: GRU sweeps, dTab scatter, MLP hidden GEMM, fused clip + Adam), measured inside the
-    timed steps with HIP events on the launching stream; `kernels` lists every probed site;
+    sites: GRU sweeps, dTab scatter, MLP hidden GEMM, fused clip + Adam), measured with HIP
+    events on the launching stream around each launch over eager steps of the same run (a
+    replayed graph runs the same kernels); `kernels` lists every probed site;
     `step_mfma`: executed MFMA work of the whole step / step time / bf16 peak;
   * generation throughput of configs[2] (`gen` bf16 persistent loop, `gen_fp32` the reference
     precision) and configs[4] (`gen_config_e`), rows sharded over ranks (each rank its
@@ -134,9 +138,28 @@ SITE_NOTES = {
 }
 
 
+class _LossLog:
+    """Trainer 'iteration' plugin keeping a copy of every step's loss (a replayed graph step
+    hands out the same static loss buffer each time)."""
+
+    def __init__(self):
+        self.trigger_interval = [(1, 'iteration')]
+        self.values = []
+
+    def register(self, trainer):
+        pass
+
+    def iteration(self, it, inputs, target, output, loss):
+        self.values.append(loss.detach().clone())
+
+
 def run_tbptt(dev, dist_mod, rows, steps, warmup, dtype, probe=True):
     """Warm-up then `steps` timed chunks of the drop-in Trainer.train on `rows` stream rows
-    of this rank.  Returns a dict (seconds = max over ranks)."""
+    of this rank (graph mode: the warm-up runs the eager steps and the capture, the timed
+    steps are replays).  Then, when `probe`, up to 5 more chunks run eagerly with the HIP-event
+    probes around the kernel sites (per-kernel durations for the roofline; events cannot
+    time kernels inside a replayed graph) -- untimed for the headline value.  Returns a dict
+    (seconds = max over ranks)."""
     import nn as snn
     import optim
     import samplernn_hip as H
@@ -147,37 +170,48 @@ def run_tbptt(dev, dist_mod, rows, steps, warmup, dtype, probe=True):
     sync = dist_mod.GradAllReduce(overlap_groups=dist_mod.readiness_groups(pred)) \
         if dist_mod.world() > 1 else None
     opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3), grad_sync=sync)
-    batches = gpu_batches(synth_batches(rows, T, L, warmup + steps, dist_mod.rank() * rows), dev)
-    losses = []
-
-    def criterion(out, tgt):
-        loss = snn.sequence_nll_loss_bits(out, tgt)
-        losses.append(loss.detach())
-        return loss
-    tr = Trainer(pred, criterion, opt, batches[:warmup], True, None)
+    n_probe = min(steps, 5) if probe else 0
+    batches = gpu_batches(synth_batches(rows, T, L, warmup + steps + n_probe,
+                                        dist_mod.rank() * rows), dev)
+    tr = Trainer(pred, snn.sequence_nll_loss_bits, opt, batches[:warmup], True, None)
+    log_ = _LossLog()
+    tr.register_plugin(log_)
     tr.train()                              # warm-up chunks (ends with the failure check)
     torch.cuda.synchronize()
     dist_mod.barrier()
     torch.cuda.synchronize()
-    tr.dataset = batches[warmup:]
+    tr.dataset = batches[warmup:warmup + steps]
     tr.enqueue_s = 0.0
-    H.ROOF_EVENTS = {} if probe else None
+    g0 = tr.graph_steps
     t0 = time.perf_counter()
     tr.train()                              # the timed chunks
     torch.cuda.synchronize()
     dist_mod.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    ev, H.ROOF_EVENTS = H.ROOF_EVENTS, None
-    sites = {}
-    for site, lst in (ev or {}).items():
-        ms = sum(a.elapsed_time(b) for a, b, _ in lst) / steps
-        work = sum(w for _, _, w in lst) / steps
-        sites[site] = (ms, work, len(lst) // steps)
+    enq = tr.enqueue_s
+    replayed = tr.graph_steps - g0
+    losses = [float(v) for v in log_.values]
+    sites, eager_ms, eager_enq = {}, None, None
+    if n_probe:
+        tr.dataset = batches[warmup + steps:]
+        tr.enqueue_s = 0.0
+        H.ROOF_EVENTS = {}
+        t1 = time.perf_counter()
+        tr.train()
+        torch.cuda.synchronize()
+        eager_ms = (time.perf_counter() - t1) / n_probe * 1e3
+        eager_enq = tr.enqueue_s / n_probe * 1e3
+        ev, H.ROOF_EVENTS = H.ROOF_EVENTS, None
+        for site, lst in (ev or {}).items():
+            ms = sum(a.elapsed_time(b) for a, b, _ in lst) / n_probe
+            work = sum(w for _, _, w in lst) / n_probe
+            sites[site] = (ms, work, len(lst) // n_probe)
     dt = dist_mod.max_over_ranks(dt, dev)
     res = {'seconds': dt, 'ms_per_step': dt / steps * 1e3,
-           'enqueue_ms_per_step': tr.enqueue_s / steps * 1e3,
-           'losses': [float(l) for l in losses], 'sites': sites, 'rows': rows}
+           'enqueue_ms_per_step': enq / steps * 1e3, 'graph_replays': replayed,
+           'eager_ms_per_step': eager_ms, 'eager_enqueue_ms_per_step': eager_enq,
+           'losses': losses[:warmup + steps], 'sites': sites, 'rows': rows}
     del tr, opt, pred, m, batches
     torch.cuda.empty_cache()
     return res
@@ -190,6 +224,10 @@ def tbptt_summary(r, N, dtype_peak, label):
            'tbptt_steps_per_s': round(1e3 / r['ms_per_step'], 3),
            'rows_per_gpu': r['rows'], 'global_batch': N * r['rows'],
            'host_enqueue_ms_per_step': round(r['enqueue_ms_per_step'], 3),
+           'graph_replays': r['graph_replays'],
+           'eager_ms_per_step': r['eager_ms_per_step'] and round(r['eager_ms_per_step'], 3),
+           'eager_host_enqueue_ms_per_step': r['eager_enqueue_ms_per_step'] and
+           round(r['eager_enqueue_ms_per_step'], 3),
            'final_loss': round(r['losses'][-1], 4), 'workload': label}
     flops = step_mfma_flops(r['rows'])
     ach = flops / (r['ms_per_step'] * 1e-3) / 1e12
@@ -406,8 +444,10 @@ def main():
         raise SystemExit('global batch %d not divisible by %d ranks' % (GLOBAL_B, N))
 
     main_r = run_tbptt(dev, D, rows, args.steps, args.warmup, dtype)
-    log('tbptt %d rows/GPU: %.2f ms/step (host enqueue %.2f ms/step), losses %s' % (
-        rows, main_r['ms_per_step'], main_r['enqueue_ms_per_step'],
+    log('tbptt %d rows/GPU: %.2f ms/step (host enqueue %.2f ms/step, %d graph replays; eager '
+        '%s ms/step), losses %s' % (
+        rows, main_r['ms_per_step'], main_r['enqueue_ms_per_step'], main_r['graph_replays'],
+        main_r['eager_ms_per_step'],
         ['%.3f' % l for l in main_r['losses']]))
     label = ('configs[3]: TBPTT step, 3-tier SampleRNN dim1024 FS=[16,4] n_rnn=1 cond 43 spk 6, '
              'T=1024, global batch %d = %d rows/GPU x %d GPU, Trainer.train (fwd+bwd+%sclip+'
@@ -419,9 +459,10 @@ def main():
     if dom:
         roof = dict(ks[dom])
         roof['traffic'] = pmc_traffic(dom, rows)
-        roof['kernel'] = '%s; %.3f ms per step inside the timed steps (%d launches, HIP events on '\
-                         'the launching stream)' % (SITE_NOTES.get(dom, dom), ks[dom]['ms_per_step'],
-                                                    ks[dom]['launches_per_step'])
+        roof['kernel'] = '%s; %.3f ms per step (%d launches; HIP events on the launching stream '\
+                         'around each launch, over eager steps of the same run right after the '\
+                         'timed graph replays)' % (SITE_NOTES.get(dom, dom), ks[dom]['ms_per_step'],
+                                                   ks[dom]['launches_per_step'])
         roof['site'] = dom
 
     extra = {}
@@ -505,6 +546,9 @@ def main():
                            'rows_per_gpu': rows, 'parallelism': 'dp%d' % N},
                 'tbptt_steps_per_s': summ['tbptt_steps_per_s'],
                 'host_enqueue_ms_per_step': summ['host_enqueue_ms_per_step'],
+                'graph_replays': summ['graph_replays'],
+                'eager_ms_per_step': summ['eager_ms_per_step'],
+                'eager_host_enqueue_ms_per_step': summ['eager_host_enqueue_ms_per_step'],
                 'roofline': roof, 'kernels': ks, 'step_mfma': summ['step_mfma'],
                 'cpu_baseline': cpu, 'gen': gen, 'gen_fp32': gen_fp32,
                 'gen_config_e': gen_e, 'gru_sweep': gru,

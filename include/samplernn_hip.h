@@ -270,6 +270,17 @@ int srnn_adam_clip_multi2(int ntensors, float* const* p, void* const* g, int gdt
                           float* const* m, float* const* v, void* const* p_bf16, const int64_t* n,
                           float clip_lo, float clip_hi, double lr, double beta1, double beta2,
                           double eps, int64_t step, void* stream);
+/* srnn_adam_clip_multi2 with the step count on the device: dstep (NULL = use `step`) holds
+ * the number of completed steps and the kernel takes step = *dstep + 1 for the bias
+ * corrections (host formula, torch.optim.Adam).  With srnn_step_advance this makes the
+ * optimizer step replayable from a captured HIP graph (trainer/__init__.py graph mode).   */
+int srnn_adam_clip_multi3(int ntensors, float* const* p, void* const* g, int gdtype, float gscale,
+                          float* const* m, float* const* v, void* const* p_bf16, const int64_t* n,
+                          float clip_lo, float clip_hi, double lr, double beta1, double beta2,
+                          double eps, int64_t step, const int64_t* dstep, void* stream);
+/* dstep[0..n) += 1 unless the persistent-sweep failure flag is up (the step's update was
+ * skipped, so its count must not advance either).  n <= 1024.                            */
+int srnn_step_advance(int64_t* dstep, int n, void* stream);
 /* Data-parallel gradient bucket packing: src[i] (fp32, n[i] elements, NULL = zeros) ->
  * flat + dst_off[i] in dtype (fp32 / bf16), all tensors in one launch.  The reference has no
  * distributed step; this feeds distributed.GradAllReduce's RCCL all-reduce.   */

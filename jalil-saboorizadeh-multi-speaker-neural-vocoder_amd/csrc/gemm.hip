@@ -450,17 +450,9 @@ int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int 
     const void* mk = mask;
     int64_t ldmk = ldmask;
     if (mbi) {
-        static void* scratch = nullptr;
-        static size_t bytes = 0;
         const int es = dtype == SRNN_F32 ? 4 : 2;
-        const size_t need = (size_t)M * N * es;
-        if (need > bytes) {
-            if (scratch) SRNN_CHECK_HIP(hipFree(scratch));
-            scratch = nullptr;
-            bytes = 0;
-            SRNN_CHECK_HIP(hipMalloc(&scratch, need));
-            bytes = need;
-        }
+        void* scratch = srnn_scratch(SRNN_SCRATCH_MASK, (size_t)M * N * es);
+        SRNN_REQUIRE(scratch, "gemm: mask scratch allocation failed");
         const int64_t n = (int64_t)M * N;
         if (dtype == SRNN_F32)
             hipLaunchKernelGGL((bits_expand_kernel<float>), dim3((unsigned)cdiv(n, 256)), dim3(256),

@@ -406,17 +406,26 @@ __global__ __launch_bounds__(256) void g3_splitk_sum_kernel(const float* __restr
     *reinterpret_cast<floatx4*>(C + (int64_t)m * ldc + n) = s;
 }
 
-float* srnn_splitk_scratch(size_t bytes) {
-    static float* scratch = nullptr;
-    static size_t have = 0;
-    if (bytes > have) {
-        if (scratch && hipFree(scratch) != hipSuccess) return nullptr;
-        scratch = nullptr;
-        have = 0;
-        if (hipMalloc((void**)&scratch, bytes) != hipSuccess) return nullptr;
-        have = bytes;
+// Grow-only device scratch buffers, one per slot (samplernn_hip_internal.hpp).  A buffer
+// that is outgrown is retired, never freed: a captured HIP graph (trainer graph mode) keeps
+// the pointer that was current at capture, so every buffer must outlive later growth.  The
+// retired ones total less than the live one (sizes grow geometrically from the first calls).
+void* srnn_scratch(int slot, size_t bytes) {
+    static void* buf[SRNN_SCRATCH_SLOTS] = {};
+    static size_t have[SRNN_SCRATCH_SLOTS] = {};
+    if (slot < 0 || slot >= SRNN_SCRATCH_SLOTS) return nullptr;
+    if (bytes > have[slot]) {
+        const size_t want = bytes > 2 * have[slot] ? bytes : 2 * have[slot];
+        void* p = nullptr;
+        if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+        buf[slot] = p;
+        have[slot] = want;
     }
-    return scratch;
+    return buf[slot];
+}
+
+float* srnn_splitk_scratch(size_t bytes) {
+    return (float*)srnn_scratch(SRNN_SCRATCH_SPLITK, bytes);
 }
 
 int srnn_splitk_sum(const float* part, float* C, int64_t ldc, int M, int N, int ks, hipStream_t s) {

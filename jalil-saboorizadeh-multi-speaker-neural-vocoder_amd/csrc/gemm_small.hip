@@ -223,11 +223,9 @@ __global__ __launch_bounds__(256) void gemm_small_nt_sum_kernel(const float* __r
 }
 
 // Split-K partials of the thin NT path: one grow-only scratch buffer reused by every call
-// (stream-ordered on the caller's stream).  A stream-ordered hipMallocAsync per call cost
-// up to 4 ms of host time per TBPTT step (the 1024 x 64 x 2048 input-projection weight
-// gradient), which stalled the launch queue; growth only happens on the first calls.
-static float* g_nt_scratch = nullptr;
-static size_t g_nt_bytes = 0;
+// (stream-ordered on the caller's stream; srnn_scratch).  A stream-ordered hipMallocAsync per
+// call cost up to 4 ms of host time per TBPTT step (the 1024 x 64 x 2048 input-projection
+// weight gradient), which stalled the launch queue; growth only happens on the first calls.
 
 template <typename T>
 static int launch_small_nt(const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
@@ -238,15 +236,8 @@ static int launch_small_nt(const void* A, int64_t lda, const void* B, int64_t ld
     const int kchunk = cdiv(cdiv(K, nks), 4 * gsn::KR) * 4 * gsn::KR;
     nks = cdiv(K, kchunk);
     const size_t need = (size_t)nks * N * M * sizeof(float);
-    if (need > g_nt_bytes) {
-        // (hipFree waits for the device, so no in-flight call still reads the old buffer)
-        if (g_nt_scratch) SRNN_CHECK_HIP(hipFree(g_nt_scratch));
-        g_nt_scratch = nullptr;
-        g_nt_bytes = 0;
-        SRNN_CHECK_HIP(hipMalloc((void**)&g_nt_scratch, need));
-        g_nt_bytes = need;
-    }
-    float* P = g_nt_scratch;
+    float* P = (float*)srnn_scratch(SRNN_SCRATCH_NT, need);
+    SRNN_REQUIRE(P, "gemm_small: split-K scratch allocation failed");
     hipLaunchKernelGGL((gemm_small_nt_part_kernel<T>), dim3(mblk, ngrp, nks), dim3(256), 0, s,
                        (const T*)A, lda, (const T*)B, ldb, P, M, N, K, kchunk);
     SRNN_LAUNCH_CHECK();

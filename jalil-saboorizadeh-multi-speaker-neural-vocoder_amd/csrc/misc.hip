@@ -883,7 +883,9 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
                                                               float w1, float b2, float omb2,
                                                               float step_size, float bc2s,
                                                               float eps, float gscale,
-                                                              const int* skip) {
+                                                              const int* skip,
+                                                              const int64_t* dstep, double lr,
+                                                              double beta1, double beta2) {
     constexpr int CH = 2048;
     constexpr bool WB = std::is_same<GT, float>::value;      // write the clamped grad back
     // a persistent sweep of this step gave up a hand-off (persist.hip): its gradients are
@@ -891,6 +893,13 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
     if (__builtin_amdgcn_readfirstlane(__hip_atomic_load(skip, __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT)))
         return;
+    // device-resident step count (graph-replayed steps, srnn_adam_clip_multi3): the bias
+    // corrections follow from the count of completed steps, with the host formula
+    if (dstep) {
+        const double s = (double)(*dstep + 1);
+        step_size = (float)(lr / (1.0 - pow(beta1, s)));
+        bc2s = (float)sqrt(1.0 - pow(beta2, s));
+    }
     // workgroups never straddle tensors, so the tensor index is uniform and its pointers
     // come from the argument block with scalar loads
     int t = 0;
@@ -956,13 +965,15 @@ __global__ __launch_bounds__(256) void adam_clip_multi_kernel(AdamMulti a, float
     }
 }
 
-extern "C" int srnn_adam_clip_multi2(int ntensors, float* const* p, void* const* g, int gdtype,
+extern "C" int srnn_adam_clip_multi3(int ntensors, float* const* p, void* const* g, int gdtype,
                                      float gscale, float* const* m, float* const* v,
                                      void* const* p_bf16, const int64_t* n, float clip_lo,
                                      float clip_hi, double lr, double beta1, double beta2,
-                                     double eps, int64_t step, void* stream) {
+                                     double eps, int64_t step, const int64_t* dstep,
+                                     void* stream) {
     SRNN_REQUIRE(ntensors >= 0, "adam_multi: bad tensor count");
-    SRNN_REQUIRE(step >= 1, "adam: step must be >= 1");
+    SRNN_REQUIRE(dstep || step >= 1, "adam: step must be >= 1");
+    if (dstep) step = 1;   // placeholder: the kernel reads the count
     SRNN_REQUIRE(gdtype == SRNN_F32 || gdtype == SRNN_BF16, "adam_multi: gradient dtype");
     const double bc1 = 1.0 - pow(beta1, (double)step);
     const double bc2 = 1.0 - pow(beta2, (double)step);
@@ -993,14 +1004,42 @@ extern "C" int srnn_adam_clip_multi2(int ntensors, float* const* p, void* const*
             hipLaunchKernelGGL(adam_clip_multi_kernel<float>, dim3((unsigned)nblk), dim3(256), 0,
                                (hipStream_t)stream, a, clip_lo, clip_hi, (float)(1.0 - beta1),
                                (float)beta2, (float)(1.0 - beta2), step_size, bc2s, (float)eps,
-                               gscale, skip);
+                               gscale, skip, dstep, lr, beta1, beta2);
         else
             hipLaunchKernelGGL(adam_clip_multi_kernel<bf16>, dim3((unsigned)nblk), dim3(256), 0,
                                (hipStream_t)stream, a, clip_lo, clip_hi, (float)(1.0 - beta1),
                                (float)beta2, (float)(1.0 - beta2), step_size, bc2s, (float)eps,
-                               gscale, skip);
+                               gscale, skip, dstep, lr, beta1, beta2);
         SRNN_LAUNCH_CHECK();
     }
+    return 0;
+}
+
+extern "C" int srnn_adam_clip_multi2(int ntensors, float* const* p, void* const* g, int gdtype,
+                                     float gscale, float* const* m, float* const* v,
+                                     void* const* p_bf16, const int64_t* n, float clip_lo,
+                                     float clip_hi, double lr, double beta1, double beta2,
+                                     double eps, int64_t step, void* stream) {
+    return srnn_adam_clip_multi3(ntensors, p, g, gdtype, gscale, m, v, p_bf16, n, clip_lo,
+                                 clip_hi, lr, beta1, beta2, eps, step, nullptr, stream);
+}
+
+// Completed-step counters of srnn_adam_clip_multi3: +1 each, unless the sticky failure flag
+// is up (that step's update was skipped, so the bias correction must not advance either).
+__global__ void step_advance_kernel(int64_t* dstep, int n, const int* skip) {
+    if (__hip_atomic_load(skip, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    const int i = threadIdx.x;
+    if (i < n) dstep[i] = dstep[i] + 1;
+}
+
+extern "C" int srnn_step_advance(int64_t* dstep, int n, void* stream) {
+    SRNN_REQUIRE(dstep && n >= 0 && n <= 1024, "step_advance: bad arguments");
+    if (n == 0) return 0;
+    const int* skip = srnn_sticky_flag();
+    SRNN_REQUIRE(skip, "step_advance: sticky flag allocation failed");
+    hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64 * (unsigned)cdiv(n, 64)), 0,
+                       (hipStream_t)stream, dstep, n, skip);
+    SRNN_LAUNCH_CHECK();
     return 0;
 }
 

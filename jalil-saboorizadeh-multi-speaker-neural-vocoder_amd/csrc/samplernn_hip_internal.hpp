@@ -34,9 +34,14 @@ static inline int env_flag(const char* name, int dflt) {
 int* srnn_sticky_flag();
 int srnn_persist_spin_limit(int dflt);
 
-// gemm3.hip: deterministic split-K support.  srnn_splitk_scratch returns a grow-only device
-// buffer of at least `bytes` (null on a HIP error; allocated on first use, i.e. outside graph
-// captures); srnn_splitk_sum writes C[m][n] = sum_z part[z][m][n] in z order (float4 columns:
+// gemm3.hip: grow-only device scratch buffers, one per slot, never freed (a captured HIP graph
+// keeps the pointer current at its capture); null on a HIP error.  Allocated on first use,
+// i.e. by the eager warm-up step, outside graph captures.
+enum { SRNN_SCRATCH_SPLITK = 0, SRNN_SCRATCH_MASK = 1, SRNN_SCRATCH_NT = 2, SRNN_SCRATCH_SLOTS = 4 };
+void* srnn_scratch(int slot, size_t bytes);
+
+// Deterministic split-K support.  srnn_splitk_scratch = srnn_scratch(SRNN_SCRATCH_SPLITK);
+// srnn_splitk_sum writes C[m][n] = sum_z part[z][m][n] in z order (float4 columns:
 // N % 4 == 0, C 16-B aligned, ldc % 4 == 0).
 float* srnn_splitk_scratch(size_t bytes);
 int srnn_splitk_sum(const float* part, float* C, int64_t ldc, int M, int N, int ks, hipStream_t s);

@@ -12,6 +12,7 @@ The drop-in classes call these ops, so the registered ops ARE the product path:
   srnn::upsample / upsample_bwd LearnedUpsampling1d used on its own (nn.py:7-43)
   srnn::dequant                 2 * udequantize / linear_dequantize (utils.py:18-19, 62-63)
   srnn::adam_clip_              gradient_clipping + Adam (optim.py:4-21), in place
+  srnn::step_advance_           the device step counters srnn::adam_clip_ can read (graph mode)
   srnn::generate                Generator.__call__'s sample loop (model.py:445-520)
 
 Every op has a fake (meta) kernel, so FakeTensor / torch.compile tracing sees shapes without
@@ -349,29 +350,48 @@ def _(samples, q_levels, scale, mode):
 def adam_clip_(params: list[Tensor], grads: list[Optional[Tensor]], exp_avg: list[Tensor],
                exp_avg_sq: list[Tensor], shadows: list[Optional[Tensor]], grad_scale: float,
                clip_lo: float, clip_hi: float, lr: float, beta1: float, beta2: float,
-               eps: float, step: int) -> None:
+               eps: float, step: int, dstep: Optional[Tensor] = None) -> None:
     """gradient_clipping(lo, hi) + torch.optim.Adam over every tensor in ONE launch per 64
-    (srnn_adam_clip_multi2): g = clamp(g * grad_scale) (written back for fp32 gradients),
+    (srnn_adam_clip_multi3): g = clamp(g * grad_scale) (written back for fp32 gradients),
     moments and parameters updated in place, bf16 shadows (optional) refreshed; a None
     gradient is an all-zero one; skipped on the device while the persistent-sweep failure
-    flag is up.  All gradients share one dtype (fp32, or bf16 from DP buckets)."""
+    flag is up.  All gradients share one dtype (fp32, or bf16 from DP buckets).  dstep: a
+    one-element int64 device tensor holding the count of completed steps, read by the
+    kernel in place of `step` (a graph-replayed step; advanced by srnn::step_advance_)."""
     import ctypes
     n = len(params)
     if n == 0:
         return
+    if dstep is not None and (dstep.dtype != torch.int64 or dstep.numel() < 1 or
+                              dstep.device != params[0].device):
+        raise ValueError('adam_clip_: dstep must be an int64 tensor on the parameters\' device')
     arr = lambda ts: (ctypes.c_void_p * n)(*[H.ptr(t) for t in ts])  # noqa: E731
     gdt = next((g.dtype for g in grads if g is not None), torch.float32)
-    H.lib().call('srnn_adam_clip_multi2', n, arr(params), arr(grads), H.dcode(gdt),
+    H.lib().call('srnn_adam_clip_multi3', n, arr(params), arr(grads), H.dcode(gdt),
                  float(grad_scale), arr(exp_avg), arr(exp_avg_sq),
                  arr(shadows) if any(t is not None for t in shadows) else None,
                  (ctypes.c_int64 * n)(*[p.numel() for p in params]), float(clip_lo),
                  float(clip_hi), float(lr), float(beta1), float(beta2), float(eps), int(step),
-                 H.stream())
+                 H.ptr(dstep) if dstep is not None else None, H.stream())
 
 
 @adam_clip_.register_fake
 def _(params, grads, exp_avg, exp_avg_sq, shadows, grad_scale, clip_lo, clip_hi, lr, beta1,
-      beta2, eps, step):
+      beta2, eps, step, dstep=None):
+    return None
+
+
+@torch.library.custom_op('srnn::step_advance_', mutates_args=('dstep',))
+def step_advance_(dstep: Tensor) -> None:
+    """Device step counters += 1 unless the persistent-sweep failure flag is up
+    (srnn_step_advance): the count srnn::adam_clip_ reads when given dstep."""
+    if dstep.dtype != torch.int64 or not dstep.is_contiguous():
+        raise ValueError('step_advance_: contiguous int64 counters')
+    H.lib().call('srnn_step_advance', H.ptr(dstep), dstep.numel(), H.stream())
+
+
+@step_advance_.register_fake
+def _(dstep):
     return None
 
 
@@ -413,4 +433,4 @@ def _(weights, meta, cond, row_bias, noise, seed, row_offset, flags, return_logp
 
 
 OPS = ('tier_fwd', 'tier_bwd', 'mlp_fwd', 'mlp_bwd', 'nll_bits', 'nll_bits_bwd', 'upsample',
-       'upsample_bwd', 'dequant', 'adam_clip_', 'generate')
+       'upsample_bwd', 'dequant', 'adam_clip_', 'step_advance_', 'generate')

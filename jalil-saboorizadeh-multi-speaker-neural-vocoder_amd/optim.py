@@ -10,20 +10,47 @@ semantics: the learned h0 keeps moving on its Adam moments on non-reset steps, a
 did in the reference's environment.  An optional `grad_sync` callable (set by
 distributed.py) all-reduces gradients after the closure and before the clamp.
 """
+import os
+
 import torch
 
 import samplernn_hip as H
 
 
-def _fused_adam_step(optimizer, lo, hi, reduced=None):
+class DeviceSteps:
+    """Per-parameter-group count of completed Adam steps on the device (int64, one entry per
+    group), read by srnn::adam_clip_ in place of a host step and advanced on the device by
+    srnn::step_advance_ -- which skips while the persistent-sweep failure flag is up, as the
+    update does.  A captured step (trainer graph mode) therefore replays with the right bias
+    corrections.  `mirror[g]` is the value the host believes entry g holds (None: unknown);
+    whenever it disagrees with the optimizer's own step count the entry is re-seeded."""
+
+    def __init__(self, optimizer, device):
+        self.t = torch.zeros(len(optimizer.param_groups), dtype=torch.int64, device=device)
+        self.mirror = [0] * len(optimizer.param_groups)
+        self.uniform = True       # every group's parameters share one step count
+
+
+def _host_step(optimizer, group):
+    for p in group['params']:
+        st = optimizer.state.get(p)
+        if st and 'step' in st:
+            return int(st['step'].item())
+    return None
+
+
+def _fused_adam_step(optimizer, lo, hi, reduced=None, dsteps=None):
     """All parameters of a group that share a step count go through ONE multi-tensor
-    launch (srnn_adam_clip_multi2) instead of one launch per tensor.  reduced: the data-
+    launch (srnn_adam_clip_multi3) instead of one launch per tensor.  reduced: the data-
     parallel gradient buckets ((param, view) pairs, dtype, 1 / world scale; distributed.py)
-    read in place instead of p.grad."""
+    read in place instead of p.grad.  dsteps (DeviceSteps): take the step count from the
+    device counters (re-seeded from the host count when they disagree) and advance them."""
     import custom_ops  # noqa: F401  (registers srnn::adam_clip_)
     rv = {id(p): v for p, v in reduced[0]} if reduced else None
     gscale = reduced[2] if reduced else 1.0
-    for group in optimizer.param_groups:
+    capturing = torch.cuda.is_current_stream_capturing()
+    uniform = True
+    for gi, group in enumerate(optimizer.param_groups):
         if group.get('weight_decay', 0) != 0 or group.get('amsgrad', False) or \
                 group.get('maximize', False):
             raise NotImplementedError('fused clip+Adam: weight_decay/amsgrad/maximize')
@@ -45,6 +72,18 @@ def _fused_adam_step(optimizer, lo, hi, reduced=None):
                 raise NotImplementedError('fused clip+Adam: contiguous fp32 parameters only')
             st['step'] += 1
             by_step.setdefault(int(st['step'].item()), []).append((p, st))
+        dstep = None
+        if dsteps is not None and len(by_step) == 1:
+            step = next(iter(by_step))
+            if dsteps.mirror[gi] != step - 1:
+                if capturing:
+                    raise RuntimeError('fused Adam: device step counter out of step with the '
+                                       'optimizer during graph capture')
+                dsteps.t[gi].fill_(step - 1)
+                dsteps.mirror[gi] = step - 1
+            dstep = dsteps.t[gi:gi + 1]
+        elif len(by_step) > 1:
+            uniform = False
         for step, items in sorted(by_step.items()):
             # parameters with a cached bf16 copy (samplernn_hip.cast_param) get it rewritten
             # by the same kernel, so the next forward needs no cast
@@ -57,7 +96,7 @@ def _fused_adam_step(optimizer, lo, hi, reduced=None):
                                       [s['exp_avg'] for _, s in items],
                                       [s['exp_avg_sq'] for _, s in items], shadows,
                                       float(gscale), float(lo), float(hi), float(group['lr']),
-                                      float(b1), float(b2), float(group['eps']), step)
+                                      float(b1), float(b2), float(group['eps']), step, dstep)
             for (p, _), sh in zip(items, shadows):
                 if sh is not None:
                     H.shadow_refreshed(p)
@@ -65,6 +104,10 @@ def _fused_adam_step(optimizer, lo, hi, reduced=None):
             # clamped (hardtanh_ in place, optim.py:13), the bf16 copies written
             H.roof_end('adam_clip', ev, nel * 32 + 2 * sum(
                 p.numel() for (p, _), sh in zip(items, shadows) if sh is not None))
+    if dsteps is not None:
+        dsteps.uniform = uniform
+        torch.ops.srnn.step_advance_(dsteps.t)
+        dsteps.mirror = [None if m is None else m + 1 for m in dsteps.mirror]
 
 
 def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
@@ -73,6 +116,7 @@ def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
 
         def __init__(self):
             self.grad_sync = grad_sync
+            self.dsteps = None        # DeviceSteps, created by the first fused step
 
         def _fused(self):
             return isinstance(optimizer, torch.optim.Adam) and all(
@@ -97,8 +141,10 @@ def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
                         reduced = self.grad_sync.reduced
                     else:
                         self.grad_sync(optimizer)
+                if self.dsteps is None:
+                    self.dsteps = DeviceSteps(optimizer, optimizer.param_groups[0]['params'][0].device)
                 with torch.no_grad():
-                    _fused_adam_step(optimizer, min, max, reduced)
+                    _fused_adam_step(optimizer, min, max, reduced, self.dsteps)
                 return loss
 
             def closure_wrapper():
@@ -123,6 +169,48 @@ def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
                     st = optimizer.state.get(p)
                     if st and 'step' in st:
                         st['step'] -= k
+            if self.dsteps is not None:        # re-seed the device counters on the next step
+                self.dsteps.mirror = [None] * len(self.dsteps.mirror)
+
+        # ---- graph mode (trainer/__init__.py): the step replayed from a captured graph
+        def graph_ready(self):
+            """True when the step can be captured: the fused path with device step counters
+            whose groups each share one step count, no data-parallel gradient hook (its
+            collectives run on side streams) unless SRNN_GRAPH_DP=1."""
+            if not self._fused() or self.dsteps is None or not self.dsteps.uniform:
+                return False
+            return self.grad_sync is None or os.environ.get('SRNN_GRAPH_DP', '0') == '1'
+
+        def graph_signature(self):
+            """What a captured step baked in: hyper-parameters (kernel arguments) and the
+            addresses of every parameter, moment and bf16 copy (kernel pointers)."""
+            sig = []
+            for group in optimizer.param_groups:
+                sig.append((float(group['lr']), tuple(group['betas']), float(group['eps'])))
+                for p in group['params']:
+                    st = optimizer.state.get(p) or {}
+                    sh = H.shadow_of(p)
+                    sig.append((p.data_ptr(), st['exp_avg'].data_ptr() if 'exp_avg' in st else 0,
+                                st['exp_avg_sq'].data_ptr() if 'exp_avg_sq' in st else 0,
+                                sh.data_ptr() if sh is not None else 0))
+            return tuple(sig)
+
+        def before_replay(self):
+            """Re-seed any device counter that disagrees with the optimizer's step count."""
+            for gi, group in enumerate(optimizer.param_groups):
+                step = _host_step(optimizer, group)
+                if step is not None and self.dsteps.mirror[gi] != step:
+                    self.dsteps.t[gi].fill_(step)
+                    self.dsteps.mirror[gi] = step
+
+        def after_replay(self):
+            """The host bookkeeping the replayed step did not run: step counts + 1."""
+            for group in optimizer.param_groups:
+                for p in group['params']:
+                    st = optimizer.state.get(p)
+                    if st and 'step' in st:
+                        st['step'] += 1
+            self.dsteps.mirror = [None if m is None else m + 1 for m in self.dsteps.mirror]
 
         def __getattr__(self, attr):
             return getattr(optimizer, attr)

@@ -92,6 +92,9 @@ _SIGS = {
     'srnn_adam_clip_multi2': [_I, _P, _P, _I, _F, _P, _P, _P, _P, _F, _F, _D, _D, _D, _D, _L,
                               _P],
     'srnn_pack_grads': [_I, _P, _P, _P, _P, _I, _P],
+    'srnn_adam_clip_multi3': [_I, _P, _P, _I, _F, _P, _P, _P, _P, _F, _F, _D, _D, _D, _D, _L,
+                              _P, _P],
+    'srnn_step_advance': [_P, _I, _P],
     'srnn_nll_logsoftmax_bwd': [_P, _L, _I, _L, _I, _P, _L, _F, _P, _P, _I, _L, _P],
 }
 

@@ -11,13 +11,39 @@ The per-iteration check of the persistent sweeps' failure flag is lagged by one 
 needs no device synchronisation (samplernn_hip.PersistentErrorWatch): the host keeps
 enqueuing while the GPU runs; a failure raises one iteration later (or at the epoch's end),
 after the Adam step counters of the skipped updates are rolled back.
+
+Graph mode (SRNN_GRAPH=1, the default on a GPU): the whole TBPTT step -- forward, loss,
+backward, clip + Adam -- is captured once per step kind into a HIP graph and replayed, so
+the host enqueues one graph launch instead of every kernel.  A step kind is (fresh hidden
+state or carried, batch shapes, what the optimizer baked in: learning rates and the
+addresses of parameters / moments / bf16 copies); the first occurrence of a kind runs
+eagerly (it is also the warm-up that sizes every workspace), the second is captured and
+replayed, later ones replay.  The batch is copied into static input buffers and the carried
+hidden state lives in static buffers the graph reads and rewrites; the Adam step count is
+read from a device counter (optim.DeviceSteps) so replays keep the bias correction exact.
+Anything a captured step cannot honour falls back to the eager step: roofline probes on
+(bench.py's per-kernel timing), a data-parallel gradient hook (unless SRNN_GRAPH_DP=1), a
+criterion or model without the Predictor's hidden-state carry.
 """
 import heapq
+import os
 import time
 
 import torch
 
 import samplernn_hip as H
+
+GRAPHS = os.environ.get('SRNN_GRAPH', '1') != '0'
+
+
+class _StepGraph:
+    """One captured TBPTT step: the graph, its static inputs and outputs."""
+
+    def __init__(self, x, tgt, cond, spk):
+        self.x, self.tgt, self.cond, self.spk = x, tgt, cond, spk
+        self.graph = None
+        self.out = self.loss = None
+        self.replays = 0
 
 
 class Trainer(object):
@@ -41,6 +67,10 @@ class Trainer(object):
         self.writer = writer
         self._watch = None
         self.enqueue_s = 0.0        # host seconds spent enqueuing steps (bench.py)
+        self.graphs = {}            # step kind -> _StepGraph (graph mode)
+        self._seen = set()          # step kinds that ran eagerly once
+        self._hbuf = {}             # (tier index, rows) -> static carried hidden state
+        self.graph_steps = 0        # steps replayed from a graph (tests, bench.py)
 
     def register_plugin(self, plugin):
         plugin.register(self)
@@ -115,6 +145,18 @@ class Trainer(object):
                 batch_cond = batch_cond.cuda(non_blocking=True)
                 batch_spk = batch_spk.cuda(non_blocking=True)
 
+            kind = self._step_kind(batch_inputs, batch_target, batch_cond, batch_spk)
+            if kind is not None and (kind in self.graphs or kind in self._seen):
+                plugin_data = self._graph_step(kind, batch_inputs, batch_target, batch_cond,
+                                               batch_spk)
+                self.enqueue_s += time.perf_counter() - t_enq
+                self._watch.step(self._rollback)
+                self.call_plugins('iteration', self.iterations, batch_inputs, batch_target,
+                                  *plugin_data)
+                self.call_plugins('update', self.iterations, self.model)
+                continue
+            if kind is not None:
+                self._seen.add(kind)
             plugin_data = [None, None]
 
             def closure():
@@ -137,3 +179,107 @@ class Trainer(object):
             self.call_plugins('update', self.iterations, self.model)
         if self.cuda:
             self._watch.flush(self._rollback)
+
+    # ------------------------------------------------------------------ graph mode
+    def _step_kind(self, batch_inputs, target, cond, spk):
+        """The key of a capturable step, or None when this step must run eagerly."""
+        if not (GRAPHS and self.cuda) or H.ROOF_EVENTS is not None:
+            return None
+        opt = self.optimizer
+        if not (hasattr(opt, 'graph_ready') and opt.graph_ready()):
+            return None
+        hs = getattr(self.model, 'hidden_states', None)
+        rnns = getattr(getattr(self.model, 'model', None), 'frame_level_rnns', None)
+        if hs is None or rnns is None:
+            return None
+        inputs, reset = batch_inputs
+        fresh = bool(reset) or all(h is None for h in hs.values())
+        if not fresh and any(hs.get(r) is None for r in rnns):
+            return None
+        ts = (inputs, target, cond, spk)
+        if not all(torch.is_tensor(t) and t.is_cuda for t in ts):
+            return None
+        return (fresh,) + tuple((tuple(t.shape), t.dtype) for t in ts) + \
+            (opt.graph_signature(),)
+
+    def _hidden_bufs(self, rows):
+        """Static carried hidden state per tier (n_rnn, rows, dim) fp32."""
+        bufs = []
+        dev = self.optimizer.dsteps.t.device
+        for i, rnn in enumerate(self.model.model.frame_level_rnns):
+            b = self._hbuf.get((i, rows))
+            if b is None:
+                b = torch.zeros(rnn.n_rnn, rows, rnn.dim, device=dev)
+                self._hbuf[(i, rows)] = b
+            bufs.append(b)
+        return bufs
+
+    def _graph_step(self, kind, batch_inputs, target, cond, spk):
+        """Replay the captured step of this kind (capturing it first if needed); returns the
+        static (output, loss) handed to the plugins."""
+        model = self.model
+        rnns = model.model.frame_level_rnns
+        fresh = kind[0]
+        inputs = batch_inputs[0]
+        bufs = self._hidden_bufs(inputs.shape[0])
+        sg = self.graphs.get(kind)
+        if not fresh:
+            for rnn, b in zip(rnns, bufs):       # the carried state into the static buffers
+                h = model.hidden_states[rnn]
+                if h is not b:
+                    if h.shape != b.shape or h.dtype != b.dtype:
+                        raise RuntimeError('graph mode: carried hidden state %s %s, buffer %s'
+                                           % (tuple(h.shape), h.dtype, tuple(b.shape)))
+                    b.copy_(h)
+                    model.hidden_states[rnn] = b
+        if sg is None:
+            sg = self._capture(kind, inputs, target, cond, spk, bufs)
+        else:
+            sg.x.copy_(inputs)
+            sg.tgt.copy_(target)
+            sg.cond.copy_(cond)
+            sg.spk.copy_(spk)
+            self.optimizer.before_replay()
+            sg.graph.replay()
+            self.optimizer.after_replay()
+        sg.replays += 1
+        self.graph_steps += 1
+        for rnn, b in zip(rnns, bufs):
+            model.hidden_states[rnn] = b
+        return [sg.out, sg.loss]
+
+    def _capture(self, kind, inputs, target, cond, spk, bufs):
+        """Capture one step (its Python side effects -- Adam step counts, hidden-state
+        bookkeeping -- happen once, for the replay that follows)."""
+        # graphs baked against an older optimizer state are dead: free their memory
+        self.graphs = {k: g for k, g in self.graphs.items() if k[-1] == kind[-1]}
+        sg = _StepGraph(inputs.clone(), target.clone(), cond.clone(), spk.clone())
+        model, fresh = self.model, kind[0]
+        rnns = model.model.frame_level_rnns
+        self._zero_grad()
+        self.optimizer.before_replay()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        out_loss = [None, None]
+
+        def closure():
+            out = model(sg.x, fresh, sg.cond, sg.spk, self.writer, self.iterations)
+            loss = self.criterion(out, sg.tgt)
+            loss.backward()
+            out_loss[0], out_loss[1] = out.data, loss.data
+            return loss
+        with torch.cuda.graph(g):     # a private memory pool per step kind
+            self.optimizer.step(closure)
+            for rnn, b in zip(rnns, bufs):
+                h = model.hidden_states[rnn]
+                if h.shape != b.shape or h.dtype != b.dtype:
+                    raise RuntimeError('graph mode: new hidden state %s %s, buffer %s'
+                                       % (tuple(h.shape), h.dtype, tuple(b.shape)))
+                b.copy_(h)
+        sg.graph = g
+        sg.out, sg.loss = out_loss
+        self.graphs[kind] = sg
+        g.replay()
+        # replays overwrite the gradients in place: leave none visible as if fresh
+        self._zero_grad()
+        return sg

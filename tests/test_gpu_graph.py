@@ -1,0 +1,120 @@
+"""Graph mode of the drop-in Trainer (trainer/__init__.py): the captured-and-replayed TBPTT
+step against the eager step, and the device-resident Adam step count it relies on
+(optim.DeviceSteps, srnn::adam_clip_'s dstep, srnn::step_advance_).
+
+The replay runs the same kernels with the same arguments as the eager step.  The bf16 path
+(bench.py's) reduces in a fixed order, so graph and eager agree to 1e-6 relative (measured:
+bit for bit).  The fp32 path keeps fp32 atomics in some weight-gradient reductions whose
+order varies from launch to launch: eager runs of it differ from EACH OTHER by up to 5e-6
+relative in the loss and, after 8 Adam steps whose update direction flips on near-zero
+gradients, up to 8e-4 absolute in a weight (lr 1e-3; measured on MI355X with
+tools/graph_diag.py) -- the fp32 bounds are 2e-5 and 2e-3 (two Adam steps' movement).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda'
+
+
+class _Losses:
+    """'iteration' plugin collecting each step's loss (a copy: replays reuse the buffer)."""
+
+    def __init__(self):
+        self.trigger_interval = [(1, 'iteration')]
+        self.values = []
+
+    def register(self, trainer):
+        pass
+
+    def iteration(self, it, inputs, target, output, loss):
+        self.values.append(loss.detach().clone())
+
+
+def _train(dtype, batches, graphs):
+    import bench
+    import nn as snn
+    import optim
+    import trainer as TR
+    _, pred = bench.make_model(dtype)
+    pred = pred.to(DEV)
+    opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3))
+    old = TR.GRAPHS
+    TR.GRAPHS = graphs
+    try:
+        tr = TR.Trainer(pred, snn.sequence_nll_loss_bits, opt, batches, True, None)
+        mon = _Losses()
+        tr.register_plugin(mon)
+        for q in tr.plugin_queues.values():
+            import heapq
+            heapq.heapify(q)
+        tr.train()
+    finally:
+        TR.GRAPHS = old
+    torch.cuda.synchronize()
+    losses = [float(v) for v in mon.values]
+    params = {k: p.detach().float().cpu().clone() for k, p in pred.named_parameters()}
+    steps = {int(opt.state[p]['step'].item()) for p in pred.parameters() if p in opt.state}
+    return losses, params, steps, tr, opt
+
+
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float32])
+def test_graph_replay_matches_eager(hip, dtype):
+    import bench
+    B, T, L = 64, 1024, 64
+    raw = bench.synth_batches(B, T, L, 8, 0)
+    # two sequences of four chunks: fresh, carried x3, fresh, carried x3
+    raw = [(a, n % 4 == 0, t, c, s) for n, (a, _, t, c, s) in enumerate(raw)]
+    batches = bench.gpu_batches(raw, DEV)
+    le, pe, se, _, _ = _train(dtype, batches, False)
+    lg, pg, sg, tr, opt = _train(dtype, batches, True)
+    print('eager', le)
+    print('graph', lg, 'replayed', tr.graph_steps, 'kinds', len(tr.graphs))
+    # step 0 (no optimizer state yet) and step 1 (first carried step) run eagerly; the 2nd
+    # carried step is captured; the 2nd fresh step (step 4) is the first of its kind with
+    # optimizer state, so eager again; everything else replays
+    assert tr.graph_steps == 5
+    assert se == sg == {8}
+    assert int(opt.dsteps.t[0].item()) == 8
+    exact = dtype == torch.bfloat16
+    np.testing.assert_allclose(lg, le, rtol=1e-6 if exact else 2e-5, atol=0)
+    for k in pe:
+        np.testing.assert_allclose(pg[k].numpy(), pe[k].numpy(), rtol=1e-5 if exact else 0,
+                                   atol=1e-7 if exact else 2e-3, err_msg=k)
+
+
+def test_device_step_adam_matches_host_step(hip):
+    import custom_ops  # noqa: F401
+    g = torch.Generator().manual_seed(5)
+    for step in (1, 2, 7, 1000, 123456):
+        ps = [torch.randn(1000, generator=g).to(DEV), torch.randn(3, 129, generator=g).to(DEV)]
+        gs = [torch.randn_like(p) * 2 for p in ps]
+        ms = [torch.randn_like(p) * 0.1 for p in ps]
+        vs = [torch.rand_like(p) * 0.01 for p in ps]
+        a = [[t.clone() for t in ts] for ts in (ps, gs, ms, vs)]
+        b = [[t.clone() for t in ts] for ts in (ps, gs, ms, vs)]
+        torch.ops.srnn.adam_clip_(*a, [None, None], 1.0, -1.0, 1.0, 1e-3, 0.9, 0.999, 1e-8,
+                                  step)
+        d = torch.tensor([step - 1], dtype=torch.int64, device=DEV)
+        torch.ops.srnn.adam_clip_(*b, [None, None], 1.0, -1.0, 1.0, 1e-3, 0.9, 0.999, 1e-8,
+                                  0, d)
+        for x, y in zip(a, b):
+            for u, v in zip(x, y):
+                assert torch.equal(u, v), step
+
+
+def test_step_advance_skips_while_flag_up(hip):
+    import custom_ops  # noqa: F401
+    import samplernn_hip as H
+    d = torch.tensor([3, 10], dtype=torch.int64, device=DEV)
+    torch.ops.srnn.step_advance_(d)
+    assert d.tolist() == [4, 11]
+    one = torch.ones(1, device=DEV)
+    H.lib().call('srnn_persistent_flag_or', H.ptr(one), H.dcode(torch.float32), H.stream())
+    torch.ops.srnn.step_advance_(d)
+    assert d.tolist() == [4, 11]
+    with pytest.raises(RuntimeError):
+        H.check_persistent_errors()          # takes (clears) the flag
+    torch.ops.srnn.step_advance_(d)
+    assert d.tolist() == [5, 12]
