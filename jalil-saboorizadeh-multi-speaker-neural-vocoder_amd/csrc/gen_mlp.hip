@@ -157,6 +157,8 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     using F = typename GmT<T>::frag;
     constexpr int GV = GmT<T>::GV, UK = GmT<T>::UK, EPL = UK / 4;
     constexpr int Q = gm::Q;
+    constexpr int HU = UPW > 4 ? 4 : UPW;
+    static_assert(UPW % HU == 0, "gen_mlp: UPW must be a multiple of the fetch chunk");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int D = DC ? DC : a.D, R = DC ? 8 : a.R, CW = DC ? 64 : a.CW;
@@ -169,8 +171,12 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     //  shift the 16-B alignment of the dynamic base)
     int* gsh = (int*)(smem + ((((size_t)gm::Q * CW * sizeof(T) + 15) & ~(size_t)15) +
                               (size_t)min(gm::NW, (D + UK - 1) / UK) *
-                                  max(CW / 16, NZ / 16) * 64 * sizeof(floatx4) +
+                                  max(CW / 16, NZ / 16) * 32 * sizeof(floatx4) +
                               (size_t)R * gm::HIST * 4));
+    // WOL (fp32, D = 1024): the W_out slice lives in LDS after the word block, rows padded to
+    // D + 8 floats (conflict-free ds_read_b128 B fragments), instead of in 32 VGPRs
+    constexpr bool WOL = std::is_same<T, float>::value && UPW > 4;
+    const T* wol = (const T*)((char*)gsh + 16);
     const int p = blockIdx.x / a.G;
     const int c0 = p * CW, z0 = p * NZ;
     const int NU = (D + UK - 1) / UK;
@@ -191,16 +197,16 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                                   : nullptr;
 #define GM_W(k) do { if (dgw && s >= 2 && s < 5) dgw[(s - 2) * 16 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
     GM_STAMP();
-    // LDS: [tab15 Q x CW][red KW x ntm x 64 floatx4][hist R x HIST]
+    // LDS: [tab15 Q x CW][red KW x ntm x 32 floatx4][hist R x HIST][words][W_out slice (WOL)]
     T* tab15 = (T*)smem;
     size_t lo = ((size_t)Q * CW * sizeof(T) + 15) & ~(size_t)15;
     floatx4* red = (floatx4*)(smem + lo);
-    lo += (size_t)KW * ntm * 64 * sizeof(floatx4);
+    lo += (size_t)KW * ntm * 32 * sizeof(floatx4);   // rows 0..7 of each 16 x 16 tile (R <= 8)
     int* hist = (int*)(smem + lo);
     const __amdgpu_buffer_rsrc_t rx1 = hx_rsrc(a.xa1), rx2 = hx_rsrc(a.xa2), rxz = hx_rsrc(a.xz);
 
     // ---- resident weights: B fragments of this wave's K units
-    F wh[UPW][NT], wo[UPW][NZT];
+    F wh[UPW][NT], wo[WOL ? 1 : UPW][NZT];
     // (loads from clamped addresses with no branches, so all of them are in flight at once;
     //  fragments outside the shape are zeroed afterwards)
     const int g = blockIdx.x % a.G;
@@ -218,7 +224,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                     __hip_atomic_store(nxt + j, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
-        uint4 lw[UPW][NT], lz[UPW][NZT];
+        uint4 lw[UPW][NT], lz[WOL ? 1 : UPW][NZT];
 #pragma unroll
         for (int j = 0; j < UPW; ++j) {
             const int u = wave + gm::NW * j;
@@ -228,10 +234,22 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 const int n = min(c0 + t * 16 + (lane & 15), D - 1);
                 lw[j][t] = *reinterpret_cast<const uint4*>((const T*)a.w_hid + (int64_t)n * D + ke);
             }
+            if constexpr (!WOL) {
 #pragma unroll
-            for (int t = 0; t < NZT; ++t) {
-                const int n = min(z0 + t * 16 + (lane & 15), Q - 1);
-                lz[j][t] = *reinterpret_cast<const uint4*>((const T*)a.w_out + (int64_t)n * D + ke);
+                for (int t = 0; t < NZT; ++t) {
+                    const int n = min(z0 + t * 16 + (lane & 15), Q - 1);
+                    lz[j][t] = *reinterpret_cast<const uint4*>((const T*)a.w_out + (int64_t)n * D + ke);
+                }
+            }
+        }
+        if constexpr (WOL) {
+            // rows z0 .. z0 + 15 of W_out into LDS (16-B pieces; NZ = 16 at D = 1024)
+            const int pr = D / 4;
+            for (int e = tid; e < 16 * pr; e += gm::NTHR) {
+                const int n = e / pr, k = (e - n * pr) * 4;
+                *reinterpret_cast<uint4*>((T*)wol + (size_t)n * (D + 8) + k) =
+                    *reinterpret_cast<const uint4*>((const T*)a.w_out +
+                                                    (int64_t)min(z0 + n, Q - 1) * D + k);
             }
         }
         constexpr int PER = 16 / sizeof(T);
@@ -268,11 +286,13 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 wh[j][t] = gm_frag<F>(v ? lw[j][t].x : 0u, v ? lw[j][t].y : 0u,
                                       v ? lw[j][t].z : 0u, v ? lw[j][t].w : 0u);
             }
+            if constexpr (!WOL) {
 #pragma unroll
-            for (int t = 0; t < NZT; ++t) {
-                const bool v = kv && t < nzt;
-                wo[j][t] = gm_frag<F>(v ? lz[j][t].x : 0u, v ? lz[j][t].y : 0u,
-                                      v ? lz[j][t].z : 0u, v ? lz[j][t].w : 0u);
+                for (int t = 0; t < NZT; ++t) {
+                    const bool v = kv && t < nzt;
+                    wo[j][t] = gm_frag<F>(v ? lz[j][t].x : 0u, v ? lz[j][t].y : 0u,
+                                          v ? lz[j][t].z : 0u, v ? lz[j][t].w : 0u);
+                }
             }
         }
         // newest-tap table slice (Q x CW, loaded in 16-B pieces above, before the census wait)
@@ -304,7 +324,15 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     // (7 registers across the loop) so the gate update after it waits only for the LUT
     const int tr = tid / CW, tb = g * R + tr, tu = c0 + (tid - tr * CW);
     float tg[7];
-    if (a.tk && tr < R && tb < B && tu < D) {
+    // (WOL: loaded after the loop instead -- 7 registers the fp32 loop cannot spare)
+    auto load_tick = [&]() {
+        const float* gr = a.tk->G + (int64_t)tb * a.tk->ldg;
+        const float* hr = a.tk->gh + (int64_t)tb * a.tk->ldgh;
+        tg[0] = gr[tu]; tg[1] = gr[D + tu]; tg[2] = gr[2 * D + tu];
+        tg[3] = hr[tu]; tg[4] = hr[D + tu]; tg[5] = hr[2 * D + tu];
+        tg[6] = a.tk->hp[(int64_t)tb * D + tu];
+    };
+    if (!WOL && a.tk && tr < R && tb < B && tu < D) {
         const float* gr = a.tk->G + (int64_t)tb * a.tk->ldg;
         const float* hr = a.tk->gh + (int64_t)tb * a.tk->ldgh;
         tg[0] = gr[tu]; tg[1] = gr[D + tu]; tg[2] = gr[2 * D + tu];
@@ -377,22 +405,34 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
 #pragma unroll
             for (int t = 0; t < NT; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
             // the next sample's table gathers go in flight under the a1 hand-off
-            auto work = [&]() { if (s + 1 < a.nsteps) issue_part(i + 1); };
+            // (WOL: after the a2 products instead -- the gathers' 15 registers would be live
+            //  across them)
+            auto work = [&]() { if (!WOL && s + 1 < a.nsteps) issue_part(i + 1); };
             if (wave >= KW) work();
             if (wave < KW) {
-                uint32_t w[UPW][4];
-                gm_fetch_a<T, UPW>(rx1, rowg, rv, wave, lane, NU, D, tag, w, a.err, work);
-                GM_W(1);
+                // (HU units per fetch: at UPW = 8 -- fp32, D = 1024 -- the hand-off is read in
+                //  two halves, so its load buffers fit beside the resident weights)
 #pragma unroll
-                for (int j = 0; j < UPW; ++j) {
-                    const F af = gm_frag<F>(w[j][0], w[j][1], w[j][2], w[j][3]);
+                for (int h = 0; h < UPW / HU; ++h) {
+                    uint32_t w[HU][4];
+                    if (h == 0)
+                        gm_fetch_a<T, HU>(rx1, rowg, rv, wave, lane, NU, D, tag, w, a.err, work);
+                    else
+                        gm_fetch_a<T, HU>(rx1, rowg, rv, wave + gm::NW * HU * h, lane, NU, D, tag,
+                                          w, a.err, [] {});
+                    if (h == 0) GM_W(1);
 #pragma unroll
-                    for (int t = 0; t < NT; ++t) Mma<T>::run(acc[t], af, wh[j][t]);
+                    for (int j = 0; j < HU; ++j) {
+                        const F af = gm_frag<F>(w[j][0], w[j][1], w[j][2], w[j][3]);
+#pragma unroll
+                        for (int t = 0; t < NT; ++t) Mma<T>::run(acc[t], af, wh[h * HU + j][t]);
+                    }
                 }
 #pragma unroll
                 for (int t = 0; t < NT; ++t)
-                    if (t < nt) red[(wave * ntm + t) * 64 + lane] = acc[t];
+                    if (t < nt && lane < 32) red[(wave * ntm + t) * 32 + lane] = acc[t];
             }
+            if (WOL && s + 1 < a.nsteps) issue_part(i + 1);
             GM_W(2);
             GM_W(3);
             __syncthreads();
@@ -404,7 +444,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 float pr[gm::NW];
                 #pragma unroll
                 for (int kw = 0; kw < gm::NW; ++kw)
-                    pr[kw] = red[(min(kw, KW - 1) * ntm + t) * 64 + ln][ii];
+                    pr[kw] = red[(min(kw, KW - 1) * ntm + t) * 32 + ln][ii];
                 #pragma unroll
                 for (int kw = 0; kw < gm::NW; ++kw) v += kw < KW ? pr[kw] : 0.f;
                 v = fmaxf(v + bh, 0.f);
@@ -430,19 +470,36 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             auto work = [&]() { if (s + 1 < a.nsteps) finish_part(); };
             if (wave >= KW) work();
             if (wave < KW) {
-                uint32_t w[UPW][4];
-                gm_fetch_a<T, UPW>(rx2, rowg, rv, wave, lane, NU, D, tag, w, a.err, work);
-                GM_W(7);
 #pragma unroll
-                for (int j = 0; j < UPW; ++j) {
-                    const F af = gm_frag<F>(w[j][0], w[j][1], w[j][2], w[j][3]);
+                for (int h = 0; h < UPW / HU; ++h) {
+                    uint32_t w[HU][4];
+                    if (h == 0)
+                        gm_fetch_a<T, HU>(rx2, rowg, rv, wave, lane, NU, D, tag, w, a.err, work);
+                    else
+                        gm_fetch_a<T, HU>(rx2, rowg, rv, wave + gm::NW * HU * h, lane, NU, D, tag,
+                                          w, a.err, [] {});
+                    if (h == 0) GM_W(7);
 #pragma unroll
-                    for (int t = 0; t < NZT; ++t)
-                        if (t < nzt) Mma<T>::run(acc[t], af, wo[j][t]);
+                    for (int j = 0; j < HU; ++j) {
+                        const F af = gm_frag<F>(w[j][0], w[j][1], w[j][2], w[j][3]);
+#pragma unroll
+                        for (int t = 0; t < NZT; ++t) {
+                            if (t >= nzt) continue;
+                            if constexpr (WOL) {
+                                const int u = wave + gm::NW * (h * HU + j);
+                                const int ke = u * UK + (lane >> 4) * EPL;
+                                Mma<T>::run(acc[t], af,
+                                            gm_load16<F>(wol + (size_t)(t * 16 + (lane & 15)) *
+                                                                   (D + 8) + ke));
+                            } else {
+                                Mma<T>::run(acc[t], af, wo[h * HU + j][t]);
+                            }
+                        }
+                    }
                 }
 #pragma unroll
                 for (int t = 0; t < NZT; ++t)
-                    if (t < nzt) red[(wave * ntm + t) * 64 + lane] = acc[t];
+                    if (t < nzt && lane < 32) red[(wave * ntm + t) * 32 + lane] = acc[t];
             }
             GM_W(8);
             __syncthreads();
@@ -454,7 +511,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 float pr[gm::NW];
                 #pragma unroll
                 for (int kw = 0; kw < gm::NW; ++kw)
-                    pr[kw] = red[(min(kw, KW - 1) * ntm + t) * 64 + ln][ii];
+                    pr[kw] = red[(min(kw, KW - 1) * ntm + t) * 32 + ln][ii];
                 #pragma unroll
                 for (int kw = 0; kw < gm::NW; ++kw) v += kw < KW ? pr[kw] : 0.f;
                 hx_put(a.xz + ((size_t)g * R + r) * Q + z0 + c, tag,
@@ -523,6 +580,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         const GenMlpArgs::Tick* tk = a.tk;
         asm volatile("" : "+s"(tk));            // fresh loads of the table after the loop
         if (tr < R && tb < B && tu < D) {
+            if (WOL) load_tick();
             const int inx = i0 + a.nsteps;
             const float* mr = tk->fmin + (int64_t)tu * 16;
             const float* mz = tk->fmin + (int64_t)(D + tu) * 16;
@@ -592,7 +650,7 @@ GmKernel pick_t(int upw, int nzt) {
     if (upw <= 1 && nzt <= 16) return gen_mlp_kernel<T, 1, 4, 16, MAXT, FS0C, 0>;
     if (upw <= 2 && nzt <= 4) return gen_mlp_kernel<T, 2, 4, 4, MAXT, FS0C, 0>;
     if (upw <= 4 && nzt <= 2) return gen_mlp_kernel<T, 4, 4, 2, MAXT, FS0C, 0>;
-    return nullptr;     // fp32 at D > 512 would spill its resident weights: per-step path
+    return nullptr;     // other fp32 shapes at D > 512 would spill their resident weights
 }
 // MAXT = older taps gathered per sample (FS0 - 1 <= MAXT)
 template <typename T>
@@ -602,6 +660,10 @@ GmKernel pick(int upw, int nzt, int fs0, int D, int R) {
     //  dim 1024 in bf16 -- the published model -- has its whole launch shape compiled in)
     if (std::is_same<T, bf16>::value && fs0 == 16 && D == 1024 && R == 8)
         return gen_mlp_kernel<T, 4, 4, 2, 15, 16, 1024>;
+    // fp32 at dim 1024 (the reference's precision): 8 K units per wave, one 16-logit tile
+    // whose W_out rows sit in LDS (WOL)
+    if (std::is_same<T, float>::value && fs0 == 16 && D == 1024 && R == 8)
+        return gen_mlp_kernel<T, 8, 4, 1, 15, 16, 1024>;
     if (fs0 == 16) return pick_t<T, 15, 16>(upw, nzt);
     return fs0 - 1 <= 15 ? pick_t<T, 15, 0>(upw, nzt) : pick_t<T, 31, 0>(upw, nzt);
 }
@@ -642,9 +704,11 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     const int KW = NU < gm::NW ? NU : gm::NW;
     const int ntm = (CW / 16) > (NZ / 16) ? CW / 16 : NZ / 16;
     size_t lds = ((size_t)gm::Q * CW * es + 15) & ~(size_t)15;
-    lds += (size_t)KW * ntm * 64 * 16;
+    lds += (size_t)KW * ntm * 32 * 16;                // rows 0..7 of the 16-row tiles (R = 8)
     lds += (size_t)R * gm::HIST * 4;
     lds += 16;                                        // group / member / mode words
+    if (dtype == SRNN_F32 && upw > 4)                 // W_out slice in LDS (gen_mlp_kernel WOL)
+        lds += (size_t)NZ * (D + 8) * 4;
     if (lds > 160 * 1024) return 0;
     pl->ok = 1;
     pl->local = env_flag("SRNN_GEN_LOCAL", 1);

@@ -38,7 +38,8 @@ def generate(m, n_seqs, cond, spk, persistent, **kw):
 
 
 @pytest.mark.parametrize('D,B,n_cond,n_rnn', [(64, 5, 3, 1), (32, 3, 2, 2), (256, 24, 2, 1),
-                                              (512, 40, 2, 1)])
+                                              (512, 40, 2, 1), (1024, 128, 2, 1),
+                                              (1024, 9, 2, 1)])
 def test_persistent_matches_per_sample_fp32(hip, D, B, n_cond, n_rnn):
     cfg = dict(recipe.CONFIGS['t3'], dim=D, n_rnn=n_rnn)
     m, _ = build(cfg, 7, torch.float32)
