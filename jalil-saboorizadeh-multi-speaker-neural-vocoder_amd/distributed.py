@@ -124,12 +124,21 @@ class GradAllReduce:
     reductions run under the rest of the backward; __call__ then only waits.  Groups whose
     grads never arrive this step (h0 on non-reset chunks) are reduced at the sync point.
     A persistent GRU sweep enqueued while reductions are in flight first makes the stream
-    wait for them (_fence): RCCL kernels and a sweep never share the CUs.  close() removes the
-    hooks and the fence.
+    wait for them (_fence): RCCL kernels and a sweep never share the CUs.  So that the fence
+    does not hold a sweep behind a large bucket that became ready just before it (the bottom
+    tier's 92 MB in front of the top tier's reverse sweep), a ready bucket is launched only
+    once the next persistent sweep has been enqueued (_after_sweep, samplernn_hip
+    AFTER_PERSISTENT) -- its pack and RCCL kernels are then ordered after that sweep and run
+    under the GEMMs that follow it -- or at the sync point at the latest (defer=False, or
+    env SRNN_DP_DEFER=0, launches at once).  close() removes the hooks and the fence.
     """
 
-    def __init__(self, bucket_mb=64, group=None, overlap_groups=None, grad_dtype=None):
+    def __init__(self, bucket_mb=64, group=None, overlap_groups=None, grad_dtype=None,
+                 defer=None):
         self.bucket_bytes = int(bucket_mb * (1 << 20))
+        self.defer = os.environ.get('SRNN_DP_DEFER', '1') != '0' if defer is None else defer
+        self._deferred = []         # ready buckets waiting for the next sweep's enqueue
+        self._after_ref = None
         self.group = group
         self.grad_dtype = _grad_dtype(grad_dtype)
         self._bufs = {}
@@ -231,6 +240,8 @@ class GradAllReduce:
         ref = weakref.WeakMethod(self._fence)
         self._fence_ref = ref
         H.BEFORE_PERSISTENT.append(ref)
+        self._after_ref = weakref.WeakMethod(self._after_sweep)
+        H.AFTER_PERSISTENT.append(self._after_ref)
         self._groups = []
         for gi, params in enumerate(groups):
             for bi, bucket in enumerate(self._split(params)):
@@ -259,7 +270,8 @@ class GradAllReduce:
         if self._fence_ref is not None:
             import samplernn_hip as H
             H.BEFORE_PERSISTENT[:] = [f for f in H.BEFORE_PERSISTENT if f is not self._fence_ref]
-            self._fence_ref = None
+            H.AFTER_PERSISTENT[:] = [f for f in H.AFTER_PERSISTENT if f is not self._after_ref]
+            self._fence_ref = self._after_ref = None
         self._bufs = {}
         self._groups = None
 
@@ -276,8 +288,23 @@ class GradAllReduce:
         idx = self._owner[id(p)]
         self._ready[idx] += 1
         key, bucket = self._groups[idx]
-        if self._ready[idx] == len(bucket) and idx not in self._pending:
+        if self._ready[idx] == len(bucket) and idx not in self._pending and \
+                idx not in self._deferred:
+            if self.defer:
+                self._deferred.append(idx)
+            else:
+                self._pending[idx] = self._launch(key, bucket, True)
+
+    def _launch_deferred(self):
+        for idx in self._deferred:
+            key, bucket = self._groups[idx]
             self._pending[idx] = self._launch(key, bucket, True)
+        self._deferred = []
+
+    def _after_sweep(self):
+        """Right after a persistent sweep is enqueued: start the buckets that became ready
+        before it (ordered after it on the stream)."""
+        self._launch_deferred()
 
     def __call__(self, optimizer, fused=False):
         """Reduce this step's gradients.  fused=True (the device clip+Adam): leave them in the
@@ -293,6 +320,7 @@ class GradAllReduce:
             # all persistent sweeps of the step: it rides in the last bucket launched here, or
             # alone when the hooks already launched every bucket (reset chunks)
             late = [idx for idx in range(len(self._groups)) if idx not in self._pending]
+            self._deferred = []                       # (launched below, in index order)
             dev = self._groups[0][1][0].is_cuda
             for idx in late:                          # grads that never arrived this step
                 key, bucket = self._groups[idx]

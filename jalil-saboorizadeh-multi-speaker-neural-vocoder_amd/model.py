@@ -512,6 +512,8 @@ def tier_backward(ctx, dY, need_h0):
                          H.ptr(h_in[l]), H.ptr(WhhT), H.ptr(dGH), H.ptr(dGHT), H.ptr(dGI),
                          Fr * 3 * D, 3 * D, H.ptr(ddir[0]), H.ptr(work), work.numel() * 4,
                          st())
+        if seq:
+            H.after_persistent_sweep()    # (DP: gradient buckets ready before it go out now)
         _STATS['gru_cell_bwd_steps'] += 0 if seq else Fr
         for t in reversed(range(Fr)) if not seq else ():
             nxt = t + 1 < Fr

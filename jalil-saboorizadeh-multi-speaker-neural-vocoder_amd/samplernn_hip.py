@@ -181,6 +181,11 @@ def exported_symbols():
 # wait on each other across ranks.  distributed.GradAllReduce registers a callback that makes
 # the current stream wait for every gradient all-reduce already in flight.
 BEFORE_PERSISTENT = []
+# ... and AFTER_PERSISTENT right after a sweep is enqueued: GradAllReduce launches the
+# all-reduces of buckets that became ready before the sweep here, so their RCCL kernels are
+# ordered after it (they overlap the GEMMs that follow) instead of in front of it, where the
+# next sweep's fence would wait for them.
+AFTER_PERSISTENT = []
 
 # Measurement hook (bench.py): when a dict, the step's heaviest launch sites (the GRU sweeps,
 # the dTab scatter, the MLP hidden-layer GEMM, the fused clip+Adam, ...) are bracketed by HIP
@@ -207,11 +212,11 @@ def roof_end(site, ev0, work):
     ROOF_EVENTS.setdefault(site, []).append((ev0, ev1, float(work)))
 
 
-def before_persistent_sweep():
+def _run_hooks(lst):
     """Run the registered callbacks (plain callables or weakref.WeakMethod references, whose
     dead entries -- a GradAllReduce that is gone -- are dropped)."""
     dead = []
-    for f in BEFORE_PERSISTENT:
+    for f in lst:
         if isinstance(f, weakref.WeakMethod):
             m = f()
             if m is None:
@@ -221,7 +226,15 @@ def before_persistent_sweep():
         else:
             f()
     for f in dead:
-        BEFORE_PERSISTENT.remove(f)
+        lst.remove(f)
+
+
+def before_persistent_sweep():
+    _run_hooks(BEFORE_PERSISTENT)
+
+
+def after_persistent_sweep():
+    _run_hooks(AFTER_PERSISTENT)
 
 
 def check_persistent_errors():

@@ -42,7 +42,8 @@ class _Toy(torch.nn.Module):
             if t == T // 2:
                 # stands in for a persistent GRU sweep inside the backward: the fence makes
                 # it wait for every all-reduce already in flight (results must not change)
-                h.register_hook(lambda g: (H.before_persistent_sweep(), g)[1])
+                h.register_hook(lambda g: (H.before_persistent_sweep(),
+                                           H.after_persistent_sweep(), g)[2])
             out.append(h)
         return torch.stack(out, 1), h.detach()
 
@@ -74,7 +75,7 @@ def _train(model, data, rows, grad_sync):
     return losses, [p.detach().clone() for p in model.parameters()]
 
 
-def _worker(rank, world, port, q, overlap=False):
+def _worker(rank, world, port, q, overlap=False, defer=True):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     import distributed as D
@@ -86,7 +87,8 @@ def _worker(rank, world, port, q, overlap=False):
     # its own group (it has no grad on non-reset chunks in the real model)
     groups = [[model.U], [model.W], [model.h0]] if overlap else None
     losses, params = _train(model, data, rows,
-                            D.GradAllReduce(bucket_mb=0.0001, overlap_groups=groups))
+                            D.GradAllReduce(bucket_mb=0.0001, overlap_groups=groups,
+                                            defer=defer))
     loss_t = torch.tensor(losses)
     dist.all_reduce(loss_t)
     if rank == 0:
@@ -94,12 +96,13 @@ def _worker(rank, world, port, q, overlap=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('overlap', [False, True])
-def test_dp_two_ranks_equals_full_batch(overlap):
+@pytest.mark.parametrize('overlap,defer', [(False, True), (True, True), (True, False)])
+def test_dp_two_ranks_equals_full_batch(overlap, defer):
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, overlap, defer))
+             for r in range(2)]
     for p in procs:
         p.start()
     losses_dp, params_dp = q.get(timeout=120)
@@ -217,3 +220,26 @@ def test_bucket_offsets_aligned():
     ps = [torch.nn.Parameter(torch.zeros(n)) for n in (3, 64, 65, 1)]
     offs, total = D.GradAllReduce._offsets(ps)
     assert offs == [0, 64, 128, 256] and total == 320
+
+
+def test_ready_buckets_wait_for_the_next_sweep():
+    """defer (default): a bucket whose gradients are complete is launched right after the next
+    persistent sweep is enqueued (samplernn_hip.AFTER_PERSISTENT), so the sweep's fence never
+    waits for it; the sync point launches whatever is still deferred, in index order."""
+    import distributed as D
+    import samplernn_hip as H
+    a, b = torch.nn.Parameter(torch.zeros(3)), torch.nn.Parameter(torch.zeros(2))
+    sync = D.GradAllReduce(bucket_mb=1, defer=True)
+    sync._install([[a], [b]])
+    launched = []
+    sync._launch = lambda key, bucket, async_op, flag=False: (launched.append(key),
+                                                             (None, _Work()))[1]
+    sync._on_grad(a)
+    assert launched == [] and sync._deferred == [0]
+    H.before_persistent_sweep()                  # nothing in flight: nothing to wait for
+    H.after_persistent_sweep()                   # the sweep is enqueued: bucket 0 goes
+    assert launched == [(0, 0)] and 0 in sync._pending and sync._deferred == []
+    sync._on_grad(b)
+    assert launched == [(0, 0)] and sync._deferred == [1]
+    sync.close()
+    assert sync._after_ref is None
