@@ -15,6 +15,7 @@
 // integer atomics into a zeroed int64 buffer; a final pass converts to fp32/bf16 in the
 // q-major layout [q][k][:] the dE / dW GEMMs consume.
 #include <algorithm>
+#include <type_traits>
 
 #include "samplernn_hip_internal.hpp"
 
@@ -305,6 +306,30 @@ __global__ __launch_bounds__(256) void dtab_prep_kernel(const T* __restrict__ da
         float m = 0.f;
         const int64_t r0 = nrows * blockIdx.x / nb_da, r1 = nrows * (blockIdx.x + 1) / nb_da;
         const int nv = D / V;
+        if (std::is_same<T, bf16>::value && ldda == D && D % V == 0) {
+            // contiguous bf16 rows: one flat stream of 16-B vectors, 4 in flight per thread;
+            // |x| of a bf16 is its low 15 bits, whose unsigned order is the magnitude order,
+            // so the max runs on integers (3 VALU per 2 values)
+            const uint4* p = reinterpret_cast<const uint4*>(da + r0 * D);
+            const int64_t n = (r1 - r0) * nv;
+            unsigned mm = 0;
+            auto take = [&](uint4 u) {
+                const unsigned w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    mm = max(mm, max(w[i] & 0x7fffu, (w[i] >> 16) & 0x7fffu));
+            };
+            int64_t j = tid;
+            for (; j + 3 * 256 < n; j += 4 * 256) {
+                uint4 u[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) u[k] = p[j + k * 256];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) take(u[k]);
+            }
+            for (; j < n; j += 256) take(p[j]);
+            m = __uint_as_float(mm << 16);
+        } else
         for (int64_t r = r0; r < r1; ++r) {
             const T* row = da + r * ldda;
             for (int j = tid; j < nv; j += 256) {
@@ -407,10 +432,20 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
             return (unsigned long long)(long long)lo + ((unsigned long long)(unsigned)hi << 32);
         };
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // strip reads of the last rows
-        for (int q = lane; q < 2 * WPB; q += 64) {
-            const int r = q >= WPB, pp = q - r * WPB;
-            const int row = b2 + r;
-            strip[q] = (row < B && pp < W) ? (unsigned char)x[(int64_t)row * ldx + xoff + pp] : 0;
+        // the two rows' indices into the strip: 12 loads in flight per lane per round (one
+        // load per round trip was ~40 serialised HBM latencies per row pair)
+        for (int q0 = lane; q0 < 2 * WPB; q0 += 64 * 12) {
+            long long v[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) {
+                const int q = q0 + 64 * k;
+                const int r = q >= WPB, pp = q - r * WPB;
+                const int row = b2 + r;
+                v[k] = (q < 2 * WPB && row < B && pp < W) ? x[(int64_t)row * ldx + xoff + pp] : 0;
+            }
+#pragma unroll
+            for (int k = 0; k < 12; ++k)
+                if (q0 + 64 * k < 2 * WPB) strip[q0 + 64 * k] = (unsigned char)v[k];
         }
         unsigned long long cur = 0;
         unsigned long long nxt = load(0);
@@ -431,18 +466,13 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
             const int jmax = min(16, W - pbase);
             unsigned ad[16];
             unsigned long long va[16];
-            // the two halves' 16 indices: uniform per half, extracted on the scalar unit
-            unsigned q0[4], q1[4];
-#pragma unroll
-            for (int w = 0; w < 4; ++w) {
-                q0[w] = __builtin_amdgcn_readlane(qc[w], 0);
-                q1[w] = __builtin_amdgcn_readlane(qc[w], 32);
-            }
+            // the 16 indices of this lane's half, from its own broadcast read: a bit-field
+            // extract and a shift-add per atomic on the VALU (the scalar unit is shared by the
+            // CU's 16 waves; extracting two halves there cost 6 SALU per atomic)
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                const unsigned a0 = ((q0[j >> 2] >> (8 * (j & 3))) & 0xffu) * (unsigned)(2 * FS * 8);
-                const unsigned a1 = ((q1[j >> 2] >> (8 * (j & 3))) & 0xffu) * (unsigned)(2 * FS * 8);
-                ad[j] = lb[j] + (h ? a1 : a0);
+                const unsigned qv = __builtin_amdgcn_ubfe(qc[j >> 2], 8 * (j & 3), 8);
+                ad[j] = lb[j] + qv * (unsigned)(2 * FS * 8);
                 va[j] = li <= j ? nv : cur;
             }
             if (jmax == 16) {
