@@ -642,7 +642,10 @@ __device__ __forceinline__ bf16x8 g3p_frag(const char* img, int f0, int u, int l
     }
 }
 
-template <typename TO, bool KCA, bool KCB, bool SW, bool MB = false>
+// PF: the k-unit 1 fragments of a stage are read into a second register set while unit 0's
+// MFMAs run (3 reads after each of its last four MFMA rows), so the unit-1 MFMAs do not wait
+// for a burst of 12 LDS reads.
+template <typename TO, bool KCA, bool KCB, bool SW, bool MB = false, bool PF = false>
 __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -716,6 +719,7 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     if (S > 0) issue_all(smem);
 
     bf16x8 a[8], b[4];
+    bf16x8 a1[PF ? 8 : 1], b1[PF ? 4 : 1];
     int ic = 0, ktc = 0;
     int epi = 0;                               // stores of the just-finished tile's epilogue
     auto read_unit = [&](const char* img, int u) {
@@ -729,6 +733,21 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
         for (int j = 0; j < 4; ++j)
             acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[j], a[i], acc[i][j], 0, 0, 0)
                            : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    };
+    auto mfma_row1 = [&](int i) {
+        if constexpr (PF) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                acc[i][j] = SW ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j], a1[i], acc[i][j], 0, 0, 0)
+                               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[i], b1[j], acc[i][j], 0, 0, 0);
+        }
+    };
+    // fragment f (0..11) of unit 1: B fragments first, then A
+    auto read1 = [&](const char* img, int f) {
+        if constexpr (PF) {
+            if (f < 4) b1[f] = g3p_frag<KCB>(img + g3p::OPB, wn * 64 + f * 16, 1, lane);
+            else a1[f - 4] = g3p_frag<KCA>(img, wm * 128 + (f - 4) * 16, 1, lane);
+        }
     };
     auto finish_stage = [&]() {
         if (++ktc == nk) {
@@ -763,22 +782,48 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
         mfma_row(1); glds(pa0 + stepA, nimg, 2); glds(pa1 + stepA, nimg, 3);
         mfma_row(2); glds(pb0, nimg + g3p::OPB, 0); glds(pb1, nimg + g3p::OPB, 1);
         mfma_row(3); glds(pb0 + stepB, nimg + g3p::OPB, 2); glds(pb1 + stepB, nimg + g3p::OPB, 3);
+        if constexpr (PF) {
 #pragma unroll
-        for (int i = 4; i < 8; ++i) mfma_row(i);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+            for (int i = 4; i < 8; ++i) {
+                mfma_row(i);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-            __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+                for (int f = 0; f < 3; ++f) read1(img, 3 * (i - 4) + f);
+            }
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) mfma_row1(i);
+            __builtin_amdgcn_s_setprio(0);
+        } else {
+#pragma unroll
+            for (int i = 4; i < 8; ++i) mfma_row(i);
+            __builtin_amdgcn_s_setprio(0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+                __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            read_unit(img, 1);
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) mfma_row(i);
+            __builtin_amdgcn_s_setprio(0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x008, 16, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        read_unit(img, 1);
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) mfma_row(i);
-        __builtin_amdgcn_s_setprio(0);
         finish_stage();
     }
     if (s < S) {
@@ -1121,10 +1166,17 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
     const bool pp = mode == 3 && k64;
     const bool q = mode == 4;
     const bool pair = !pp && !q && (mode == 1 || (mode == 2 && (KCA || KCB))) && k64;
+    // unit-1 fragment prefetch (gemm3p PF): measured 14 % faster on the bf16 NT shapes (MLP
+    // hidden forward, upsampling forward, B = 512), 3 % on NN; slower on the fp32-output NT
+    // logits GEMM (N = 256), which keeps the plain schedule.  SRNN_G3_PF=0/1 overrides.
+    const int pfe = env_flag("SRNN_G3_PF", -1);
+    const bool pf = pfe >= 0 ? pfe != 0 : !(sizeof(TO) == 4 && KCA && KCB);
     auto k = q ? gemm3q_kernel<TO, KCA, KCB, SW>
                : pp ? gemm3pp_kernel<TO, KCA, KCB, SW>
-                    : pair ? gemm3p_kernel<TO, KCA, KCB, SW> : gemm3_kernel<TO, KCA, KCB, SW>;
-    int ki = q ? 3 : pp ? 2 : pair ? 1 : 0;
+                    : pair ? (pf ? gemm3p_kernel<TO, KCA, KCB, SW, false, true>
+                                 : gemm3p_kernel<TO, KCA, KCB, SW>)
+                           : gemm3_kernel<TO, KCA, KCB, SW>;
+    int ki = q ? 3 : pp ? 2 : pair ? (pf ? 8 : 1) : 0;
     if constexpr (sizeof(TO) == 2 && SW) {
         if (g.mbi || g.mbo) {        // ReLU bit masks (srnn_gemm3_try admits modes 0-2 only)
             k = pair ? gemm3p_kernel<TO, KCA, KCB, SW, true> : gemm3_kernel<TO, KCA, KCB, SW, true>;
@@ -1132,7 +1184,7 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
         }
     }
     const int lds = (pp || pair) ? g3p::LDS : g3::LDS;
-    static bool attr[8] = {false, false, false, false, false, false, false, false};
+    static bool attr[9] = {false, false, false, false, false, false, false, false, false};
     if (!attr[ki]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds));

@@ -23,7 +23,12 @@ hidden state lives in static buffers the graph reads and rewrites; the Adam step
 read from a device counter (optim.DeviceSteps) so replays keep the bias correction exact.
 Anything a captured step cannot honour falls back to the eager step: roofline probes on
 (bench.py's per-kernel timing), a data-parallel gradient hook (unless SRNN_GRAPH_DP=1), a
-criterion or model without the Predictor's hidden-state carry.
+model without the Predictor's hidden-state carry, and any criterion other than the
+reference's `nn.sequence_nll_loss_bits` (user code runs inside the capture and may
+synchronise, e.g. read the loss with .item(); SRNN_GRAPH=force captures it anyway, and a
+capture that fails rolls the step's host state back and runs it eagerly).  After a replay
+every parameter's .grad is the graph's gradient tensor, holding this step's clamped gradient
+as after an eager step (optim.py:11-13).
 """
 import heapq
 import os
@@ -34,6 +39,7 @@ import torch
 import samplernn_hip as H
 
 GRAPHS = os.environ.get('SRNN_GRAPH', '1') != '0'
+FORCE = os.environ.get('SRNN_GRAPH', '1') == 'force'
 
 
 class _StepGraph:
@@ -43,6 +49,7 @@ class _StepGraph:
         self.x, self.tgt, self.cond, self.spk = x, tgt, cond, spk
         self.graph = None
         self.out = self.loss = None
+        self.grads = []             # (parameter, the graph's gradient tensor or None)
         self.replays = 0
 
 
@@ -71,6 +78,7 @@ class Trainer(object):
         self._seen = set()          # step kinds that ran eagerly once
         self._hbuf = {}             # (tier index, rows) -> static carried hidden state
         self.graph_steps = 0        # steps replayed from a graph (tests, bench.py)
+        self._no_graph = set()      # step kinds whose capture failed
 
     def register_plugin(self, plugin):
         plugin.register(self)
@@ -146,9 +154,11 @@ class Trainer(object):
                 batch_spk = batch_spk.cuda(non_blocking=True)
 
             kind = self._step_kind(batch_inputs, batch_target, batch_cond, batch_spk)
+            plugin_data = None
             if kind is not None and (kind in self.graphs or kind in self._seen):
                 plugin_data = self._graph_step(kind, batch_inputs, batch_target, batch_cond,
                                                batch_spk)
+            if plugin_data is not None:
                 self.enqueue_s += time.perf_counter() - t_enq
                 self._watch.step(self._rollback)
                 self.call_plugins('iteration', self.iterations, batch_inputs, batch_target,
@@ -185,6 +195,9 @@ class Trainer(object):
         """The key of a capturable step, or None when this step must run eagerly."""
         if not (GRAPHS and self.cuda) or H.ROOF_EVENTS is not None:
             return None
+        import nn as snn
+        if self.criterion is not snn.sequence_nll_loss_bits and not FORCE:
+            return None
         opt = self.optimizer
         if not (hasattr(opt, 'graph_ready') and opt.graph_ready()):
             return None
@@ -199,8 +212,9 @@ class Trainer(object):
         ts = (inputs, target, cond, spk)
         if not all(torch.is_tensor(t) and t.is_cuda for t in ts):
             return None
-        return (fresh,) + tuple((tuple(t.shape), t.dtype) for t in ts) + \
+        kind = (fresh,) + tuple((tuple(t.shape), t.dtype) for t in ts) + \
             (opt.graph_signature(),)
+        return None if kind in self._no_graph else kind
 
     def _hidden_bufs(self, rows):
         """Static carried hidden state per tier (n_rnn, rows, dim) fp32."""
@@ -234,6 +248,8 @@ class Trainer(object):
                     model.hidden_states[rnn] = b
         if sg is None:
             sg = self._capture(kind, inputs, target, cond, spk, bufs)
+            if sg is None:
+                return None                       # capture failed: run the step eagerly
         else:
             sg.x.copy_(inputs)
             sg.tgt.copy_(target)
@@ -242,6 +258,8 @@ class Trainer(object):
             self.optimizer.before_replay()
             sg.graph.replay()
             self.optimizer.after_replay()
+            for p, gr in sg.grads:
+                p.grad = gr
         sg.replays += 1
         self.graph_steps += 1
         for rnn, b in zip(rnns, bufs):
@@ -258,6 +276,11 @@ class Trainer(object):
         rnns = model.model.frame_level_rnns
         self._zero_grad()
         self.optimizer.before_replay()
+        # host state the capture's Python side effects change, for a roll-back on failure
+        saved_hidden = dict(model.hidden_states)
+        opt = self.optimizer
+        saved_steps = [(st, st['step'].clone()) for st in opt.state.values() if 'step' in st]
+        saved_mirror = list(opt.dsteps.mirror)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
         out_loss = [None, None]
@@ -268,18 +291,31 @@ class Trainer(object):
             loss.backward()
             out_loss[0], out_loss[1] = out.data, loss.data
             return loss
-        with torch.cuda.graph(g):     # a private memory pool per step kind
-            self.optimizer.step(closure)
-            for rnn, b in zip(rnns, bufs):
-                h = model.hidden_states[rnn]
-                if h.shape != b.shape or h.dtype != b.dtype:
-                    raise RuntimeError('graph mode: new hidden state %s %s, buffer %s'
-                                       % (tuple(h.shape), h.dtype, tuple(b.shape)))
-                b.copy_(h)
+        try:
+            with torch.cuda.graph(g):     # a private memory pool per step kind
+                self.optimizer.step(closure)
+                for rnn, b in zip(rnns, bufs):
+                    h = model.hidden_states[rnn]
+                    if h.shape != b.shape or h.dtype != b.dtype:
+                        raise RuntimeError('graph mode: new hidden state %s %s, buffer %s'
+                                           % (tuple(h.shape), h.dtype, tuple(b.shape)))
+                    b.copy_(h)
+        except Exception as e:  # noqa: BLE001 -- any capture failure: roll back, run eagerly
+            import warnings
+            torch.cuda.synchronize()
+            model.hidden_states.clear()
+            model.hidden_states.update(saved_hidden)
+            for st, v in saved_steps:
+                st['step'] = v
+            opt.dsteps.mirror = [None] * len(saved_mirror)   # re-seeded at the next step
+            self._zero_grad()
+            self._no_graph.add(kind)
+            warnings.warn('graph mode: capture failed (%s: %s); this step kind runs eagerly'
+                          % (type(e).__name__, e))
+            return None
         sg.graph = g
         sg.out, sg.loss = out_loss
+        sg.grads = [(p, p.grad) for grp in opt.param_groups for p in grp['params']]
         self.graphs[kind] = sg
         g.replay()
-        # replays overwrite the gradients in place: leave none visible as if fresh
-        self._zero_grad()
         return sg

@@ -56,6 +56,9 @@ def _train(dtype, batches, graphs):
     losses = [float(v) for v in mon.values]
     params = {k: p.detach().float().cpu().clone() for k, p in pred.named_parameters()}
     steps = {int(opt.state[p]['step'].item()) for p in pred.parameters() if p in opt.state}
+    grads = {k: (None if p.grad is None else p.grad.detach().float().cpu().clone())
+             for k, p in pred.named_parameters()}
+    _train.grads = grads
     return losses, params, steps, tr, opt
 
 
@@ -68,7 +71,9 @@ def test_graph_replay_matches_eager(hip, dtype):
     raw = [(a, n % 4 == 0, t, c, s) for n, (a, _, t, c, s) in enumerate(raw)]
     batches = bench.gpu_batches(raw, DEV)
     le, pe, se, _, _ = _train(dtype, batches, False)
+    ge = _train.grads
     lg, pg, sg, tr, opt = _train(dtype, batches, True)
+    gg = _train.grads
     print('eager', le)
     print('graph', lg, 'replayed', tr.graph_steps, 'kinds', len(tr.graphs))
     # step 0 (no optimizer state yet) and step 1 (first carried step) run eagerly; the 2nd
@@ -79,6 +84,14 @@ def test_graph_replay_matches_eager(hip, dtype):
     assert int(opt.dsteps.t[0].item()) == 8
     exact = dtype == torch.bfloat16
     np.testing.assert_allclose(lg, le, rtol=1e-6 if exact else 2e-5, atol=0)
+    # after the last (replayed) step every .grad holds that step's clamped gradient, as after
+    # an eager step (None where the step's backward did not reach the parameter)
+    assert ge.keys() == gg.keys()
+    for k in ge:
+        assert (ge[k] is None) == (gg[k] is None), k
+        if ge[k] is not None:
+            np.testing.assert_allclose(gg[k].numpy(), ge[k].numpy(), rtol=1e-3 if exact else 0,
+                                       atol=1e-6 if exact else 2e-3, err_msg=k)
     for k in pe:
         np.testing.assert_allclose(pg[k].numpy(), pe[k].numpy(), rtol=1e-5 if exact else 0,
                                    atol=1e-7 if exact else 2e-3, err_msg=k)
@@ -118,3 +131,54 @@ def test_step_advance_skips_while_flag_up(hip):
         H.check_persistent_errors()          # takes (clears) the flag
     torch.ops.srnn.step_advance_(d)
     assert d.tolist() == [5, 12]
+
+
+def test_capture_failure_falls_back_to_eager(hip):
+    """A criterion that synchronises (reads the loss on the host) cannot be captured: by
+    default graph mode leaves such a criterion alone; forced (SRNN_GRAPH=force), the failed
+    capture rolls back the step's host state and the step runs eagerly -- same losses and
+    Adam step counts as a plain eager run."""
+    import warnings
+    import bench
+    import nn as snn
+    import optim
+    import trainer as TR
+    B, T, L = 16, 1024, 64
+    raw = bench.synth_batches(B, T, L, 4, 0)
+    batches = bench.gpu_batches(raw, DEV)
+
+    def run(graphs, force):
+        _, pred = bench.make_model(torch.bfloat16)
+        pred = pred.to(DEV)
+        opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3))
+        seen = []
+
+        def criterion(out, tgt):
+            loss = snn.sequence_nll_loss_bits(out, tgt)
+            seen.append(float(loss.detach()))           # a host synchronisation
+            return loss
+        old = TR.GRAPHS, TR.FORCE
+        TR.GRAPHS, TR.FORCE = graphs, force
+        try:
+            tr = TR.Trainer(pred, criterion, opt, batches, True, None)
+            with warnings.catch_warnings(record=True) as w:
+                warnings.simplefilter('always')
+                tr.train()
+        finally:
+            TR.GRAPHS, TR.FORCE = old
+        torch.cuda.synchronize()
+        steps = {int(opt.state[p]['step'].item()) for p in pred.parameters() if p in opt.state}
+        return seen, steps, tr, [str(x.message) for x in w]
+
+    l0, s0, _, _ = run(False, False)
+    l1, s1, tr1, w1 = run(True, False)               # not the reference's criterion: eager
+    assert tr1.graph_steps == 0 and not tr1._no_graph
+    l2, s2, tr2, w2 = run(True, True)                # forced: capture fails, rolls back
+    assert tr2.graph_steps == 0 and len(tr2._no_graph) == 1
+    assert any('capture failed' in m for m in w2)
+    assert s0 == s1 == s2 == {4}
+    np.testing.assert_allclose(l1, l0, rtol=1e-6)
+    # the failed capture ran the criterion once more (its float() raised inside the capture),
+    # after that every step is eager again
+    assert len(l2) == 4
+    np.testing.assert_allclose(l2, l0, rtol=1e-6)
