@@ -125,9 +125,9 @@ def site_roofline(site, ms, work_per_step, dtype_peak):
 
 
 SITE_NOTES = {
-    'gru_xcd_bwd': 'gru_xcd_bwd_kernel: the GRU reverse sweeps (every tier, one persistent '
-                   'launch each; dgh_{t+1} W_hh products; latency-bound: one hand-off of dgh '
-                   'per step)',
+    'gru_xcd_bwd': 'gru_xcd_bwd_pk_kernel: the GRU reverse sweeps (every tier, one persistent '
+                   'launch each; dgh_{t+1} W_hh products; bound by reading the hand-off of dgh '
+                   '(16 rows x D {3 x bf16, tag} granules per workgroup and step) from L2)',
     'gru_xcd_fwd': 'gru_xcd_fwd_kernel: the GRU forward sweeps (W_hh h products; one hand-off '
                    'of h per step)',
     'dtab_scatter': 'dtab_pos_kernel: backward of the folded embedding.conv (dTab scatter; '

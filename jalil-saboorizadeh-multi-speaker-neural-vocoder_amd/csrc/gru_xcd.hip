@@ -406,6 +406,13 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
                 uint32_t lb = (uint32_t)((wave * UK + (lane >> 4) * 8) / 2) * 8u;
                 asm volatile("" : "+v"(lb));
                 for (;;) {
+                    if (a.exp & 32) {                    // (timing: no hand-off reads at all)
+#pragma unroll
+                        for (int j = 0; j < UPW; ++j)
+                            x[j][0] = x[j][1] = make_uint4(lane, tag, lane, tag);
+                        asm volatile("" : "+v"(x[0][0].x));
+                        break;
+                    }
 #pragma unroll
                     for (int j = 0; j < UPW; ++j) {
                         const int u = min(wave + NW * j, NU - 1);
@@ -415,6 +422,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
                         x[j][0] = hx_get2(rx, off);
                         x[j][1] = hx_get2(rx, off + 16);
                     }
+                    if (a.exp & 8) break;                // (timing: no tag check / wait)
                     bool ok = true;
 #pragma unroll
                     for (int j = 0; j < UPW; ++j)
@@ -431,6 +439,10 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
                                        : make_uint4(0u, 0u, 0u, 0u);
                     bf16x8 af;
                     __builtin_memcpy(&af, &v, 16);
+                    if (a.exp & 4) {                     // (timing: no MFMA)
+                        asm volatile("" :: "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w));
+                        continue;
+                    }
 #pragma unroll
                     for (int i = 0; i < NTB; ++i) Mma<bf16>::run(acc[i], af, wf[j][i]);
                 }
@@ -440,7 +452,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
 #pragma unroll
                     for (int e = 0; e < 4; ++e) rb[(i * 4 + e) * PS] = acc[i][e];
             }
-            __syncthreads();
+            if (!(a.exp & 16)) __syncthreads();          // (timing: no barrier)
         }
         float s = 0.f;
         if (has_next) {
@@ -501,6 +513,204 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
             if (t == 0) a.ddir0[(int64_t)row * D + unit] = o.ddir;
         }
         // (no barrier: red is double-buffered by the (step, tile) parity, see the forward)
+    }
+    }
+#pragma unroll
+    for (int m = 0; m < MT; ++m) {
+        const int row = row_of(m);
+        if (a.bsum && rv && row < B) {
+            float* bs = a.bsum + (int64_t)row * 4 * D;
+            if (MT == 1) {
+                bs[unit] = sar1; bs[D + unit] = saz1; bs[2 * D + unit] = sghn1;
+                bs[3 * D + unit] = san1;
+            } else {
+                const float* q = sl + (m * 5) * NTHR + tid;
+                bs[unit] = q[NTHR]; bs[D + unit] = q[2 * NTHR]; bs[2 * D + unit] = q[3 * NTHR];
+                bs[3 * D + unit] = q[4 * NTHR];
+            }
+        }
+    }
+    gx_note_failure(a.err, a.sticky);
+}
+
+// Packed hand-off form of the reverse sweep (the default at D % 64 == 0).  A thread's dgh_t
+// for its unit is ONE 8-byte granule {dar, daz, dghn (bf16), tag (16 bits)} instead of 1.5
+// {2 x bf16, 32-bit tag} granules per value pair: the consumers read 16 x D x 8 B per tile
+// (128 KiB at D = 1024) instead of 16 x 3D/2 x 8 B (192 KiB) -- the hand-off reads are what
+// the sweep's per-step time goes to (tools/gx_exp.py: without them 2.6 of 7.7 us at B = 128).
+// The product dgh_{t+1} . W_hh then runs over K' = 4D with k' = 4 unit + slot: slots 0-2 are
+// the gates (the granule's bytes ARE the MFMA A operand, unpacked nowhere) and slot 3, the
+// tag, meets zero weights (tags are small positive integers: finite bf16 bit patterns, so
+// tag x 0 = 0).  The W_hh^T fragments are gathered into that order once, in the prologue.
+template <int UPW, int MT>
+__global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs a) {
+    using namespace gx;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int D = a.D, B = a.B, RV = a.RV;
+    constexpr int KW = NW;                                      // NU' = D / 8 = UPW * NW
+    constexpr int NTB = 2;
+    float* red = (float*)smem;                                  // [2][KW][NTB][4][PS]
+    const size_t red_bytes = (size_t)2 * KW * NTB * 4 * PS * sizeof(float);
+    int* gsh = (int*)(smem + red_bytes);
+    const int g = blockIdx.x % a.G, p = blockIdx.x / a.G;
+    if (a.census && tid == 0) hx_group_arrive(a.census + g * a.P + p);
+    const int u0 = p * CU;
+    bf16x8 wf[UPW][NTB];
+    {
+        // lane's k' = [32 u + 8 (lane >> 4), +8): input units iu, iu + 1, slots 0..3 each
+        unsigned lw[UPW][NTB][3];
+#pragma unroll
+        for (int j = 0; j < UPW; ++j) {
+            const int u = wave + NW * j;
+            const int iu = u * 8 + (lane >> 4) * 2;
+#pragma unroll
+            for (int t = 0; t < NTB; ++t) {
+                const bf16* row = a.whh_t + (int64_t)(u0 + t * 16 + (lane & 15)) * 3 * D;
+#pragma unroll
+                for (int gt = 0; gt < 3; ++gt)
+                    lw[j][t][gt] = *reinterpret_cast<const unsigned*>(row + gt * D + iu);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < UPW; ++j)
+#pragma unroll
+            for (int t = 0; t < NTB; ++t) {
+                // [r0 z0 n0 0 | r1 z1 n1 0] (low / high halves of each gate word)
+                const unsigned r2 = lw[j][t][0], z2 = lw[j][t][1], n2 = lw[j][t][2];
+                const uint4 v = make_uint4((r2 & 0xffffu) | (z2 << 16), n2 & 0xffffu,
+                                           (r2 >> 16) | (z2 & 0xffff0000u), n2 >> 16);
+                __builtin_memcpy(&wf[j][t], &v, 16);
+            }
+    }
+    if (wave == 0) {
+        const int loc = a.census && hx_group_local(a.census + g * a.P, a.P, a.err) ? 1 : 0;
+        if (tid == 0) gsh[2] = loc;
+    }
+    __syncthreads();
+    const bool local = gsh[2] != 0;
+    const int r = tid >> 5, uu = tid & 31;
+    const bool rv = r < RV;
+    const int unit = u0 + uu;
+    int rop = r;
+    auto row_of = [&](int m) { return (g * MT + m) * RV + rop; };
+    const __amdgpu_buffer_rsrc_t rx = hx_rsrc(a.xg);
+    const size_t bufw = (size_t)a.G * MT * RG * D;              // granules per buffer
+    const int lrow = lane & 15;
+    auto fetch = [&](int t, int m, float& dyv, float& gr, float& gz, float& gn, float& gg,
+                     float& hp) {
+        const int b = min(row_of(m), B - 1);
+        dyv = a.dy[(int64_t)b * a.lddy + (int64_t)t * a.sdy + unit];
+        const float* gp = a.gates + (int64_t)b * a.ldg + (int64_t)t * a.sg;
+        gr = gp[unit]; gz = gp[D + unit]; gn = gp[2 * D + unit]; gg = gp[3 * D + unit];
+        hp = t > 0 ? a.hout[(int64_t)b * a.ldo + (int64_t)(t - 1) * a.so + unit]
+                   : a.h0[(int64_t)b * D + unit];
+    };
+    float dyv, gr, gz, gn, gg, hp;
+    float ddir1 = 0.f, sar1 = 0.f, saz1 = 0.f, sghn1 = 0.f, san1 = 0.f;
+    float* sl = (float*)(smem + red_bytes + 64);                 // [MT][5][NTHR]
+    if (MT > 1)
+        for (int k = 0; k < 5 * MT; ++k) sl[k * NTHR + tid] = 0.f;
+    fetch(a.Fr - 1, 0, dyv, gr, gz, gn, gg, hp);
+    for (int t = a.Fr - 1; t >= 0; --t) {
+    asm volatile("" : "+v"(rop));
+#pragma unroll 1
+    for (int m = 0; m < MT; ++m) {
+        const bool has_next = t + 1 < a.Fr;
+        float* q = sl + (m * 5) * NTHR + tid;
+        const float ddir_in = MT == 1 ? ddir1 : q[0];
+        floatx4 acc[NTB];
+#pragma unroll
+        for (int i = 0; i < NTB; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if (has_next) {
+            const uint32_t tag = (uint32_t)(a.Fr - 1 - t);          // dgh_{t+1}
+            const uint32_t base = (uint32_t)((((size_t)((t + 1) & 1)) * bufw +
+                                              (size_t)((g * MT + m) * RG + lrow) * D) * 8);
+            uint4 x[UPW];
+            int spins = 0;
+            // granule offset of the lane's first k': (32 wave + 8 (lane >> 4)) / 4; made
+            // opaque per step (see the unpacked kernel)
+            uint32_t lb = (uint32_t)(wave * 8 + (lane >> 4) * 2) * 8u;
+            asm volatile("" : "+v"(lb));
+            for (;;) {
+#pragma unroll
+                for (int j = 0; j < UPW; ++j)
+                    x[j] = hx_get2(rx, base + lb + (uint32_t)(j * NW * 8 * 8));
+                bool ok = true;
+#pragma unroll
+                for (int j = 0; j < UPW; ++j)
+                    ok &= ((x[j].y >> 16) == tag) & ((x[j].w >> 16) == tag);
+                if (__all(ok)) break;
+                if (hx_spin_fail(spins, a.err, lane, 1, a.spin_limit)) break;
+            }
+#pragma unroll
+            for (int j = 0; j < UPW; ++j) {
+                bf16x8 af;
+                __builtin_memcpy(&af, &x[j], 16);
+#pragma unroll
+                for (int i = 0; i < NTB; ++i) Mma<bf16>::run(acc[i], af, wf[j][i]);
+            }
+            float* rb = red + (size_t)((((a.Fr - 1 - t) * MT + m) & 1) * KW + wave) * NTB * 4 * PS + lane;
+#pragma unroll
+            for (int i = 0; i < NTB; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) rb[(i * 4 + e) * PS] = acc[i][e];
+            __syncthreads();
+        }
+        float s = 0.f;
+        if (has_next) {
+            const int ln = (r >> 2) * 16 + (uu & 15), ii = r & 3, tile = uu >> 4;
+            const float* rb = red + (size_t)(((a.Fr - 1 - t) * MT + m) & 1) * KW * NTB * 4 * PS +
+                              ii * PS + ln;
+            float pr[NW];
+#pragma unroll
+            for (int kw = 0; kw < NW; ++kw) pr[kw] = rb[(kw * NTB + tile) * 4 * PS];
+#pragma unroll
+            for (int kw = 0; kw < NW; ++kw) s += pr[kw];
+        }
+        float dh = s + dyv;
+        if (has_next) dh += ddir_in;
+        const GruBwdPoint o = gru_bwd_point(dh, gr, gz, gn, gg, hp);
+        if (MT == 1) ddir1 = o.ddir;
+        else q[0] = o.ddir;
+        // publish dgh_t of this unit: one granule {dar, daz, dghn, tag = Fr - t}
+        if (!(a.withhold && blockIdx.x == 0)) {
+            u64* dst = a.xg + (size_t)(t & 1) * bufw + (size_t)((g * MT + m) * RG + r) * D + unit;
+            const u64 v = (u64)__bfloat16_as_ushort(__float2bfloat16(o.dar)) |
+                          ((u64)__bfloat16_as_ushort(__float2bfloat16(o.daz)) << 16) |
+                          ((u64)__bfloat16_as_ushort(__float2bfloat16(o.dghn)) << 32) |
+                          ((u64)(uint32_t)(a.Fr - t) << 48);
+            if (local) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        const float cdar = o.dar, cdaz = o.daz, cdghn = o.dghn, cdan = o.dan;
+        if (m + 1 < MT) fetch(t, m + 1, dyv, gr, gz, gn, gg, hp);
+        else if (t > 0) fetch(t - 1, 0, dyv, gr, gz, gn, gg, hp);
+        const int row = row_of(m);
+        if (rv && row < B) {
+            const int64_t ob = (int64_t)row * a.ldd + (int64_t)t * a.sd;
+            if (a.dgh) {
+                float* dg = a.dgh + ob;
+                dg[unit] = cdar; dg[D + unit] = cdaz; dg[2 * D + unit] = cdghn;
+            }
+            bf16* dl = a.dgh_lp + ob;
+            const bf16 har = __float2bfloat16(cdar), haz = __float2bfloat16(cdaz);
+            dl[unit] = har; dl[D + unit] = haz; dl[2 * D + unit] = __float2bfloat16(cdghn);
+            if (a.dgi) {
+                float* di = a.dgi + ob;
+                di[unit] = cdar; di[D + unit] = cdaz; di[2 * D + unit] = cdan;
+            }
+            if (a.dgi_lp) {
+                bf16* dj = a.dgi_lp + ob;
+                dj[unit] = har; dj[D + unit] = haz; dj[2 * D + unit] = __float2bfloat16(cdan);
+            }
+            if (MT == 1) {
+                sar1 += cdar; saz1 += cdaz; sghn1 += cdghn; san1 += cdan;
+            } else {
+                q[NTHR] += cdar; q[2 * NTHR] += cdaz; q[3 * NTHR] += cdghn; q[4 * NTHR] += cdan;
+            }
+            if (t == 0) a.ddir0[(int64_t)row * D + unit] = o.ddir;
+        }
     }
     }
 #pragma unroll
@@ -721,7 +931,13 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
     GxLayout L;
     SRNN_REQUIRE(gx_layout(B, D, L), "gru_xcd_bwd: no row layout for B=%d D=%d", B, D);
     hipStream_t s = (hipStream_t)stream;
-    SRNN_CHECK_HIP(hipMemsetAsync(work, 0, need, s));
+    // packed hand-off form (gru_xcd_bwd_pk_kernel): one {3 x bf16, tag} granule per unit;
+    // tags (<= Fr) must stay finite bf16 patterns (< 0x7f80); SRNN_GX_PK=0 restores the form
+    // with {2 x bf16, 32-bit tag} granules
+    const bool pk = D % 64 == 0 && D / 64 <= 16 && (D / 64) % 4 == 0 && Fr < 0x7f80 &&
+                    env_flag("SRNN_GX_PK", 1);
+    const size_t clear = pk ? gx::HDR + (size_t)2 * L.G * L.mt * gx::RG * D * 8 : need;
+    SRNN_CHECK_HIP(hipMemsetAsync(work, 0, clear, s));
     GruXBwdArgs a;
     a.dy = dy; a.lddy = lddy; a.sdy = sdy;
     a.gates = gates; a.ldg = ldg; a.sg = sg;
@@ -743,9 +959,24 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
     a.P = L.P;
     a.RV = L.rv;
     const int NU = 3 * D / gx::UK;
-    const int KW = NU < gx::NW ? NU : gx::NW;
+    const int KW = pk ? gx::NW : NU < gx::NW ? NU : gx::NW;
     const size_t lds = (size_t)2 * KW * 2 * 4 * gx::PS * 4 + 64 +
                        (L.mt > 1 ? (size_t)L.mt * 5 * gx::NTHR * 4 : 0);
+    if (pk) {
+        typedef void (*PkK)(GruXBwdArgs);
+        static const PkK kp[4][3] = {
+            {gru_xcd_bwd_pk_kernel<4, 1>, gru_xcd_bwd_pk_kernel<4, 2>, gru_xcd_bwd_pk_kernel<4, 4>},
+            {gru_xcd_bwd_pk_kernel<8, 1>, gru_xcd_bwd_pk_kernel<8, 2>, gru_xcd_bwd_pk_kernel<8, 4>},
+            {gru_xcd_bwd_pk_kernel<12, 1>, gru_xcd_bwd_pk_kernel<12, 2>,
+             gru_xcd_bwd_pk_kernel<12, 4>},
+            {gru_xcd_bwd_pk_kernel<16, 1>, gru_xcd_bwd_pk_kernel<16, 2>,
+             gru_xcd_bwd_pk_kernel<16, 4>}};
+        const int mi = L.mt == 1 ? 0 : L.mt == 2 ? 1 : 2;
+        const PkK k = kp[D / 256 - 1][mi];
+        hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
+        SRNN_LAUNCH_CHECK();
+        return 0;
+    }
     const int upw = cdiv(NU, gx::NW);
     const int ui = upw <= 3 ? 0 : upw <= 6 ? 1 : 2;
     const bool full = NU == (ui == 0 ? 3 : ui == 1 ? 6 : 12) * gx::NW;
