@@ -624,18 +624,20 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
         for (int i = 0; i < NTB; ++i) acc[i] = floatx4{0.f, 0.f, 0.f, 0.f};
         if (has_next) {
             const uint32_t tag = (uint32_t)(a.Fr - 1 - t);          // dgh_{t+1}
+            // fragment-major tile image: k'-unit u's 1 KiB holds lane l's 16 B at l * 16 (row
+            // l & 15, k' 32 u + 8 (l >> 4) ..): every poll instruction reads 1 KiB of whole
+            // lines (the row-major image took 16 half lines per instruction)
             const uint32_t base = (uint32_t)((((size_t)((t + 1) & 1)) * bufw +
-                                              (size_t)((g * MT + m) * RG + lrow) * D) * 8);
+                                              (size_t)(g * MT + m) * RG * D) * 8);
             uint4 x[UPW];
             int spins = 0;
-            // granule offset of the lane's first k': (32 wave + 8 (lane >> 4)) / 4; made
-            // opaque per step (see the unpacked kernel)
-            uint32_t lb = (uint32_t)(wave * 8 + (lane >> 4) * 2) * 8u;
+            // (made opaque per step, see the unpacked kernel)
+            uint32_t lb = (uint32_t)(wave * 64 + lane) * 16u;
             asm volatile("" : "+v"(lb));
             for (;;) {
 #pragma unroll
                 for (int j = 0; j < UPW; ++j)
-                    x[j] = hx_get2(rx, base + lb + (uint32_t)(j * NW * 8 * 8));
+                    x[j] = hx_get2(rx, base + lb + (uint32_t)(j * NW * 64 * 16));
                 bool ok = true;
 #pragma unroll
                 for (int j = 0; j < UPW; ++j)
@@ -675,7 +677,9 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
         else q[0] = o.ddir;
         // publish dgh_t of this unit: one granule {dar, daz, dghn, tag = Fr - t}
         if (!(a.withhold && blockIdx.x == 0)) {
-            u64* dst = a.xg + (size_t)(t & 1) * bufw + (size_t)((g * MT + m) * RG + r) * D + unit;
+            // granule of (row r, unit U): k'-unit U / 8, lane ((U % 8) / 2) * 16 + r, half U % 2
+            u64* dst = a.xg + (size_t)(t & 1) * bufw + (size_t)(g * MT + m) * RG * D +
+                       ((size_t)((unit >> 3) * 64 + ((unit & 7) >> 1) * 16 + r) << 1) + (unit & 1);
             const u64 v = (u64)__bfloat16_as_ushort(__float2bfloat16(o.dar)) |
                           ((u64)__bfloat16_as_ushort(__float2bfloat16(o.daz)) << 16) |
                           ((u64)__bfloat16_as_ushort(__float2bfloat16(o.dghn)) << 32) |
