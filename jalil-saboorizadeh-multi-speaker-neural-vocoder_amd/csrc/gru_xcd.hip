@@ -145,8 +145,12 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     auto publish = [&](int s, int m, float h) {   // h_s of tile m -> buffer (s + 1) & 1, tag s + 2
         const uint32_t mine = (uint32_t)__bfloat16_as_ushort(__float2bfloat16(h));
         const uint32_t nb = lane_next16(mine);
+        // fragment-order tile image (see the poll): the granule of units (U, U + 1) is 16-B
+        // half (U % 8) / 4 of lane ((U % 32) / 8) * 16 + r in k-unit U / 32's 2 KiB
         if ((uu & 1) == 0 && !(a.withhold && blockIdx.x == 0))
-            hx_put(a.xh + ((s + 1) & 1) * bufw + (size_t)((g * MT + m) * RG + r) * DG + unit / 2,
+            hx_put(a.xh + ((s + 1) & 1) * bufw + (size_t)(g * MT + m) * RG * DG +
+                       ((size_t)(((unit >> 5) * 2 + ((unit & 7) >> 2)) * 64 +
+                                 ((unit & 31) >> 3) * 16 + r) << 1) + ((unit & 3) >> 1),
                    (uint32_t)(s + 2), mine | (nb << 16), local);
     };
 #pragma unroll
@@ -181,8 +185,12 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
             if (!polls) fetch_gi(t, m, nx);
             if (polls) {
                 const uint32_t tag = (uint32_t)(t + 1);
+                // the tile's image in fragment order: k-unit u's 2 KiB hold lane l's first 16 B
+                // (row l & 15, k = 32 u + 8 (l >> 4) + 0..3) at l * 16 and its second at
+                // 1 KiB + l * 16, so each poll instruction reads 1 KiB of whole lines (the
+                // row-major image took 16 half lines per instruction)
                 const uint32_t base = (uint32_t)(((size_t)(t & 1) * bufw +
-                                                  (size_t)((g * MT + m) * RG + lrow) * DG) * 8);
+                                                  (size_t)(g * MT + m) * RG * DG) * 8) + lane * 16u;
                 uint32_t w[UPW][4];
                 int spins = 0;
                 for (;;) {
@@ -192,9 +200,9 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     #pragma unroll
                     for (int j = 0; j < UPW; ++j) {
                         const int u = min(wave + NW * j, NU - 1);
-                        const uint32_t off = base + (uint32_t)((u * UK + (lane >> 4) * 8) / 2) * 8u;
+                        const uint32_t off = base + (uint32_t)u * 2048u;
                         x[j][0] = hx_get2(rx, off);
-                        x[j][1] = hx_get2(rx, off + 16);
+                        x[j][1] = hx_get2(rx, off + 1024);
                     }
                     bool ok = true;
     #pragma unroll
