@@ -86,28 +86,43 @@ __device__ __forceinline__ uint32_t gm_bf16_bits(float v) {
     return (uint32_t)__bfloat16_as_ushort(__float2bfloat16(v));
 }
 
-// A-operand fragments of one wave for one hand-off buffer (granules of row `row`, starting
-// at granule `rowg`): for unit j (global unit u = wave + NW*j) the lane's 16 data bytes are
-// 4 granules = two 16-B loads.  Spins until every tag == tag.  `work` (independent of the
-// hand-off) runs once between the first poll's issue and its check, so it fills the
-// hand-off's latency (the first check is straight-line code after it: its vmcnt leaves
-// work's own loads in flight).
-template <typename T, int UPW, typename W>
-__device__ __forceinline__ void gm_fetch_a(__amdgpu_buffer_rsrc_t src, uint32_t rowg, bool rv,
-                                           int wave, int lane, int NU, int D, uint32_t tag,
-                                           uint32_t (&w)[UPW][4], int* err, W&& work) {
+// Hand-off images in fragment order.  A group's a1 / a2 buffer holds, for every MFMA k-unit
+// u, the 4 granules each lane of a wave reads (row r < 8 = lane & 15, columns
+// u UK + (lane >> 4) EPL ..) as two 16-B halves: granule index
+//     (((u * 2 + half) * 4 + chunk) * 8 + r) * 2 + sub,
+// so one poll instruction reads 512 B of whole lines (lanes of rows >= R read row R - 1's
+// slots: the same addresses) instead of one half line per row.  Images are NU * 128 granules
+// per group (= R * D / GV at R = 8, D % UK == 0).
+template <typename T>
+__device__ __forceinline__ uint32_t gm_slot(int r, int k) {
     constexpr int GV = GmT<T>::GV, UK = GmT<T>::UK, EPL = UK / 4;
+    const int u = k / UK, kk = k - u * UK, c = kk / EPL, gi = (kk - c * EPL) / GV;
+    return (uint32_t)((((u * 2 + (gi >> 1)) * 4 + c) * 8 + r) * 2 + (gi & 1));
+}
+
+// A-operand fragments of one wave for one hand-off buffer (the image of its group, starting
+// at granule `gbase`; `rr` = the lane's row, clamped below R): for unit j (global unit
+// u = wave + NW*j) the lane's 16 data bytes are 4 granules = two 16-B loads.  Spins until
+// every tag == tag.  `work` (independent of the hand-off) runs once between the first poll's
+// issue and its check, so it fills the hand-off's latency (the first check is straight-line
+// code after it: its vmcnt leaves work's own loads in flight).
+template <typename T, int UPW, typename W>
+__device__ __forceinline__ void gm_fetch_a(__amdgpu_buffer_rsrc_t src, uint32_t gbase, int rr,
+                                           bool rv, int wave, int lane, int NU, int D,
+                                           uint32_t tag, uint32_t (&w)[UPW][4], int* err,
+                                           W&& work) {
+    constexpr int UK = GmT<T>::UK, EPL = UK / 4;
     uint4 x[UPW][2];
-    // every load unconditional (clamped k), so all 2 x UPW are in flight at once; a branch
+    // every load unconditional (clamped unit), so all 2 x UPW are in flight at once; a branch
     // per unit would put a vmcnt(0) between them
+    const uint32_t lo = (gbase + (uint32_t)(((lane >> 4) * 8 + rr) * 2)) * 8u;
     auto issue = [&]() {
 #pragma unroll
         for (int j = 0; j < UPW; ++j) {
-            const int u = wave + gm::NW * j;
-            const int ke = min(u * UK + (lane >> 4) * EPL, D - EPL);
-            const uint32_t off = (rowg + (uint32_t)(ke / GV)) * 8u;
+            const int u = min(wave + gm::NW * j, NU - 1);
+            const uint32_t off = lo + (uint32_t)u * (2u * 4 * 8 * 2 * 8);
             x[j][0] = hx_get2(src, off);
-            x[j][1] = hx_get2(src, off + 16);
+            x[j][1] = hx_get2(src, off + 4 * 8 * 2 * 8);
         }
     };
     auto check = [&]() -> bool {
@@ -183,6 +198,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     const int KW = min(gm::NW, NU);
     const int nt = CW / 16, nzt = NZ / 16, ntm = max(nt, nzt);
     const int DG = D / GV;
+    const int XW = max(R * DG, ((D + UK - 1) / UK) * 128);   // granules per group image
     const T* __restrict__ tab = (const T*)a.tab;
     // optional phase timestamps (workgroup 0, thread 0; s_memrealtime = 100 MHz)
     unsigned long long* dg = (a.diag && blockIdx.x == 0 && tid == 0) ? a.diag : nullptr;
@@ -374,15 +390,15 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     // publish a1(i) = relu(part + Tab[FS0-1][x_{i-1}]) as granules tagged i (x = x_{i-1} of
     // this thread's row)
     auto publish_a1 = [&](int i, int x) {
-        u64* dst = a.xa1 + (size_t)g * R * DG;
+        u64* dst = a.xa1 + (size_t)g * XW;
         float v = 0.f;
         if (own) v = fmaxf(part + to_f(tab15[x * CW + ec]), 0.f);
         if (GV == 2) {
             const uint32_t mine = gm_bf16_bits(v);
             const uint32_t nb = lane_next16(mine);
-            if (own && (ec & 1) == 0) hx_put(dst + (size_t)er * DG + (c0 + ec) / 2, i, mine | (nb << 16), local);
+            if (own && (ec & 1) == 0) hx_put(dst + gm_slot<T>(er, c0 + ec), i, mine | (nb << 16), local);
         } else if (own) {
-            hx_put(dst + (size_t)er * DG + c0 + ec, i, gm_bits(v), local);
+            hx_put(dst + gm_slot<T>(er, c0 + ec), i, gm_bits(v), local);
         }
     };
 
@@ -394,7 +410,8 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
 
     const int row = lane & 15;
     const bool rv = row < R;
-    const uint32_t rowg = (uint32_t)((g * R + min(row, R - 1)) * DG);   // in-bounds for row >= R
+    const int rr = min(row, R - 1);                 // (rows >= R read row R - 1's slots)
+    const uint32_t gb1 = (uint32_t)((size_t)g * XW);
     for (int s = 0; s < a.nsteps; ++s) {
         const int i = i0 + s;
         const uint32_t tag = (uint32_t)i;
@@ -416,9 +433,9 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 for (int h = 0; h < UPW / HU; ++h) {
                     uint32_t w[HU][4];
                     if (h == 0)
-                        gm_fetch_a<T, HU>(rx1, rowg, rv, wave, lane, NU, D, tag, w, a.err, work);
+                        gm_fetch_a<T, HU>(rx1, gb1, rr, rv, wave, lane, NU, D, tag, w, a.err, work);
                     else
-                        gm_fetch_a<T, HU>(rx1, rowg, rv, wave + gm::NW * HU * h, lane, NU, D, tag,
+                        gm_fetch_a<T, HU>(rx1, gb1, rr, rv, wave + gm::NW * HU * h, lane, NU, D, tag,
                                           w, a.err, [] {});
                     if (h == 0) GM_W(1);
 #pragma unroll
@@ -437,7 +454,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             GM_W(3);
             __syncthreads();
             GM_W(4);
-            u64* dst = a.xa2 + (size_t)g * R * DG;
+            u64* dst = a.xa2 + (size_t)g * XW;
             float v = 0.f;
             if (own) {
                 const int t = ec >> 4, ln = (er >> 2) * 16 + (ec & 15), ii = er & 3;
@@ -453,9 +470,9 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 const uint32_t mine = gm_bf16_bits(v);
                 const uint32_t nb = lane_next16(mine);
                 if (own && (ec & 1) == 0)
-                    hx_put(dst + (size_t)er * DG + (c0 + ec) / 2, tag, mine | (nb << 16), local);
+                    hx_put(dst + gm_slot<T>(er, c0 + ec), tag, mine | (nb << 16), local);
             } else if (own) {
-                hx_put(dst + (size_t)er * DG + c0 + ec, tag, gm_bits(v), local);
+                hx_put(dst + gm_slot<T>(er, c0 + ec), tag, gm_bits(v), local);
             }
             GM_W(5);
             __syncthreads();                   // red is reused by the next phase
@@ -474,9 +491,9 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 for (int h = 0; h < UPW / HU; ++h) {
                     uint32_t w[HU][4];
                     if (h == 0)
-                        gm_fetch_a<T, HU>(rx2, rowg, rv, wave, lane, NU, D, tag, w, a.err, work);
+                        gm_fetch_a<T, HU>(rx2, gb1, rr, rv, wave, lane, NU, D, tag, w, a.err, work);
                     else
-                        gm_fetch_a<T, HU>(rx2, rowg, rv, wave + gm::NW * HU * h, lane, NU, D, tag,
+                        gm_fetch_a<T, HU>(rx2, gb1, rr, rv, wave + gm::NW * HU * h, lane, NU, D, tag,
                                           w, a.err, [] {});
                     if (h == 0) GM_W(7);
 #pragma unroll
@@ -721,7 +738,8 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     pl->lds = lds;
     pl->kernel = (const void*)k;
     const int GV = dtype == SRNN_BF16 ? 2 : 1;
-    pl->xa_words = (size_t)pl->G * R * (D / GV);
+    // fragment-order images: max(R D / GV, NU * 128) granules per group (gm_slot)
+    pl->xa_words = (size_t)pl->G * std::max(R * (D / GV), NU * 128);
     pl->xz_words = (size_t)pl->G * R * Q;
     return 1;
 }
