@@ -531,7 +531,11 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                     pr[kw] = red[(min(kw, KW - 1) * ntm + t) * 32 + ln][ii];
                 #pragma unroll
                 for (int kw = 0; kw < gm::NW; ++kw) v += kw < KW ? pr[kw] : 0.f;
-                hx_put(a.xz + ((size_t)g * R + r) * Q + z0 + c, tag,
+                // (a row's logits in the order the draw reads them: lane l's z[4l .. 4l+1] at
+                //  granule 2l, z[4l+2 .. 4l+3] at 128 + 2l: each poll reads 1 KiB of lines)
+                const int zc = z0 + c;
+                hx_put(a.xz + ((size_t)g * R + r) * Q + ((((zc & 3) >> 1) * 64 + (zc >> 2)) * 2 +
+                                                         (zc & 1)), tag,
                        gm_bits(v + (e < gm::NTHR ? bo : a.b_out[z0 + c])), local);
             }
             GM_W(10);
@@ -543,7 +547,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         for (int r = wave; r < R; r += gm::NW) {
             const int b = g * R + r;
             const bool valid = b < B;
-            const uint32_t zoff = (uint32_t)((((size_t)g * R + r) * Q + 4 * lane) * 8);
+            const uint32_t zoff = (uint32_t)((((size_t)g * R + r) * Q + 2 * lane) * 8);
             floatx4 v;
             uint4 x0, x1;
             auto zcheck = [&]() -> bool {
@@ -552,7 +556,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 return __all((x0.y == tag) & (x0.w == tag) & (x1.y == tag) & (x1.w == tag));
             };
             x0 = hx_get2(rxz, zoff);
-            x1 = hx_get2(rxz, zoff + 16);
+            x1 = hx_get2(rxz, zoff + 1024);
             // the row's noise: precomputed by gen_noise_kernel (loaded under the z hand-off)
             // or drawn here, under the first poll
             floatx4 lq = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -564,7 +568,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 for (;;) {
                     if (hx_spin_fail(spins, a.err, lane)) break;
                     x0 = hx_get2(rxz, zoff);
-                    x1 = hx_get2(rxz, zoff + 16);
+                    x1 = hx_get2(rxz, zoff + 1024);
                     if (zcheck()) break;
                 }
             }
