@@ -130,8 +130,9 @@ SITE_NOTES = {
                    '(16 rows x D {3 x bf16, tag} granules per workgroup and step) from L2)',
     'gru_xcd_fwd': 'gru_xcd_fwd_kernel: the GRU forward sweeps (W_hh h products; one hand-off '
                    'of h per step)',
-    'dtab_scatter': 'dtab_pos_kernel: backward of the folded embedding.conv (dTab scatter; '
-                    'bound by LDS u64-atomic issue, priced against HBM)',
+    'dtab_scatter': 'dtab_prep_kernel + dtab_pk_kernel: backward of the folded embedding.conv '
+                    '(dTab scatter, two columns per 64-bit LDS atomic; bound by LDS atomic '
+                    'issue, priced against HBM)',
     'mlp_hidden_gemm': 'gemm3p_kernel: sample-level MLP hidden layer (B*T x D x D, bias + '
                        'ReLU epilogue)',
     'adam_clip': 'adam_clip_multi_kernel: fused clamp + Adam over every parameter',
@@ -347,7 +348,7 @@ def run_gen(dev, n_seqs, n_cond, dtype, frame_sizes=(16, 4), cond_dim=43, row0=0
     return time.perf_counter() - t0, w_step
 
 
-def gen_traffic(path=os.path.join(ROOT, 'profiles', 'r02_pmc_gen.txt')):
+def gen_traffic(path=os.path.join(ROOT, 'profiles', 'r03_pmc_gen.txt')):
     """HBM bytes per generation step of the bf16 loop (B = 128, D = 1024, FS = [16, 4]) from the
     committed rocprofv3 PMC passes (tools/pmc_gen.py: FETCH_SIZE kB x 2 + WRITE_SIZE kB over
     every dispatch of the loop's kernels / samples generated)."""

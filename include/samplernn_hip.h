@@ -185,7 +185,23 @@ int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x, int
 int srnn_mlp_dtab2(int dtype, const void* da, int64_t ldda, const int64_t* x, int64_t ldx,
                    int xoff, int B, int Tlen, void* dtab_out, int out_dtype, int D, int FS0, int Q,
                    void* work, size_t work_bytes, float* colsum, int* colsum_done, void* stream);
-/* (deterministic: 2^-40 fixed-point int64 accumulation; work >= Q*FS0*D*8 bytes)        */
+/* (deterministic: 2^-40 fixed-point int64 accumulation; work >= Q*FS0*D*8 bytes)        *
+ * bf16 da and bf16 output at FS0 = 16, Q = 256, D % 8 == 0 take the packed form: two      *
+ * columns per 64-bit LDS atomic in 32-bit fixed point at a power-of-2 scale from max |da| *
+ * and the most frequent sample value (exact integer sums, deterministic).                 */
+/* srnn_mlp_dtab2 with amax_in (device, may be NULL): max |da| as float bits, measured by  *
+ * the GEMM that produced da (srnn_gemm_amax_next), so the packed form skips its own pass  *
+ * over da.  Replaces nothing new in the reference: the same model.py:311-320 backward.    */
+int srnn_mlp_dtab3(int dtype, const void* da, int64_t ldda, const int64_t* x, int64_t ldx,
+                   int xoff, int B, int Tlen, void* dtab_out, int out_dtype, int D, int FS0, int Q,
+                   void* work, size_t work_bytes, float* colsum, int* colsum_done,
+                   const unsigned* amax_in, void* stream);
+/* Ask the next bf16-output GEMM that runs on the 256 x 256 gemm3 path (model.py:311-320's
+ * da1 = (da2 W_hid) * relu', the GEMM producing the dTab scatter's input) to also write
+ * max |C| (float bits, atomicMax into *amax, which must be zero).  srnn_gemm_amax_taken()
+ * returns 1 if a GEMM did since (host state; also clears a request no GEMM took).        */
+int srnn_gemm_amax_next(unsigned* amax);
+int srnn_gemm_amax_taken(void);
 /* log_softmax (model.py:324-325) + NLL rows (nn.py:66-70) + dlogits (softmax-onehot)*g  */
 /* dz = dlogp - exp(logp) * rowsum(dlogp)   (log_softmax backward, rows of Q)          */
 int srnn_logsoftmax_bwd(const float* dlogp, int64_t lddl, const float* logp, int64_t ldl,

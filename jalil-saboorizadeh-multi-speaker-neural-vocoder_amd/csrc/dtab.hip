@@ -363,8 +363,8 @@ __global__ __launch_bounds__(256) void dtab_prep_kernel(const T* __restrict__ da
 template <typename T>
 __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
     const T* __restrict__ da, int64_t ldda, const int64_t* __restrict__ x, int64_t ldx, int xoff,
-    int Tlen, int B, const DtabStat* __restrict__ st, bf16* __restrict__ out,
-    float* __restrict__ colsum, int D, int Q) {
+    int Tlen, int B, const DtabStat* __restrict__ st, const unsigned* __restrict__ amax_in,
+    bf16* __restrict__ out, float* __restrict__ colsum, int D, int Q) {
     constexpr int CW = 4, FS = 16;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [Q][2][FS]
@@ -395,7 +395,7 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
     }
     __syncthreads();
     const int cmax = max(max(red[0], red[1]), max(red[2], red[3]));
-    const float amax = __uint_as_float(st->amax_bits);
+    const float amax = __uint_as_float(amax_in ? *amax_in : st->amax_bits);
     int e = 0;
     if (amax > 0.f && cmax > 0) {
         int ex;
@@ -606,10 +606,11 @@ static int dtab_pos(const void* da, int64_t ldda, const int64_t* x, int64_t ldx,
 // dtab_out (Q, FS0, D) in out_dtype; work: >= Q*FS0*D*8 bytes of device scratch.
 // colsum (optional, (FS0 * D) fp32): sum over batch rows of da rows t = j (mod FS0) at
 // [j * D + c]; *colsum_done (host) = 1 when it was written (the direct position-major path)
-extern "C" int srnn_mlp_dtab2(int dtype, const void* da, int64_t ldda, const int64_t* x,
+extern "C" int srnn_mlp_dtab3(int dtype, const void* da, int64_t ldda, const int64_t* x,
                               int64_t ldx, int xoff, int B, int Tlen, void* dtab_out,
                               int out_dtype, int D, int FS0, int Q, void* work, size_t work_bytes,
-                              float* colsum, int* colsum_done, void* stream) {
+                              float* colsum, int* colsum_done, const unsigned* amax_in,
+                              void* stream) {
     SRNN_REQUIRE(Q <= 256, "dtab: q_levels must be <= 256 (byte indices)");
     const int64_t n = (int64_t)Q * FS0 * D;
     SRNN_REQUIRE(work && work_bytes >= (size_t)n * 8, "dtab: workspace too small");
@@ -623,7 +624,9 @@ extern "C" int srnn_mlp_dtab2(int dtype, const void* da, int64_t ldda, const int
         DtabStat* st = (DtabStat*)work;
         SRNN_CHECK_HIP(hipMemsetAsync(st, 0, sizeof(DtabStat), s));
         const int64_t nrows = (int64_t)B * Tlen;
-        const int nb_da = (int)std::min<int64_t>(1024, std::max<int64_t>(1, nrows / 64));
+        // amax_in: max |da| already measured by the GEMM that wrote da (srnn_gemm_amax_next):
+        // the prep pass only counts the sample values
+        const int nb_da = amax_in ? 0 : (int)std::min<int64_t>(1024, std::max<int64_t>(1, nrows / 64));
         const int W = Tlen + 15;
         hipLaunchKernelGGL(dtab_prep_kernel<bf16>, dim3(nb_da + B), dim3(256), 0, s,
                            (const bf16*)da, ldda, nrows, D, x, ldx, xoff, W, B, nb_da, st);
@@ -637,7 +640,7 @@ extern "C" int srnn_mlp_dtab2(int dtype, const void* da, int64_t ldda, const int
         }
         hipLaunchKernelGGL(dtab_pk_kernel<bf16>, dim3(cdiv(D, 4)), dim3(DTAB_NT),
                            pk_lds_bytes(Q, Tlen), s, (const bf16*)da, ldda, x, ldx, xoff, Tlen, B,
-                           st, (bf16*)dtab_out, colsum, D, Q);
+                           st, amax_in, (bf16*)dtab_out, colsum, D, Q);
         SRNN_LAUNCH_CHECK();
         if (colsum && colsum_done) *colsum_done = 1;
         return 0;
@@ -683,6 +686,14 @@ convert:
                            (bf16*)dtab_out, n);
     SRNN_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int srnn_mlp_dtab2(int dtype, const void* da, int64_t ldda, const int64_t* x,
+                              int64_t ldx, int xoff, int B, int Tlen, void* dtab_out,
+                              int out_dtype, int D, int FS0, int Q, void* work, size_t work_bytes,
+                              float* colsum, int* colsum_done, void* stream) {
+    return srnn_mlp_dtab3(dtype, da, ldda, x, ldx, xoff, B, Tlen, dtab_out, out_dtype, D, FS0, Q,
+                          work, work_bytes, colsum, colsum_done, nullptr, stream);
 }
 
 extern "C" int srnn_mlp_dtab(int dtype, const void* da, int64_t ldda, const int64_t* x,

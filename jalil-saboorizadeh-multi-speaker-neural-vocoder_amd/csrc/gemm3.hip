@@ -47,6 +47,9 @@ struct Gemm3Args {
     int64_t ldmbi;
     unsigned short* mbo;
     int64_t ldmbo;
+    // optional: max |C| over the stored bf16 values, as float bits, atomicMax-ed here (the
+    // packed dTab scatter's scale, dtab.hip); the word must be zero before the GEMM
+    unsigned* amax;
 };
 
 namespace g3 {
@@ -153,7 +156,9 @@ __device__ __forceinline__ void g3_store4(bf16* p, const float (&v)[4]) {
 // path, where a lane's 4 values are 4 rows of one column and each atomic instruction
 // covers 16 consecutive columns (64 B) of 4 rows instead of 16 rows x 4 B.
 // epilogue of one finished tile (registers -> C); zeroes the accumulators
-template <typename TO, bool SW, bool CIN, bool MB = false>
+// AMX: also reduce max |C| into g.amax (its own instantiation: tracking the max in the
+// plain epilogue pushed the main loops past 256 VGPRs -- ~100 spilled)
+template <typename TO, bool SW, bool CIN, bool MB = false, bool AMX = false>
 __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
                                               int n0, int wm, int wn, int lane, int kb) {
     if constexpr (!SW) {
@@ -222,6 +227,7 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
     const unsigned short* mbi = MB ? g.mbi : nullptr;
     unsigned short* mbo = MB ? g.mbo : nullptr;
     const int g4 = (lane >> 4) * 4;
+    unsigned amx = 0u;
     // the mask in two halves of 16 fragments (register budget): two waits per tile
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -247,7 +253,9 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
         if constexpr (sizeof(TO) == 2 && !CIN) {
             // bf16 out: fragments j, j + 1 of a row combined by two v_permlane16_swap per
             // pair, so every lane stores 16 B (8 columns) -- half the store instructions of
-            // the 8-B-per-fragment form (the epilogue tail is store-issue-bound)
+            // the 8-B-per-fragment form (the epilogue tail is store-issue-bound).  amx: the
+            // largest |value| stored (bf16 magnitude bits: their unsigned order is the
+            // magnitude order)
             const int grp = lane >> 4;
             const int coff = 16 * (grp & 1) + 8 * (grp >> 1) - 4 * grp;   // lane's 16-B column
             unsigned wbits[4][2];                      // bits out: rows 4h + ii, words lo / hi
@@ -279,9 +287,12 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
                             for (int e = 0; e < 4; ++e) v[e] = mbit(ii, j, e) ? v[e] : 0.f;
                         }
 #pragma unroll
-                        for (int e = 0; e < 2; ++e)
+                        for (int e = 0; e < 2; ++e) {
                             pk[t][e] = (unsigned)__bfloat16_as_ushort(__float2bfloat16(v[2 * e])) |
                                        ((unsigned)__bfloat16_as_ushort(__float2bfloat16(v[2 * e + 1])) << 16);
+                            if constexpr (AMX)
+                                amx = max(amx, max(pk[t][e] & 0x7fffu, (pk[t][e] >> 16) & 0x7fffu));
+                        }
                         if (mbo) {
                             // value > 0 of the stored bf16: 0x0001 .. 0x7f80 (no -0, no NaN)
                             unsigned nib = 0u;
@@ -358,6 +369,14 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
             }
         }
     }
+    if (AMX && g.amax) {
+        // (one atomic per wave and tile, younger than the epilogue's stores: the callers'
+        //  counted DMA waits then cover one store more than needed -- safe)
+        unsigned m = amx;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+        if (lane == 0 && m) atomicMax(g.amax, m << 16);
+    }
 }
 
 // The Cin branch is resolved once per tile: a uniform branch inside the store loop makes
@@ -366,9 +385,13 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 // Returns the number of stores each wave issued (SW path): the main loops' counted DMA
 // waits leave exactly that many younger stores in flight, so the count must be exact -- a
 // larger allowance would let a stage's DMA pieces still be outstanding at the read.
-template <typename TO, bool SW, bool MB = false>
+template <typename TO, bool SW, bool MB = false, bool AMX = false>
 __device__ __forceinline__ int g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
                                            int n0, int wm, int wn, int lane, int kb) {
+    if constexpr (AMX) {
+        g3_epilogue_t<TO, SW, false, false, true>(g, acc, m0, n0, wm, wn, lane, kb);
+        return 16;
+    }
     if constexpr (MB) {
         // the bit-mask kernels (their own instantiation: the plain epilogue keeps its registers)
         g3_epilogue_t<TO, SW, false, true>(g, acc, m0, n0, wm, wn, lane, kb);
@@ -645,7 +668,8 @@ __device__ __forceinline__ bf16x8 g3p_frag(const char* img, int f0, int u, int l
 // PF: the k-unit 1 fragments of a stage are read into a second register set while unit 0's
 // MFMAs run (3 reads after each of its last four MFMA rows), so the unit-1 MFMAs do not wait
 // for a burst of 12 LDS reads.
-template <typename TO, bool KCA, bool KCB, bool SW, bool MB = false, bool PF = false>
+template <typename TO, bool KCA, bool KCB, bool SW, bool MB = false, bool PF = false,
+          bool AMX = false>
 __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -753,7 +777,7 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
         if (++ktc == nk) {
             int m0, n0, kb;
             unit(ic, m0, n0, kb);
-            epi = (g.diag & 8) ? 0 : g3_epilogue<TO, SW, MB>(g, acc, m0, n0, wm, wn, lane, kb);
+            epi = (g.diag & 8) ? 0 : g3_epilogue<TO, SW, MB, AMX>(g, acc, m0, n0, wm, wn, lane, kb);
             ktc = 0;
             ++ic;
         }
@@ -1181,10 +1205,13 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
         if (g.mbi || g.mbo) {        // ReLU bit masks (srnn_gemm3_try admits modes 0-2 only)
             k = pair ? gemm3p_kernel<TO, KCA, KCB, SW, true> : gemm3_kernel<TO, KCA, KCB, SW, true>;
             ki += 4;
+        } else if (g.amax && pair) {  // max |C| wanted (srnn_gemm_amax_next): no prefetch set
+            k = gemm3p_kernel<TO, KCA, KCB, SW, false, false, true>;
+            ki = 9;
         }
     }
     const int lds = (pp || pair) ? g3p::LDS : g3::LDS;
-    static bool attr[9] = {false, false, false, false, false, false, false, false, false};
+    static bool attr[10] = {};
     if (!attr[ki]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -1231,6 +1258,29 @@ static int g3_pick_split(int tiles, int K) {
 // Returns -1 if the shape/layout is not eligible (caller falls back), else the status.
 // force: take the path whenever eligible (tile == 5), else only when the 256-tile grid
 // (with split-K) occupies the chip at least as well as the 128-tile kernel would.
+// max |C| request for the next bf16-output GEMM that takes the gemm3 path (srnn_gemm_amax_next)
+static unsigned*& g3_amax_pending() {
+    static unsigned* p = nullptr;
+    return p;
+}
+static int& g3_amax_taken() {
+    static int t = 0;
+    return t;
+}
+
+extern "C" int srnn_gemm_amax_next(unsigned* amax) {
+    g3_amax_pending() = amax;
+    g3_amax_taken() = 0;
+    return 0;
+}
+
+extern "C" int srnn_gemm_amax_taken(void) {
+    const int t = g3_amax_taken();
+    g3_amax_pending() = nullptr;
+    g3_amax_taken() = 0;
+    return t;
+}
+
 int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
                    float alpha, const void* A, int64_t lda, const void* B, int64_t ldb,
                    float beta, const float* Cin, int64_t ldcin, void* C, int64_t ldc,
@@ -1258,6 +1308,7 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     g.bias_mode = bias ? bias_mode : 0; g.relu = relu;
     g.diag = env_flag("SRNN_G3DIAG", 0);
     g.mbi = mbi; g.ldmbi = ldmbi; g.mbo = mbo; g.ldmbo = ldmbo;
+    g.amax = nullptr;
     const int tiles = (M / g3::BM) * (N / g3::BN);
     const bool plain = beta == 0.f && !bias && !relu && !mask && !mbi && !mbo &&
                        out_dtype == SRNN_F32;
@@ -1291,5 +1342,13 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
         return srnn_splitk_sum((const float*)g.part, (float*)C, ldc, M, N, ks, s);
     }
     if (out_dtype == SRNN_F32) return launch3_layout<float, true>(g, kca, kcb, s);
+    // max |C| (srnn_gemm_amax_next): computed by the pair-mode kernels (an operand
+    // k-contiguous, K a multiple of 64, no bit masks) -- the request is taken only then
+    if (g3_amax_pending() && beta == 0.f && !mbi && !mbo && (kca || kcb) &&
+        K % g3p::BK == 0 && g3_mode() <= 2 && (g3_mode() != 0)) {
+        g.amax = g3_amax_pending();
+        g3_amax_pending() = nullptr;
+        g3_amax_taken() = 1;
+    }
     return launch3_layout<bf16, true>(g, kca, kcb, s);
 }

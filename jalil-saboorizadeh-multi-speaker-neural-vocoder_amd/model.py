@@ -725,11 +725,19 @@ def mlp_backward(ctx, dlogp, nll=None):
         da2 = H.gemm(dz, W_out, mask=a2, out_dtype=T)                # (M, D)
     dW_hid = H.gemm(da2, a1, transA=True)                            # (D, D)
     db_hid = H.colsum(da2, M, D)
-    # d(upper) in upper's dtype: bf16 when the bottom tier hands the MLP a bf16 upper
+    # d(upper) in upper's dtype: bf16 when the bottom tier hands the MLP a bf16 upper.  A
+    # bf16 da1 also gets max |da1| from the GEMM's epilogue (the packed dTab scatter's
+    # scale), so the scatter needs no pass of its own over da1
+    amax = None
+    if ctx.udt == torch.bfloat16:
+        amax = torch.zeros(1, device=dev, dtype=torch.int32)
+        H.lib().call('srnn_gemm_amax_next', H.ptr(amax))
     if m1 is not None:
         da1 = H.gemm(da2, W_hid, mask_bits=m1, out_dtype=ctx.udt)     # (M, D)
     else:
         da1 = H.gemm(da2, W_hid, mask=a1, out_dtype=ctx.udt)          # (M, D)
+    if amax is not None and not H.lib().dll.srnn_gemm_amax_taken():
+        amax = None
     # folded embedding . conv backward: dTab[q][k][:] += da1[t] for x_{t+k} = q
     dtabT = torch.empty((Q, FS0 * D), device=dev, dtype=T)
     work = torch.empty(Q * FS0 * D, device=dev, dtype=torch.int64)
@@ -738,9 +746,9 @@ def mlp_backward(ctx, dlogp, nll=None):
     colsum = torch.empty(FS0 * D, device=dev, dtype=torch.float32)
     done = ctypes.c_int(0)
     ev = H.roof_begin()
-    H.lib().call('srnn_mlp_dtab2', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.stride(0), 0, B,
+    H.lib().call('srnn_mlp_dtab3', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.stride(0), 0, B,
                  Tl, H.ptr(dtabT), H.dcode(T), D, FS0, Q, H.ptr(work), work.numel() * 8,
-                 H.ptr(colsum), ctypes.byref(done), st())
+                 H.ptr(colsum), ctypes.byref(done), H.ptr(amax), st())
     # algorithmic bytes: da1 and the index window read once, dTab^T and the column sums
     # written once
     H.roof_end('dtab_scatter', ev, B * Tl * D * da1.element_size() +

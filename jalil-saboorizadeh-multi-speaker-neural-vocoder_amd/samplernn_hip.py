@@ -50,6 +50,9 @@ _SIGS = {
     'srnn_mlp_dtab': [_I, _P, _L, _P, _L, _I, _I, _I, _P, _I, _I, _I, _I, _P, _SZ, _P],
     'srnn_mlp_dtab2': [_I, _P, _L, _P, _L, _I, _I, _I, _P, _I, _I, _I, _I, _P, _SZ, _P,
                        ctypes.POINTER(_I), _P],
+    'srnn_mlp_dtab3': [_I, _P, _L, _P, _L, _I, _I, _I, _P, _I, _I, _I, _I, _P, _SZ, _P,
+                       ctypes.POINTER(_I), _P, _P],
+    'srnn_gemm_amax_next': [_P],
     'srnn_logsoftmax_nll': [_P, _L, _P, _L, _I, _L, _I, _P, _P, _L, _P, _I, _L, _F, _P],
     'srnn_logsoftmax_bwd': [_P, _L, _P, _L, _L, _I, _P, _I, _L, _P],
     'srnn_nll_fwd': [_P, _L, _P, _L, _I, _L, _P, _P],
@@ -127,7 +130,8 @@ class _Lib:
             fn.restype = _I
         # query entry points called on .dll directly (pointers are passed as plain ints, so
         # every pointer argument needs its declared type)
-        for name, args in (('srnn_gru_xcd_error', [_P]), ('srnn_persistent_error_take', [])):
+        for name, args in (('srnn_gru_xcd_error', [_P]), ('srnn_persistent_error_take', []),
+                           ('srnn_gemm_amax_taken', [])):
             fn = getattr(self.dll, name)
             fn.argtypes = args
             fn.restype = _I
@@ -172,7 +176,7 @@ def exported_symbols():
     return sorted(_SIGS) + ['srnn_last_error', 'srnn_abi_version', 'srnn_gru_seq_supported',
                             'srnn_gen_persistent_rows', 'srnn_gru_xcd_work_bytes',
                             'srnn_gru_xcd_bwd_work_bytes', 'srnn_gru_xcd_error',
-                            'srnn_persistent_error_take']
+                            'srnn_persistent_error_take', 'srnn_gemm_amax_taken']
 
 
 # Callbacks run just before a persistent sweep (gru_xcd / gru_seq) is enqueued.  Such a sweep

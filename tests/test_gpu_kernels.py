@@ -1218,3 +1218,25 @@ def test_fused_nll_logsoftmax_backward_bit_identical(hip, monkeypatch, dtype):
     loss = snn.sequence_nll_loss_bits(lp, x[:, L:]) + lp.sum() * 0.0
     with pytest.raises(RuntimeError, match='used twice'):
         loss.backward()
+
+
+def test_gemm_amax_request(hip):
+    """srnn_gemm_amax_next: the next bf16-output GEMM on the gemm3 path also writes max |C|
+    (as float bits) -- exactly the max of the bf16 values it stored; a GEMM that takes another
+    path leaves the request untaken."""
+    g = torch.Generator().manual_seed(11)
+    a = (torch.randn(8192, 1024, generator=g)).to(DEV, torch.bfloat16)
+    w = (torch.randn(1024, 1024, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    mask = (torch.rand(8192, 1024, generator=g) > 0.5).to(DEV, torch.bfloat16)
+    amax = torch.zeros(1, device=DEV, dtype=torch.int32)
+    hip.lib().call('srnn_gemm_amax_next', hip.ptr(amax))
+    c = hip.gemm(a, w, mask=mask, out_dtype=torch.bfloat16)
+    assert hip.lib().dll.srnn_gemm_amax_taken() == 1
+    torch.cuda.synchronize()
+    got = amax.view(torch.float32).item()
+    assert got == c.float().abs().max().item()
+    # a small GEMM (not on the 256 x 256 path) does not take the request
+    amax.zero_()
+    hip.lib().call('srnn_gemm_amax_next', hip.ptr(amax))
+    hip.gemm(a[:64, :64].contiguous(), w[:64, :64].contiguous(), out_dtype=torch.bfloat16)
+    assert hip.lib().dll.srnn_gemm_amax_taken() == 0
