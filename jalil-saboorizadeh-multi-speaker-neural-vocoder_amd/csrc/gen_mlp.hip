@@ -241,20 +241,29 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             }
         }
         uint4 lw[UPW][NT], lz[WOL ? 1 : UPW][NZT];
+        // fragment-order images (gen_mlp_prep_weights): the wave's 16 B per lane of (unit,
+        // tile) are one contiguous KiB -- whole lines, where the (D, D) layout read 16 rows x
+        // 64 B per instruction
+        const uint4* fh = reinterpret_cast<const uint4*>(a.wfr_hid);
+        const uint4* fo = reinterpret_cast<const uint4*>(a.wfr_out);
+        const int nzt1 = nzt > 0 ? nzt : 1;
 #pragma unroll
         for (int j = 0; j < UPW; ++j) {
             const int u = wave + gm::NW * j;
+            const int uc = min(u, NU - 1);
             const int ke = min(u * UK + (lane >> 4) * EPL, D - EPL);
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
                 const int n = min(c0 + t * 16 + (lane & 15), D - 1);
-                lw[j][t] = *reinterpret_cast<const uint4*>((const T*)a.w_hid + (int64_t)n * D + ke);
+                lw[j][t] = fh ? fh[(((size_t)p * NU + uc) * nt + min(t, nt - 1)) * 64 + lane]
+                              : *reinterpret_cast<const uint4*>((const T*)a.w_hid + (int64_t)n * D + ke);
             }
             if constexpr (!WOL) {
 #pragma unroll
                 for (int t = 0; t < NZT; ++t) {
                     const int n = min(z0 + t * 16 + (lane & 15), Q - 1);
-                    lz[j][t] = *reinterpret_cast<const uint4*>((const T*)a.w_out + (int64_t)n * D + ke);
+                    lz[j][t] = fo ? fo[(((size_t)p * NU + uc) * nzt1 + min(t, nzt1 - 1)) * 64 + lane]
+                                  : *reinterpret_cast<const uint4*>((const T*)a.w_out + (int64_t)n * D + ke);
                 }
             }
         }
@@ -662,6 +671,23 @@ int gen_noise_launch(const float* noise, uint64_t seed, int row0, const int* bas
     return 0;
 }
 
+// Fragment-order weight images: piece (p, u, t, lane) = 16 B of row p CW + t 16 + (lane & 15)
+// (W_hid) or p NZ + t 16 + (lane & 15) (W_out, clamped to Q - 1), columns u UK + (lane >> 4)
+// EPL .. (clamped to D - EPL), at index ((p NU + u) NT + t) 64 + lane.
+__global__ void gen_wfrag_kernel(const char* __restrict__ w, int64_t ld_bytes, int rows_max,
+                                 int P, int NU, int NT, int RPW, int UKB, int EPLB, int DB,
+                                 uint4* __restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)P * NU * NT * 64;
+    if (i >= total) return;
+    const int lane = (int)(i & 63);
+    const int64_t q = i >> 6;
+    const int t = (int)(q % NT), u = (int)((q / NT) % NU), p = (int)(q / ((int64_t)NT * NU));
+    const int row = min(p * RPW + t * 16 + (lane & 15), rows_max - 1);
+    const int colb = min(u * UKB + (lane >> 4) * EPLB, DB - EPLB);
+    dst[i] = *reinterpret_cast<const uint4*>(w + (int64_t)row * ld_bytes + colb);
+}
+
 // ------------------------------------------------------------------ host side
 namespace {
 typedef void (*GmKernel)(GenMlpArgs);
@@ -745,7 +771,38 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     // fragment-order images: max(R D / GV, NU * 128) granules per group (gm_slot)
     pl->xa_words = (size_t)pl->G * std::max(R * (D / GV), NU * 128);
     pl->xz_words = (size_t)pl->G * R * Q;
+    // fragment-order weight images (16 B per lane per (p, unit, tile)); the fp32 WOL form
+    // keeps W_out in LDS and reads it row-wise
+    const int nt = CW / 16, nzt = NZ / 16 > 0 ? NZ / 16 : 1;
+    pl->wfr_hid_bytes = (size_t)P * NU * nt * 64 * 16;
+    pl->wfr_out_bytes = (dtype == SRNN_F32 && upw > 4) ? 0 : (size_t)P * NU * nzt * 64 * 16;
+    if (!env_flag("SRNN_GEN_WFRAG", 1)) pl->wfr_hid_bytes = pl->wfr_out_bytes = 0;
     return 1;
+}
+
+int gen_mlp_prep_weights(const GenMlpPlan* pl, const void* w_hid, const void* w_out, int D,
+                         int Q, void* fr_hid, void* fr_out, hipStream_t s) {
+    const int es = pl->dtype == SRNN_BF16 ? 2 : 4;
+    const int UK = pl->dtype == SRNN_BF16 ? 32 : 16;
+    const int NU = (D + UK - 1) / UK;
+    const int EPLB = UK / 4 * es;
+    if (pl->wfr_hid_bytes && fr_hid) {
+        const int nt = pl->CW / 16;
+        const int64_t n = (int64_t)pl->P * NU * nt * 64;
+        hipLaunchKernelGGL(gen_wfrag_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s,
+                           (const char*)w_hid, (int64_t)D * es, D, pl->P, NU, nt, pl->CW,
+                           UK * es, EPLB, D * es, (uint4*)fr_hid);
+        SRNN_LAUNCH_CHECK();
+    }
+    if (pl->wfr_out_bytes && fr_out) {
+        const int nzt = pl->NZ / 16 > 0 ? pl->NZ / 16 : 1;
+        const int64_t n = (int64_t)pl->P * NU * nzt * 64;
+        hipLaunchKernelGGL(gen_wfrag_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s,
+                           (const char*)w_out, (int64_t)D * es, Q, pl->P, NU, nzt, pl->NZ,
+                           UK * es, EPLB, D * es, (uint4*)fr_out);
+        SRNN_LAUNCH_CHECK();
+    }
+    return 0;
 }
 
 #define GM_DIAG_BLOCKS 1024

@@ -337,6 +337,8 @@ struct Bufs {
     // persistent sample loop (gen_mlp.hip): hand-off granules + error word, one zeroed block
     unsigned long long* xa1;
     unsigned long long* xa2;
+    void* wfr_hid;                   // fragment-order weight images (gen_mlp_prep_weights)
+    void* wfr_out;
     unsigned long long* xz;
     int* gerr;
     float* lq;               // (lq_steps, B, Q) log q of the persistent launches' draws
@@ -424,6 +426,7 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
     b->lut2 = (float*)take((size_t)Q * 4);
     b->base = (int*)take(64);
     b->xa1 = b->xa2 = b->xz = nullptr;
+    b->wfr_hid = b->wfr_out = nullptr;
     b->gerr = nullptr;
     b->lq = nullptr;
     b->lq_steps = 0;
@@ -434,6 +437,8 @@ size_t carve(const SrnnModel* m, int B, char* ws, Bufs* b, const GenMlpPlan* pl)
         b->xa1 = (unsigned long long*)take(pl->xa_words * 8);
         b->xa2 = (unsigned long long*)take(pl->xa_words * 8);
         b->xz = (unsigned long long*)take(pl->xz_words * 8);
+        b->wfr_hid = pl->wfr_hid_bytes ? take(pl->wfr_hid_bytes) : nullptr;
+        b->wfr_out = pl->wfr_out_bytes ? take(pl->wfr_out_bytes) : nullptr;
         b->lq_steps = m->tier[0].frame_size * (b->fold ? m->tier[1].frame_size : 1);
         b->lq = (float*)take((size_t)b->lq_steps * B * Q * 4);
         b->gm_bytes = off - start;
@@ -642,6 +647,7 @@ int run_block(Ctx& c, int periods) {
             memset(&a, 0, sizeof(a));
             a.tab = m->tab; a.w_hid = m->w_hid; a.b_hid = m->b_hid;
             a.w_out = m->w_out; a.b_out = m->b_out;
+            a.wfr_hid = c.b.wfr_hid; a.wfr_out = c.b.wfr_out;
             a.up0 = c.b.up[0]; a.ldup = c.b.ldup0;
             a.noise = c.noise; a.seed = c.seed; a.row0 = c.row0;
             a.seq = c.seq; a.ldseq = c.ldseq; a.logp = c.logp;
@@ -771,6 +777,9 @@ extern "C" int srnn_generate2(const SrnnModel* m, int n_seqs, int n_cond, const 
             if (rc) break;
             if (c.pl) {
                 rc = hipMemsetAsync(c.b.gerr, 0, c.b.gm_bytes, s) ? 2 : 0;
+                if (rc) break;
+                rc = gen_mlp_prep_weights(c.pl, m->w_hid, m->w_out, D, m->q_levels,
+                                          c.b.wfr_hid, c.b.wfr_out, s);
                 if (rc) break;
             }
             int L = c.L;
