@@ -136,6 +136,11 @@ SITE_NOTES = {
     'mlp_hidden_gemm': 'gemm3p_kernel: sample-level MLP hidden layer (B*T x D x D, bias + '
                        'ReLU epilogue)',
     'adam_clip': 'adam_clip_multi_kernel: fused clamp + Adam over every parameter',
+    'mlp_da1_gemm': 'gemm3p_kernel: sample-level MLP input-activation gradient da1 = (da2 '
+                    'W_hid) * [a1 > 0] (B*T x D x D, ReLU-mask epilogue, max |da1| for the '
+                    'dTab scale)',
+    'mlp_dw_hid_gemm': 'gemm3_kernel: sample-level MLP hidden weight gradient da2^T a1 '
+                       '(D x D x B*T, fp32 out)',
 }
 
 

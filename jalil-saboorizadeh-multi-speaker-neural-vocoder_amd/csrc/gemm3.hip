@@ -1205,13 +1205,16 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
         if (g.mbi || g.mbo) {        // ReLU bit masks (srnn_gemm3_try admits modes 0-2 only)
             k = pair ? gemm3p_kernel<TO, KCA, KCB, SW, true> : gemm3_kernel<TO, KCA, KCB, SW, true>;
             ki += 4;
-        } else if (g.amax && pair) {  // max |C| wanted (srnn_gemm_amax_next): no prefetch set
-            k = gemm3p_kernel<TO, KCA, KCB, SW, false, false, true>;
-            ki = 9;
+        } else if (g.amax && pair) {  // max |C| wanted (srnn_gemm_amax_next)
+            // (SRNN_G3_AMX_PF: with the unit-1 fragment prefetch as well)
+            const int amx_pf = env_flag("SRNN_G3_AMX_PF", 0);
+            k = amx_pf ? gemm3p_kernel<TO, KCA, KCB, SW, false, true, true>
+                       : gemm3p_kernel<TO, KCA, KCB, SW, false, false, true>;
+            ki = amx_pf ? 10 : 9;
         }
     }
     const int lds = (pp || pair) ? g3p::LDS : g3::LDS;
-    static bool attr[10] = {};
+    static bool attr[11] = {};
     if (!attr[ki]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds));

@@ -1,35 +1,46 @@
-"""Time srnn_mlp_dtab at the TBPTT shape (B=128 rows x T=1024, D=1024, FS0=16, Q=256)."""
+"""Time the bf16 dTab scatter (srnn_mlp_dtab2 with column sums, the TBPTT step's call) at
+B = 128 and 512 rows x T = 1024, D = 1024, FS0 = 16, Q = 256, on the bench's synthetic
+mu-law index streams.  HIP events around 10 back-to-back calls after 3 warm-ups."""
+import ctypes
 import os
 import sys
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, 'jalil-saboorizadeh-multi-speaker-neural-vocoder_amd'))
+sys.path.insert(0, os.path.join(ROOT, 'tests', 'golden'))
+import recipe  # noqa: E402
 import samplernn_hip as H  # noqa: E402
+import utils  # noqa: E402
 
 
 def main():
-    B, T, D, FS0, Q = 128, 1024, 1024, 16, 256
-    dt = torch.bfloat16 if os.environ.get('DT', 'bf16') == 'bf16' else torch.float32
-    g = torch.Generator(device='cuda').manual_seed(0)
-    x = torch.randint(0, Q, (B, T + FS0 - 1), device='cuda', generator=g)
-    da = (torch.randn(B * T, D, device='cuda', generator=g) * 1e-4).to(dt)
-    out = torch.empty(Q, FS0 * D, device='cuda', dtype=torch.bfloat16)
-    work = torch.empty(Q * FS0 * D, device='cuda', dtype=torch.int64)
+    T, D, FS0, Q = 1024, 1024, 16, 256
+    for B in (128, 512):
+        audio = np.stack([recipe.synth_audio(T + FS0 - 1, b) for b in range(B)])
+        x = utils.uquantize(torch.from_numpy(audio), Q).cuda()
+        g = torch.Generator(device='cuda').manual_seed(0)
+        da = (torch.randn(B * T, D, device='cuda', generator=g) * 1e-4).bfloat16()
+        out = torch.empty(Q, FS0 * D, device='cuda', dtype=torch.bfloat16)
+        col = torch.empty(FS0 * D, device='cuda')
+        work = torch.empty(Q * FS0 * D, device='cuda', dtype=torch.int64)
+        done = ctypes.c_int(0)
 
-    def run():
-        H.lib().call('srnn_mlp_dtab', H.dcode(dt), H.ptr(da), D, H.ptr(x), x.shape[1], 0, B, T,
-                     H.ptr(out), H.BF16, D, FS0, Q, H.ptr(work), work.numel() * 8, H.stream())
-    for _ in range(3):
-        run()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(10):
-        run()
-    e1.record()
-    e1.synchronize()
-    print('dtab %s: %.3f ms' % (dt, e0.elapsed_time(e1) / 10))
+        def run():
+            H.lib().call('srnn_mlp_dtab2', H.BF16, H.ptr(da), D, H.ptr(x), x.shape[1], 0, B, T,
+                         H.ptr(out), H.BF16, D, FS0, Q, H.ptr(work), work.numel() * 8,
+                         H.ptr(col), ctypes.byref(done), H.stream())
+        for _ in range(3):
+            run()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            run()
+        e1.record()
+        e1.synchronize()
+        print('dtab B=%d: %.3f ms' % (B, e0.elapsed_time(e1) / 10), flush=True)
 
 
 if __name__ == '__main__':
