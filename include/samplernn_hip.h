@@ -202,6 +202,11 @@ int srnn_mlp_dtab3(int dtype, const void* da, int64_t ldda, const int64_t* x, in
  * returns 1 if a GEMM did since (host state; also clears a request no GEMM took).        */
 int srnn_gemm_amax_next(unsigned* amax);
 int srnn_gemm_amax_taken(void);
+/* Number of GEMMs srnn_gemm / srnn_gemm_bits handed to hipBLASLt so far in this process:
+ * large plain bf16 problems (alpha, per-column bias, ReLU, beta 0, no mask; M N >= 4 Mi,
+ * 2 M N K >= 2^33) run as the ROCm library GEMM (SRNN_BLASLT=0: the library's own gemm3
+ * kernels).  Diagnostic; replaces no reference interface.                               */
+int srnn_blaslt_calls(void);
 /* log_softmax (model.py:324-325) + NLL rows (nn.py:66-70) + dlogits (softmax-onehot)*g  */
 /* dz = dlogp - exp(logp) * rowsum(dlogp)   (log_softmax backward, rows of Q)          */
 int srnn_logsoftmax_bwd(const float* dlogp, int64_t lddl, const float* logp, int64_t ldl,

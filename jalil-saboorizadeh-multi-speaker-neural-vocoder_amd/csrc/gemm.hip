@@ -529,6 +529,13 @@ static int gemm_core(int dtype, int out_dtype, int transA, int transB, int M, in
         }
         SRNN_REQUIRE(tile != 4, "gemm: shape not eligible for the skinny path");
     }
+    // large plain bf16 problems: hipBLASLt (blaslt.cpp) unless a fused epilogue or a pending
+    // max |C| request needs gemm3
+    if (tile < 0 && batch == 1 && !mask && !srnn_gemm_amax_pending()) {
+        int rc = srnn_blaslt_try(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, B, ldb,
+                                 beta, C, ldc, bias, bias_mode, relu, s);
+        if (rc >= 0) return rc;
+    }
     // large aligned bf16 problems: the 256x256 8-wave kernel (gemm3.hip); tile 5 forces it
     if ((tile < 0 || tile == 5) && batch == 1 && (tile == 5 || g_use_gemm3())) {
         int rc = srnn_gemm3_try(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, B, ldb,

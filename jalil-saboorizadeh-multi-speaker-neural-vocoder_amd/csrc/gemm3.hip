@@ -1271,6 +1271,8 @@ static int& g3_amax_taken() {
     return t;
 }
 
+int srnn_gemm_amax_pending() { return g3_amax_pending() != nullptr; }
+
 extern "C" int srnn_gemm_amax_next(unsigned* amax) {
     g3_amax_pending() = amax;
     g3_amax_taken() = 0;

@@ -37,7 +37,8 @@ int srnn_persist_spin_limit(int dflt);
 // gemm3.hip: grow-only device scratch buffers, one per slot, never freed (a captured HIP graph
 // keeps the pointer current at its capture); null on a HIP error.  Allocated on first use,
 // i.e. by the eager warm-up step, outside graph captures.
-enum { SRNN_SCRATCH_SPLITK = 0, SRNN_SCRATCH_MASK = 1, SRNN_SCRATCH_NT = 2, SRNN_SCRATCH_SLOTS = 4 };
+enum { SRNN_SCRATCH_SPLITK = 0, SRNN_SCRATCH_MASK = 1, SRNN_SCRATCH_NT = 2, SRNN_SCRATCH_BLASLT = 3,
+       SRNN_SCRATCH_SLOTS = 4 };
 void* srnn_scratch(int slot, size_t bytes);
 
 // Deterministic split-K support.  srnn_splitk_scratch = srnn_scratch(SRNN_SCRATCH_SPLITK);
@@ -45,3 +46,13 @@ void* srnn_scratch(int slot, size_t bytes);
 // N % 4 == 0, C 16-B aligned, ldc % 4 == 0).
 float* srnn_splitk_scratch(size_t bytes);
 int srnn_splitk_sum(const float* part, float* C, int64_t ldc, int M, int N, int ks, hipStream_t s);
+
+// blaslt.cpp: plain large bf16 GEMMs (alpha, optional per-column bias, optional ReLU, beta 0)
+// through hipBLASLt; 0 done, -1 not taken (run the library's own kernels), > 0 error
+int srnn_blaslt_enabled();
+int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
+                    float alpha, const void* A, int64_t lda, const void* B, int64_t ldb, float beta,
+                    void* C, int64_t ldc, const float* bias, int bias_mode, int relu,
+                    hipStream_t s);
+// gemm3.hip: a max |C| request (srnn_gemm_amax_next) waits for the next bf16 gemm3 launch
+int srnn_gemm_amax_pending();

@@ -131,7 +131,7 @@ class _Lib:
         # query entry points called on .dll directly (pointers are passed as plain ints, so
         # every pointer argument needs its declared type)
         for name, args in (('srnn_gru_xcd_error', [_P]), ('srnn_persistent_error_take', []),
-                           ('srnn_gemm_amax_taken', [])):
+                           ('srnn_gemm_amax_taken', []), ('srnn_blaslt_calls', [])):
             fn = getattr(self.dll, name)
             fn.argtypes = args
             fn.restype = _I
@@ -176,7 +176,8 @@ def exported_symbols():
     return sorted(_SIGS) + ['srnn_last_error', 'srnn_abi_version', 'srnn_gru_seq_supported',
                             'srnn_gen_persistent_rows', 'srnn_gru_xcd_work_bytes',
                             'srnn_gru_xcd_bwd_work_bytes', 'srnn_gru_xcd_error',
-                            'srnn_persistent_error_take', 'srnn_gemm_amax_taken']
+                            'srnn_persistent_error_take', 'srnn_gemm_amax_taken',
+                            'srnn_blaslt_calls']
 
 
 # Callbacks run just before a persistent sweep (gru_xcd / gru_seq) is enqueued.  Such a sweep

@@ -92,6 +92,43 @@ def test_gemm3_256_kernel(hip, out_dtype, transA, transB, M, N, K, epi):
     torch.testing.assert_close(out.float().cpu(), ref, atol=tol, rtol=1e-2)
 
 
+@pytest.mark.parametrize('out_dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('transA,transB', [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize('M,N,K,epi', [(4096, 2048, 1024, 'bias_relu'), (2048, 4096, 1024, 'bias'),
+                                       (4096, 1024, 2048, 'plain')])
+def test_gemm_blaslt_plain(hip, monkeypatch, out_dtype, transA, transB, M, N, K, epi):
+    """Large plain bf16 GEMMs (alpha, per-column bias, ReLU; beta 0) go to hipBLASLt
+    (blaslt.cpp): every layout against the fp32 product of the same bf16 operands, against
+    gemm3 (SRNN_BLASLT=0) within bf16 rounding, and bit-identical run to run."""
+    dtype = torch.bfloat16
+    A = _rand(K, M, seed=1) if transA else _rand(M, K, seed=1)
+    B = _rand(N, K, seed=2) if transB else _rand(K, N, seed=2)
+    Ad, Bd = A.to(DEV, dtype), B.to(DEV, dtype)
+    Af, Bf = Ad.float().cpu(), Bd.float().cpu()
+    ref = 1.25 * ((Af.t() if transA else Af) @ (Bf.t() if transB else Bf))
+    bias = _rand(N, seed=3)
+    kw = dict(transA=bool(transA), transB=bool(transB), out_dtype=out_dtype, alpha=1.25)
+    if epi != 'plain':
+        kw['bias'] = bias.to(DEV)
+        ref = ref + bias
+    if epi == 'bias_relu':
+        kw['relu'] = True
+        ref = ref.clamp_min(0)
+
+    def run(on):
+        monkeypatch.setenv('SRNN_BLASLT', '1' if on else '0')
+        n0 = hip.lib().dll.srnn_blaslt_calls()
+        out = hip.gemm(Ad, Bd, **kw)
+        torch.cuda.synchronize()
+        assert hip.lib().dll.srnn_blaslt_calls() - n0 == (1 if on else 0)
+        return out.float().cpu()
+    lt, lt2, g3 = run(True), run(True), run(False)
+    assert torch.equal(lt, lt2)
+    tol = 2e-3 * np.sqrt(K) if out_dtype == torch.float32 else 1e-2 * np.sqrt(K)
+    torch.testing.assert_close(lt, ref, atol=tol, rtol=1e-2)
+    torch.testing.assert_close(lt, g3, atol=tol, rtol=1e-2)
+
+
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('transA', [0, 1])
 @pytest.mark.parametrize('M,N,K', [(1024, 16, 8192), (1024, 43, 2048), (1000, 6, 128),
