@@ -102,6 +102,10 @@ int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int
     // large enough to pay for the library's launch and wide enough that gemm3's split-K deep
     // reductions are not the better choice (M N >= 4 Mi outputs, 2 M N K >= 2^33 flop)
     if ((int64_t)M * N < (4ll << 20) || 2.0 * M * N * K < 8589934592.0) return -1;
+    // (SRNN_BLASLT_F32_MINK: fp32-output problems only from this K on.  In isolation gemm3 writes
+    //  fp32 faster at K of a few thousand -- GRU input projection 32768 x 3072 x 1024: 220 vs
+    //  266 us -- but inside the step the library form measured 0.1-0.2 ms per step faster)
+    if (out_dtype == SRNN_F32 && K < env_flag("SRNN_BLASLT_F32_MINK", 0)) return -1;
     if (M % 16 || N % 16 || K % 16 || lda % 8 || ldb % 8 || ldc % 8) return -1;
     const int epi = bias ? (relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_BIAS)
                          : (relu ? HIPBLASLT_EPILOGUE_RELU : HIPBLASLT_EPILOGUE_DEFAULT);

@@ -29,7 +29,11 @@ shapes = [('hid_fwd NT', M, 1024, 1024, False, True, torch.bfloat16),
           ('up_fwd NT', 32768, 16384, 1024, False, True, torch.bfloat16),
           ('up_dX NN', 32768, 1024, 16384, False, False, torch.float32),
           ('up_dW TN', 16384, 1024, 32768, True, False, torch.float32),
-          ('out_fwd NT', M, 256, 1024, False, True, torch.float32)]
+          ('out_fwd NT', M, 256, 1024, False, True, torch.float32),
+          ('dW_ih TN', 3072, 1024, 32768, True, False, torch.float32),
+          ('dW_out TN', 256, 1024, M, True, False, torch.float32),
+          ('gi_fwd NT', 32768, 3072, 1024, False, True, torch.float32),
+          ('dX_ih NN', 32768, 1024, 3072, False, False, torch.float32)]
 try:
     torch.mm(torch.ones(16, 16, device='cuda', dtype=torch.bfloat16),
              torch.ones(16, 16, device='cuda', dtype=torch.bfloat16), out_dtype=torch.float32)

@@ -1,6 +1,6 @@
 set -e
 R=$PWD; O=$R/gpurun_out; mkdir -p $O; export TMPDIR=/tmp; cd /tmp
-for B in 512 128; do
+for B in ${BS:-512 128}; do
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d /tmp/p$B -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-gen --no-cpu --no-extra --batch $B > $O/r03_prof_b$B.log 2>&1
 db=$(find /tmp/p$B -name '*.db' | head -1)
 python3 $R/tools/kstats.py $db 3 12 > $O/r03_step_kernels_b$B.txt
