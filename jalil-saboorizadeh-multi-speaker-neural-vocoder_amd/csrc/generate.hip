@@ -314,9 +314,10 @@ __global__ void init_state_kernel(const float* __restrict__ h0, float* __restric
 
 __global__ void advance_kernel(int* base, int by) { *base += by; }
 
-__global__ void copy_bf16_kernel(const float* __restrict__ src, bf16* __restrict__ dst, int n) {
+template <typename T>
+__global__ void copy_cast_kernel(const float* __restrict__ src, T* __restrict__ dst, int n) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < n) dst[e] = from_f<bf16>(src[e]);
+    if (e < n) dst[e] = from_f<T>(src[e]);
 }
 
 namespace {
@@ -362,9 +363,13 @@ struct Bufs {
     int64_t ldg1;            //  upper tick], ldg1 = FS1 3D + 3D
 };
 
+// fp32 too (SRNN_GEN_FOLD_F32=0: unfolded fp32 ticks): the folds reassociate fp32 sums
+// (W_ih (W_in a + b) -> (W_ih W_in) a + W_ih b), same precision, rounding in the last bits
 bool fold_ok(const SrnnModel* m) {
     const SrnnTier& t = m->tier[0];
-    return m->dtype == SRNN_BF16 && m->n_tiers >= 2 && m->n_rnn == 1 &&
+    return (m->dtype == SRNN_BF16 || (env_flag("SRNN_GEN_FOLD_F32", 1) && m->dim % 64 == 0)) &&
+           m->n_tiers >= 2 &&
+           m->n_rnn == 1 &&
            t.in_dim == t.n_frame_samples && t.n_frame_samples <= 16 && t.b_up &&
            m->tier[1].frame_size <= FOLD_MAX_FS1 &&
            env_flag("SRNN_GEN_FOLD", 1);
@@ -492,11 +497,18 @@ int tier_tick(Ctx& c, int k, int off, int par) {
             return linear_fwd(dt, SRNN_F32, B, (int)(fs0d + 3 * D), D, c.b.hlp[0][0][nxt], D,
                               c.b.wcat, D, c.b.bcat, c.b.up[0], c.b.ldup0, 0, c.s);
         }
-        hipLaunchKernelGGL((fold_gru_kernel<bf16>), dim3(g2.x, g2.y, planes), dim3(256), 0, c.s,
-                           c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.L,
-                           c.b.fmin, c.b.fg + (size_t)fi * 3 * D, c.b.ldg1,
-                           c.b.up[0] + fs0d, c.b.ldup0, c.b.h[0][0][cur], c.b.h[0][0][nxt],
-                           (bf16*)c.b.hlp[0][0][nxt], B, D, nz);
+        if (dt == SRNN_F32)
+            hipLaunchKernelGGL((fold_gru_kernel<float>), dim3(g2.x, g2.y, planes), dim3(256), 0,
+                               c.s, c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2,
+                               c.L, c.b.fmin, c.b.fg + (size_t)fi * 3 * D, c.b.ldg1,
+                               c.b.up[0] + fs0d, c.b.ldup0, c.b.h[0][0][cur], c.b.h[0][0][nxt],
+                               (float*)c.b.hlp[0][0][nxt], B, D, nz);
+        else
+            hipLaunchKernelGGL((fold_gru_kernel<bf16>), dim3(g2.x, g2.y, planes), dim3(256), 0,
+                               c.s, c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2,
+                               c.L, c.b.fmin, c.b.fg + (size_t)fi * 3 * D, c.b.ldg1,
+                               c.b.up[0] + fs0d, c.b.ldup0, c.b.h[0][0][cur], c.b.h[0][0][nxt],
+                               (bf16*)c.b.hlp[0][0][nxt], B, D, nz);
         SRNN_LAUNCH_CHECK();
         return linear_fwd(dt, SRNN_F32, B, (int)(fs0d + 3 * D), D, c.b.hlp[0][0][nxt], D,
                           c.b.wcat, D, c.b.bcat, c.b.up[0], c.b.ldup0, 0, c.s);
@@ -514,9 +526,14 @@ int tier_tick(Ctx& c, int k, int off, int par) {
             c.noise_beg = off;
             c.noise_end = off + nz.nsteps;
         }
-        hipLaunchKernelGGL((tier_a_kernel<bf16>), dim3(gx, 1, planes), dim3(256), 0, c.s, c.seq,
-                           c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.cond, c.n_cond,
-                           m->cond_dim, c.L, t.in_dim, (bf16*)c.b.atop, B, nz);
+        if (dt == SRNN_F32)
+            hipLaunchKernelGGL((tier_a_kernel<float>), dim3(gx, 1, planes), dim3(256), 0, c.s,
+                               c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.cond,
+                               c.n_cond, m->cond_dim, c.L, t.in_dim, (float*)c.b.atop, B, nz);
+        else
+            hipLaunchKernelGGL((tier_a_kernel<bf16>), dim3(gx, 1, planes), dim3(256), 0, c.s,
+                               c.seq, c.ldseq, c.b.base, off, t.n_frame_samples, c.b.lut2, c.cond,
+                               c.n_cond, m->cond_dim, c.L, t.in_dim, (bf16*)c.b.atop, B, nz);
         SRNN_LAUNCH_CHECK();
         const int64_t g0 = (int64_t)t.frame_size * 3 * D;
         RET(srnn_gru_cell_x_impl(dt, B, D, TA_AP, c.b.atop, TA_AP, c.b.min1, nullptr, c.b.p1,
@@ -804,8 +821,9 @@ extern "C" int srnn_generate2(const SrnnModel* m, int n_seqs, int n_cond, const 
             // folded bottom tick operands (see fold_gru_kernel), and gh of its first tick
             const SrnnTier& t0 = m->tier[0];
             const size_t upw = (size_t)t0.frame_size * D;
-            rc = (hipMemcpyAsync(c.b.wcat, t0.w_up, upw * D * 2, hipMemcpyDeviceToDevice, s) ||
-                  hipMemcpyAsync((char*)c.b.wcat + upw * D * 2, t0.w_hh[0], (size_t)3 * D * D * 2,
+            const size_t es = m->dtype == SRNN_F32 ? 4 : 2;
+            rc = (hipMemcpyAsync(c.b.wcat, t0.w_up, upw * D * es, hipMemcpyDeviceToDevice, s) ||
+                  hipMemcpyAsync((char*)c.b.wcat + upw * D * es, t0.w_hh[0], (size_t)3 * D * D * es,
                                  hipMemcpyDeviceToDevice, s) ||
                   hipMemcpyAsync(c.b.bcat, t0.b_up, upw * 4, hipMemcpyDeviceToDevice, s))
                      ? 2 : 0;
@@ -816,10 +834,16 @@ extern "C" int srnn_generate2(const SrnnModel* m, int n_seqs, int n_cond, const 
                          ? 2 : 0;
             if (rc) { srnn_set_error("generate: fold weight copy"); break; }
             const SrnnTier& t1 = m->tier[1];
-            hipLaunchKernelGGL((fold_input_kernel<bf16>), dim3(cdiv(3 * D, 4)), dim3(256), 0, s,
-                               (const bf16*)t0.w_ih[0], (const bf16*)t0.w_in, t0.n_frame_samples,
-                               t0.b_in, t0.b_ih[0], t1.b_up, t1.frame_size, c.b.fmin, c.b.bfold,
-                               3 * D, D);
+            if (m->dtype == SRNN_F32)
+                hipLaunchKernelGGL((fold_input_kernel<float>), dim3(cdiv(3 * D, 4)), dim3(256), 0,
+                                   s, (const float*)t0.w_ih[0], (const float*)t0.w_in,
+                                   t0.n_frame_samples, t0.b_in, t0.b_ih[0], t1.b_up,
+                                   t1.frame_size, c.b.fmin, c.b.bfold, 3 * D, D);
+            else
+                hipLaunchKernelGGL((fold_input_kernel<bf16>), dim3(cdiv(3 * D, 4)), dim3(256), 0,
+                                   s, (const bf16*)t0.w_ih[0], (const bf16*)t0.w_in,
+                                   t0.n_frame_samples, t0.b_in, t0.b_ih[0], t1.b_up,
+                                   t1.frame_size, c.b.fmin, c.b.bfold, 3 * D, D);
             if (hipGetLastError() != hipSuccess) {
                 srnn_set_error("generate: fold_input launch");
                 rc = 2;
@@ -832,7 +856,7 @@ extern "C" int srnn_generate2(const SrnnModel* m, int n_seqs, int n_cond, const 
             if (rc) break;
             // [W_hh1; b_hh1] after the folded rows, and gh1 of the first upper tick
             const size_t g0 = (size_t)t1.frame_size * 3 * D;
-            rc = (hipMemcpyAsync((char*)c.b.wfold + g0 * D * 2, t1.w_hh[0], (size_t)3 * D * D * 2,
+            rc = (hipMemcpyAsync((char*)c.b.wfold + g0 * D * es, t1.w_hh[0], (size_t)3 * D * D * es,
                                  hipMemcpyDeviceToDevice, s) ||
                   (t1.b_hh[0] ? hipMemcpyAsync(c.b.bfold + g0, t1.b_hh[0], (size_t)3 * D * 4,
                                                hipMemcpyDeviceToDevice, s)
@@ -863,14 +887,18 @@ extern "C" int srnn_generate2(const SrnnModel* m, int n_seqs, int n_cond, const 
             if (c.b.fold_top) {
                 // Min1 = W_ih1 (3D x D) . W_in1 (D x in_dim), zero-padded to TA_AP columns;
                 // P1 = bf16(row_bias) . W_ih1^T + b_ih1
-                rc = hipMemsetAsync(c.b.min1, 0, (size_t)3 * D * TA_AP * 2, s) ? 2 : 0;
+                rc = hipMemsetAsync(c.b.min1, 0, (size_t)3 * D * TA_AP * es, s) ? 2 : 0;
                 if (!rc)
                     rc = srnn_gemm_impl(m->dtype, m->dtype, 0, 0, 3 * D, t1.in_dim, D, 1.f,
                                         t1.w_ih[0], D, 0, t1.w_in, t1.in_dim, 0, 0.f, nullptr, 0,
                                         0, c.b.min1, TA_AP, 0, nullptr, 0, 0, 1, -1, s);
                 if (!rc) {
-                    hipLaunchKernelGGL((copy_bf16_kernel), dim3(cdiv(B * D, 256)), dim3(256), 0,
-                                       s, c.row_bias, (bf16*)c.b.x[1], B * D);
+                    if (m->dtype == SRNN_F32)
+                        hipLaunchKernelGGL((copy_cast_kernel<float>), dim3(cdiv(B * D, 256)),
+                                           dim3(256), 0, s, c.row_bias, (float*)c.b.x[1], B * D);
+                    else
+                        hipLaunchKernelGGL((copy_cast_kernel<bf16>), dim3(cdiv(B * D, 256)),
+                                           dim3(256), 0, s, c.row_bias, (bf16*)c.b.x[1], B * D);
                     rc = linear_fwd(m->dtype, SRNN_F32, B, 3 * D, D, c.b.x[1], D, t1.w_ih[0], D,
                                     t1.b_ih[0], c.b.p1, 3 * D, 0, s);
                 }

@@ -176,6 +176,26 @@ def test_folded_bottom_tick_bf16(hip, monkeypatch, cfgname, D, B, persistent):
     assert err.mean().item() < 0.02, err.mean().item()
 
 
+@pytest.mark.parametrize('persistent', [True, False])
+def test_folded_ticks_fp32(hip, monkeypatch, persistent):
+    """fp32 folded ticks (SRNN_GEN_FOLD_F32, dim % 64 == 0: gi = (W_ih W_in) a + G[fi], gh
+    carried by the previous tick's [W_up; W_hh] GEMM, the folded top tick) against the
+    unfolded fp32 ticks: the same index stream (the folds only reassociate fp32 sums) and
+    log-probs within fp32 reassociation error."""
+    cfg = dict(recipe.CONFIGS['t3'], dim=128)
+    m, _ = build(cfg, 19, torch.float32)
+    B, n_cond = 24, 3
+    cond = recipe.synth_cond((B, n_cond, cfg['cond_dim']), 16)
+    spk = np.arange(B) % cfg['spk_dim']
+    noise = torch.from_numpy(recipe.synth_noise((n_cond * m.lookback, B, 256), 17))
+    monkeypatch.setenv('SRNN_GEN_FOLD_F32', '1')
+    s1, l1 = generate(m, B, cond, spk, persistent, noise=noise)
+    monkeypatch.setenv('SRNN_GEN_FOLD_F32', '0')
+    s0, l0 = generate(m, B, cond, spk, persistent, noise=noise)
+    assert torch.equal(s1, s0)
+    torch.testing.assert_close(l1, l0, atol=2e-5, rtol=0)
+
+
 def test_persistent_philox_matches_per_sample_fp32(hip):
     """Device RNG: both paths draw Philox4x32-10(seed) noise with the same counters."""
     cfg = dict(recipe.CONFIGS['t3'], dim=128)
