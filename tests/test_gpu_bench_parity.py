@@ -83,4 +83,8 @@ def test_bench_bf16_step_matches_fp32(hip, B):
     for rel, cos, k in worst:
         print('%-60s rel %.4f cos %.6f' % (k, rel, cos))
     for rel, cos, k in worst:
-        assert rel < 0.1 and cos >= 0.995, (k, rel, cos)
+        # the MLP's dense layers see no recurrence: bf16 operand rounding only (measured
+        # <= 0.6 %, MI355X round 3); everything upstream of the GRU sweeps or the dTab
+        # scatter carries the recurrences' roundings (measured <= 6.8 %, cos >= 0.9977)
+        dense = k.startswith(('model.sample_level_mlp.hidden', 'model.sample_level_mlp.output'))
+        assert rel < (0.01 if dense else 0.085) and cos >= 0.997, (k, rel, cos)

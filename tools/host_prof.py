@@ -35,6 +35,14 @@ def main():
     torch.cuda.synchronize()
     tr.dataset = batches[3:]
     tr.enqueue_s = 0.0
+    t0 = time.perf_counter()
+    tr.train()
+    torch.cuda.synchronize()
+    print('rows %d, no profiler: %.3f ms/step wall, host enqueue %.3f ms/step'
+          % (rows, (time.perf_counter() - t0) / steps * 1e3, tr.enqueue_s / steps * 1e3))
+    tr.enqueue_s = 0.0
+    # the backward's Python functions run on the calling thread (visible to cProfile)
+    torch.autograd.set_multithreading_enabled(False)
     pr = cProfile.Profile()
     t0 = time.perf_counter()
     pr.enable()
@@ -46,7 +54,7 @@ def main():
           % (rows, dt / steps * 1e3, tr.enqueue_s / steps * 1e3, tr.graph_steps))
     for key in ('tottime', 'cumulative'):
         s = io.StringIO()
-        pstats.Stats(pr, stream=s).sort_stats(key).print_stats(45)
+        pstats.Stats(pr, stream=s).sort_stats(key).print_stats(70)
         print(s.getvalue())
 
 
