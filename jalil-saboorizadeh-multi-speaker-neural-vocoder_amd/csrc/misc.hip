@@ -703,7 +703,19 @@ __global__ __launch_bounds__(256) void colsum_kernel(const T* __restrict__ src, 
     const int64_t r1 = min(rows, r0 + rpb);
     float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
     if (VEC && c + 3 < cols) {
-        for (int64_t r = r0 + ty; r < r1; r += 16) {
+        // four rows' loads in flight before their adds (one 8-16 B load per thread and
+        // round trip left the pass latency-bound at ~4.9 TB/s); same summation order
+        int64_t r = r0 + ty;
+        for (; r + 48 < r1; r += 64) {
+            float v[4][4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) cs_ld4(src + (r + 16 * u) * lds + c, v[u]);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                s0 += v[u][0]; s1 += v[u][1]; s2 += v[u][2]; s3 += v[u][3];
+            }
+        }
+        for (; r < r1; r += 16) {
             float v[4];
             cs_ld4(src + r * lds + c, v);
             s0 += v[0]; s1 += v[1]; s2 += v[2]; s3 += v[3];
