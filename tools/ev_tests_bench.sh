@@ -1,6 +1,7 @@
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r03c_gpu_tests.log 2>&1
-timeout -k 10 300 python3 bench.py > gpurun_out/r03c_bench.json 2> gpurun_out/r03c_bench.err
+timeout -k 10 420 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r03e_gpu_tests.log 2>&1
+timeout -k 10 300 python3 bench.py > gpurun_out/r03e_bench.json 2> gpurun_out/r03e_bench.err
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03e_smoke.log 2>&1
 echo ok
