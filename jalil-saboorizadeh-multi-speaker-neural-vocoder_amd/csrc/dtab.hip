@@ -360,7 +360,11 @@ __global__ __launch_bounds__(256) void dtab_prep_kernel(const T* __restrict__ da
     if (hist[tid]) atomicAdd(&st->count[tid], hist[tid]);
 }
 
-template <typename T>
+// PD: how many 16-position batches ahead a lane's da value is loaded (raw bits, converted
+// when its batch comes up).  A batch of 16 atomics takes ~0.7 us of the CU's LDS pipeline
+// with 16 waves resident, less than an HBM load's latency under load, so a one-batch-ahead
+// load left the waves waiting on vmcnt between batches.
+template <typename T, int PD = 1>
 __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
     const T* __restrict__ da, int64_t ldda, const int64_t* __restrict__ x, int64_t ldx, int xoff,
     int Tlen, int B, const DtabStat* __restrict__ st, const unsigned* __restrict__ amax_in,
@@ -418,10 +422,12 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
         const int b = b2 + h;
         const bool rv = b < B;
         const T* drow = da + (int64_t)(rv ? b : b2) * Tlen * ldda + cA;
-        auto load = [&](int pbase) -> unsigned long long {
+        auto raw = [&](int pbase) -> uint32_t {
             const int t = pbase + li;
-            if (!(rv && t < Tlen)) return 0ull;
-            const uint32_t u = *reinterpret_cast<const uint32_t*>(drow + (int64_t)t * ldda);
+            if (!(rv && t < Tlen)) return 0u;                 // zero bits: a zero pair
+            return *reinterpret_cast<const uint32_t*>(drow + (int64_t)t * ldda);
+        };
+        auto conv = [&](uint32_t u) -> unsigned long long {
             const float gA = to_f(*reinterpret_cast<const T*>(&u));
             const float gB = to_f(*(reinterpret_cast<const T*>(&u) + 1));
             if (want_col) {
@@ -448,7 +454,10 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
                 if (q0 + 64 * k < 2 * WPB) strip[q0 + 64 * k] = (unsigned char)v[k];
         }
         unsigned long long cur = 0;
-        unsigned long long nxt = load(0);
+        unsigned long long nxt = conv(raw(0));
+        uint32_t pre[PD > 1 ? PD - 1 : 1];               // raw values of batches bt + 2 ..
+#pragma unroll
+        for (int i = 0; i + 1 < PD; ++i) pre[i] = raw(16 * (i + 1));
         const unsigned sh = strip_base + (unsigned)(h * WPB);
         dt_u32x4 qn;
         asm volatile("s_waitcnt lgkmcnt(0)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
@@ -459,7 +468,14 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
             const unsigned long long nv = nxt;
             const dt_u32x4 qc = qn;
             if (bt + 1 < nbatch) {
-                nxt = load(pbase + 16);
+                if constexpr (PD > 1) {
+                    nxt = conv(pre[0]);
+#pragma unroll
+                    for (int i = 0; i + 2 < PD; ++i) pre[i] = pre[i + 1];
+                    pre[PD - 2] = raw(pbase + 16 * PD);
+                } else {
+                    nxt = conv(raw(pbase + 16));
+                }
                 asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(qn)
                              : "v"(sh + (unsigned)pbase) : "memory");
             }
@@ -633,12 +649,18 @@ extern "C" int srnn_mlp_dtab3(int dtype, const void* da, int64_t ldda, const int
         SRNN_LAUNCH_CHECK();
         static bool attr = false;
         if (!attr) {
-            SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_pk_kernel<bf16>,
+            SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_pk_kernel<bf16, 1>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               160 * 1024));
+            SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_pk_kernel<bf16, 4>,
                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                160 * 1024));
             attr = true;
         }
-        hipLaunchKernelGGL(dtab_pk_kernel<bf16>, dim3(cdiv(D, 4)), dim3(DTAB_NT),
+        // SRNN_DTAB_PD=1: the one-batch-ahead da load (default: four batches ahead)
+        const char* pde = getenv("SRNN_DTAB_PD");
+        auto pk = (pde && pde[0] == '1') ? dtab_pk_kernel<bf16, 1> : dtab_pk_kernel<bf16, 4>;
+        hipLaunchKernelGGL(pk, dim3(cdiv(D, 4)), dim3(DTAB_NT),
                            pk_lds_bytes(Q, Tlen), s, (const bf16*)da, ldda, x, ldx, xoff, Tlen, B,
                            st, amax_in, (bf16*)dtab_out, colsum, D, Q);
         SRNN_LAUNCH_CHECK();

@@ -40,7 +40,8 @@ def main():
             run()
         e1.record()
         e1.synchronize()
-        print('dtab B=%d: %.3f ms' % (B, e0.elapsed_time(e1) / 10), flush=True)
+        print('dtab B=%d SRNN_DTAB_PD=%s: %.3f ms' % (B, os.environ.get('SRNN_DTAB_PD', '4'),
+                                                    e0.elapsed_time(e1) / 10), flush=True)
 
 
 if __name__ == '__main__':
