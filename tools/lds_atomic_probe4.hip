@@ -2,7 +2,9 @@
 // atomics?  Same ds_add_u64 pattern as lds_atomic_probe3 (16 waves/CU, 16 atomics then
 // lgkmcnt(15)); mode 1 adds, per 16 atomics, the scatter's da load: each lane reads 4 B of a
 // different 2-KiB row (16 rows x 2 adjacent lanes per half-wave: 32 cache lines per
-// instruction, 8 B used of each), issued four batches ahead, its value feeding the atomics.
+// instruction, 8 B used of each), issued four batches ahead, its value feeding the atomics;
+// mode 2 the same loads from a column-blocked layout (the 16 rows' 8-B pairs contiguous: one
+// whole line per half-wave).
 //   hipcc --offload-arch=gfx950 -O3 -o tools/probe4.bin tools/lds_atomic_probe4.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -24,6 +26,7 @@ __global__ __launch_bounds__(1024) void k(const unsigned* __restrict__ src,
     const int row0 = (int)((blockIdx.x * 16 + wave) * 2 + h) * 4096;
     auto ld = [&](int i) -> unsigned {
         const int row = (row0 + i * 16 + li) & (NROWS - 1);
+        if (MODE == 2) return src[(size_t)row * 2 + p];           // < 2 * NROWS: in bounds
         return src[(size_t)row * ROWU + col];
     };
     unsigned r0 = 0, r1 = 0, r2 = 0, r3 = 0;
@@ -54,6 +57,7 @@ int main() {
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
     (void)hipFuncSetAttribute((const void*)k<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     (void)hipFuncSetAttribute((const void*)k<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    (void)hipFuncSetAttribute((const void*)k<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     const int blocks = ncu * 4;                   // 4 rounds of one 1024-thread workgroup per CU
     unsigned long long* out;
     unsigned* src;
@@ -64,13 +68,15 @@ int main() {
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     const int iters = 2048;
-    for (int mode = 0; mode < 2; ++mode)
+    for (int mode = 0; mode < 3; ++mode)
         for (int rep = 0; rep < 3; ++rep) {
             (void)hipEventRecord(e0);
             if (mode == 0)
                 hipLaunchKernelGGL(k<0>, dim3(blocks), dim3(1024), 100 * 1024, 0, src, out, iters, 7u + rep);
-            else
+            else if (mode == 1)
                 hipLaunchKernelGGL(k<1>, dim3(blocks), dim3(1024), 100 * 1024, 0, src, out, iters, 7u + rep);
+            else
+                hipLaunchKernelGGL(k<2>, dim3(blocks), dim3(1024), 100 * 1024, 0, src, out, iters, 7u + rep);
             (void)hipEventRecord(e1);
             (void)hipEventSynchronize(e1);
             float ms;
@@ -78,7 +84,8 @@ int main() {
             const double ops = (double)blocks * 1024 * iters * 16;
             if (rep)
                 printf("mode %d (%s): %.3f ms  %.1f lane-ops per clock per CU at 2.4 GHz\n", mode,
-                       mode ? "atomics + da-pattern loads" : "atomics only", ms,
+                       mode == 2 ? "atomics + whole-line loads" : mode ? "atomics + da-pattern loads"
+                                                                   : "atomics only", ms,
                        ops / (ms * 1e-3) / ncu / 2.4e9);
         }
     return 0;
