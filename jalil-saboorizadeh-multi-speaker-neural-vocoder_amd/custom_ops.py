@@ -427,9 +427,10 @@ def generate(weights: list[Tensor], meta: list[int], cond: Tensor, row_bias: Ten
 def _(weights, meta, cond, row_bias, noise, seed, row_offset, flags, return_logp):
     n_seqs, num_cond = cond.shape[0], cond.shape[1]
     L = meta[-1]
+    Q = meta[3]                      # q_levels (model.generation_weights' meta layout)
     T = num_cond * L
     return (cond.new_empty((n_seqs, L + T), dtype=torch.long),
-            cond.new_empty((T, n_seqs, 256) if return_logp else (0,)))
+            cond.new_empty((T, n_seqs, Q) if return_logp else (0,)))
 
 
 OPS = ('tier_fwd', 'tier_bwd', 'mlp_fwd', 'mlp_bwd', 'nll_bits', 'nll_bits_bwd', 'upsample',

@@ -177,12 +177,15 @@ def main(frame_sizes, **params):
             spks[j * n:(j + 1) * n] = jobs[j][1]
         gen = Generator(model, use_cuda)
         if world > 1:
-            # rank-sharded: contiguous row shards, Philox noise of the global
-            # rows, gathered at the end (rows padded to a multiple of the world size)
+            # rank-sharded: contiguous row shards gathered at the end (rows
+            # padded to a multiple of the world size); either sampler reproduces the
+            # single-process stream (shard_generate)
             pad = (-len(rows)) % world
             prow = np.concatenate([rows, np.zeros((pad,) + rows.shape[1:], rows.dtype)])
             pspk = np.concatenate([spks, np.zeros(pad, spks.dtype)])
-            out = shard_generate(gen, len(prow), prow, pspk, params['seed']).numpy()[:len(rows)]
+            out = shard_generate(gen, len(prow), prow, pspk, params['seed'],
+                                 sampler=params['sampler'],
+                                 seq_len=params['sample_length']).numpy()[:len(rows)]
         else:
             out = gen(len(rows), params['sample_length'], rows, spks, sampler=params['sampler'],
                       seed=params['seed']).numpy()

@@ -990,23 +990,38 @@ class Generator(Runner):
         return out
 
 
-def shard_generate(generator, n_seqs, cond, spk, seed, rank=None, world=None, **kw):
+def shard_generate(generator, n_seqs, cond, spk, seed, rank=None, world=None, sampler='philox',
+                   seq_len=0, **kw):
     """Rank-sharded generation (the reference runs generate.py:241-253 per file on
     one device): rank r generates the contiguous rows [r n / N, (r + 1) n / N) of an n_seqs batch
-    with replicated weights and no collective in the loop (Philox noise of the GLOBAL rows, so
-    the union equals the single-process output); the dequantized rows are gathered to every
-    rank at the end.  cond: (num_cond, C) shared or (n_seqs, num_cond, C) per row; spk: int or
-    (n_seqs,).  Returns the host float32 (n_seqs, num_cond * lookback) batch."""
+    with replicated weights and no collective in the loop; the dequantized rows are gathered to
+    every rank at the end, and the union equals the single-process output for either sampler:
+      * 'philox': the device noise of the GLOBAL rows (row_offset);
+      * 'torch' (the reference's multinomial stream, model.py:514-517): every rank draws the
+        whole batch's Exp(1) noise from torch's CPU generator exactly as a single process
+        would (one (T, n_seqs, Q) draw, so every rank must have been seeded alike) and keeps
+        its rows' slice -- host memory T * n_seqs * Q * 4 bytes per rank.
+    cond: (num_cond, C) shared or (n_seqs, num_cond, C) per row; spk: int or (n_seqs,).
+    seq_len is accepted like Generator's (the reference ignores it, model.py:455).
+    Returns the host float32 (n_seqs, num_cond * lookback) batch."""
     import distributed as Dd
     rank = Dd.rank() if rank is None else rank
     world = Dd.world() if world is None else world
+    if sampler not in ('philox', 'torch'):
+        raise ValueError('shard_generate: unknown sampler %r' % (sampler,))
     rows = Dd.shard_rows(n_seqs, rank, world)
     c = torch.as_tensor(np.asarray(cond) if not torch.is_tensor(cond) else cond)
+    num_cond = c.shape[-2]
     if c.dim() == 3:
         c = c[rows]
     s = torch.as_tensor(np.asarray(spk) if not torch.is_tensor(spk) else spk).reshape(-1)
     if s.numel() > 1:
         s = s[rows]
-    out = generator(rows.stop - rows.start, 0, c, s, sampler='philox', seed=seed,
+    if sampler == 'torch' and kw.get('noise') is None:
+        model = generator.model
+        full = torch.empty(num_cond * model.lookback, n_seqs, model.q_levels).exponential_(1)
+        kw['noise'] = full[:, rows].contiguous()
+        del full
+    out = generator(rows.stop - rows.start, seq_len, c, s, sampler=sampler, seed=seed,
                     row_offset=rows.start, **kw)
     return Dd.gather_rows(out, n_seqs)

@@ -168,8 +168,11 @@ def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
                         reduced = self.grad_sync.reduced
                     else:
                         self.grad_sync(optimizer)
-                if self.dsteps is None:
+                if self.dsteps is None or len(self.dsteps.mirror) != len(optimizer.param_groups):
+                    # first step, or add_param_group since: one counter per group, re-seeded
+                    # from the host step counts on this step
                     self.dsteps = DeviceSteps(optimizer, optimizer.param_groups[0]['params'][0].device)
+                    self.dsteps.mirror = [None] * len(optimizer.param_groups)
                 with torch.no_grad():
                     _fused_adam_step(optimizer, min, max, reduced, self.dsteps)
                 return loss
@@ -233,7 +236,9 @@ def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
         def after_replay(self):
             """The host bookkeeping the replayed step did not run: step counts + 1."""
             for gi, group in enumerate(optimizer.param_groups):
-                _advance_steps([(p, st) for p in group['params']
+                # the same item list _fused_adam_step advances (requires_grad AND state), so
+                # the flat step buffer is reused and a frozen parameter's count stays put
+                _advance_steps([(p, st) for p in group['params'] if p.requires_grad
                                 for st in (optimizer.state.get(p),) if st and 'step' in st],
                                optimizer, gi)
             self.dsteps.mirror = [None if m is None else m + 1 for m in self.dsteps.mirror]

@@ -21,11 +21,58 @@ def golden(name):
     return np.load(os.path.join(GOLDEN, name + '.npz'))
 
 
-@pytest.fixture(scope='session')
-def hip():
-    """The product HIP library; GPU tests fail loudly if it cannot be loaded."""
+def genlong_noise(g, q_levels=256):
+    """The reference's multinomial noise of a genlong_* fixture, regenerated from torch's CPU
+    generator state captured at the reference's loop start; checked against the stored
+    checksum so a platform difference in the draw fails here, not as an index mismatch."""
+    import numpy as np
     import torch
-    assert torch.cuda.is_available(), 'gpu test needs a GPU'
-    import samplernn_hip
-    samplernn_hip.lib()  # raises if the .so is missing
-    return samplernn_hip
+    T = g['idx'].shape[1]
+    n = int(g['n_seqs'])
+    saved = torch.get_rng_state()
+    try:
+        torch.set_rng_state(torch.from_numpy(g['rng_state'].copy()))
+        q = torch.empty(T, n, q_levels).exponential_(1).numpy()
+    finally:
+        torch.set_rng_state(saved)
+    assert np.array_equal(q[:4], g['noise_head']) and np.array_equal(q[-4:], g['noise_tail'])
+    assert q.astype(np.float64).sum() == float(g['noise_sum'])
+    return q
+
+
+# Tolerances for the sampled TBPTT fixtures (tbptt_big / tbptt_a).  Step 0 (fresh weights)
+# is the forward + backward at the fixture's dims: every sampled gradient within
+# atol + rtol |g|.  From the first Adam update on, the trajectory is chaotic at the rounding
+# level: near-zero gradients flip sign under fp32 summation-order noise and Adam (first
+# steps ~ lr * sign(g)) moves those weights by +-lr.  make_golden.py measured the reference
+# against ITSELF (1 vs 8 threads, alt_* keys): at D = 1024 its step-2 gradients differ beyond
+# 1e-4 + 1e-3|g| at up to 1.5 % of entries (relative L2 1.8e-2, max 3.5e-4), its final
+# parameters beyond 2e-4 at 0.1 % (max 9.2e-4 = ~lr), its step-2 hidden state by 9.1e-3.
+# The later-step bounds below are those measured self-drifts with a ~3x margin.
+DRIFT = dict(grad_viol=0.05, grad_rel_l2=0.05, grad_max=2e-3,
+             param_viol=0.01, param_max=3e-3, param_rel_l2=5e-3)
+
+
+def assert_sampled_close(got, g, key, name, atol, rtol, max_viol=0.0, max_abs=None,
+                         max_rel_l2=1e-3):
+    """Compare a full tensor against a sampled fixture entry (seeded sample + L2 norm):
+    at most max_viol of the sampled entries outside atol + rtol |ref|, none beyond
+    max_abs, and the sample's relative L2 difference and the tensor's L2 norm within
+    max_rel_l2."""
+    import numpy as np
+    import recipe
+    a = np.asarray(got, dtype=np.float32).ravel()
+    idx = recipe.sample_index(a.size, name)
+    r = g['smp_%s/%s' % (key, name)]
+    d = np.abs(a[idx].astype(np.float64) - r)
+    bad = d > atol + rtol * np.abs(r)
+    msg = '%s %s: %d/%d outside %.3g + %.3g|ref|, max diff %.3g' % (
+        key, name, int(bad.sum()), d.size, atol, rtol, float(d.max()))
+    assert bad.mean() <= max_viol, msg
+    if max_abs is not None:
+        assert d.max() <= max_abs, msg
+    rn = np.sqrt((r.astype(np.float64) ** 2).sum())
+    assert np.sqrt((d * d).sum()) <= max_rel_l2 * rn + atol, msg + ' (sample relative L2)'
+    f = a.astype(np.float64)
+    l2 = float(g['l2_%s/%s' % (key, name)])
+    assert abs(np.sqrt((f * f).sum()) - l2) <= max_rel_l2 * l2 + atol, msg + ' (L2 norm)'

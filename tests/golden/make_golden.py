@@ -332,9 +332,10 @@ class _RowwisePredictor(torch.nn.Module):
 class _Adam(torch.optim.Adam):
     """torch-0.4 zero_grad semantics + capture of the clipped grads per step."""
 
-    def __init__(self, *a, **k):
+    def __init__(self, *a, on_step=None, **k):
         super().__init__(*a, **k)
         self.captured = []
+        self.on_step = on_step
 
     def zero_grad(self, set_to_none=False):
         super().zero_grad(set_to_none=False)
@@ -344,17 +345,38 @@ class _Adam(torch.optim.Adam):
         self.captured.append([p.grad.detach().clone() for g in self.param_groups
                               for p in g['params']])
         super().step()
+        if self.on_step is not None:
+            self.on_step()
         return loss
 
 
-def tbptt_goldens(name, B, T, n_steps, seed, lr=1e-3):
+def _stats(out, key, name, a):
+    """sum, L2 norm and the recipe's fixed sample of a (large) tensor."""
+    a = a.detach().numpy() if hasattr(a, 'detach') else a
+    f = a.astype(np.float64).ravel()
+    out['sum_%s/%s' % (key, name)] = np.array(f.sum())
+    out['l2_%s/%s' % (key, name)] = np.array(np.sqrt((f * f).sum()))
+    out['smp_%s/%s' % (key, name)] = a.ravel()[recipe.sample_index(f.size, name)]
+
+
+def tbptt_goldens(name, B, T, n_steps, seed, lr=1e-3, sampled=False, tag=None, alt_threads=None):
+    """3-step TBPTT trajectory through the reference's own Trainer.train (reset chunk, then
+    carried hidden state; clip + Adam).  sampled=True (the D = 1024 / configs[0] fixtures)
+    stores per tensor a sum, an L2 norm and a fixed seeded sample of >= 4096 entries for the
+    gradients of EVERY step and the final parameters, plus the hidden state after every step,
+    instead of full tensors."""
     cfg = recipe.CONFIGS[name]
     w = recipe.make_weights(cfg, seed)
     m, _ = build_ref(cfg, w)
     rp = _RowwisePredictor(m, B)
     names = [k for k, _ in rp.named_parameters()]
     params = [p for _, p in rp.named_parameters()]
-    opt = ref_optim.gradient_clipping(_Adam(params, lr=lr))
+    hidden_steps = []
+
+    def on_step():
+        hidden_steps.append([np.concatenate([r.hidden_states[rnn].numpy() for r in rp.rows], 1)
+                             for rnn in m.frame_level_rnns])
+    opt = ref_optim.gradient_clipping(_Adam(params, lr=lr, on_step=on_step))
     audio, chunks = make_chunks(cfg, B, T, n_steps, seed + 11)
     losses = []
 
@@ -375,16 +397,135 @@ def tbptt_goldens(name, B, T, n_steps, seed, lr=1e-3):
         out['cond_%d' % n] = cnd
         out['spk_%d' % n] = spk
         out['reset_%d' % n] = np.array(reset)
-    for s, grads in enumerate(opt.captured[:2]):  # step 1 = non-reset (h0 zero grad)
-        for k, g in zip(names, grads):
-            out['grad_%d/%s' % (s, k)] = g.numpy()
-    for k, p in zip(names, params):
-        out['param_final/%s' % k] = p.detach().numpy()
+    if sampled:
+        out['sampled'] = np.array(True)
+        for s, grads in enumerate(opt.captured):
+            for k, g in zip(names, grads):
+                _stats(out, 'grad_%d' % s, k, g)
+        for k, p in zip(names, params):
+            _stats(out, 'param_final', k, p)
+        for s, hs in enumerate(hidden_steps):
+            for t, h in enumerate(hs):
+                out['hidden_%d_tier%d' % (s, t)] = h
+        if alt_threads:
+            # The reference against ITSELF: the same trajectory with another thread count
+            # (MKL's GEMM blocking changes the fp32 summation order).  From the first Adam
+            # step on, gradients near zero flip sign under such rounding noise and Adam moves
+            # those weights by +-lr, so later steps drift apart; this run records how far the
+            # reference drifts from itself -- the floor any other fp32 implementation meets.
+            nt = torch.get_num_threads()
+            torch.set_num_threads(alt_threads)
+            try:
+                alt = _tbptt_run(cfg, w, B, T, n_steps, lr, seed)
+            finally:
+                torch.set_num_threads(nt)
+            a_losses, a_grads, a_params, a_hidden = alt
+            out['alt_threads'] = np.array(alt_threads)
+            out['alt_losses'] = np.array(a_losses)
+            for s, grads in enumerate(a_grads):
+                for k, g in zip(names, grads):
+                    _stats(out, 'alt_grad_%d' % s, k, g)
+            for k, p in zip(names, a_params):
+                _stats(out, 'alt_param_final', k, p)
+            for s, hs in enumerate(a_hidden):
+                for t, h in enumerate(hs):
+                    out['alt_hidden_%d_tier%d' % (s, t)] = h
+    else:
+        for s, grads in enumerate(opt.captured[:2]):  # step 1 = non-reset (h0 zero grad)
+            for k, g in zip(names, grads):
+                out['grad_%d/%s' % (s, k)] = g.numpy()
+        for k, p in zip(names, params):
+            out['param_final/%s' % k] = p.detach().numpy()
     for t, rnn in enumerate(m.frame_level_rnns):
         out['hidden_final_tier%d' % t] = np.concatenate(
             [r.hidden_states[rnn].numpy() for r in rp.rows], 1)
     print('tbptt %s losses' % name, losses)
-    save('tbptt_' + name, **out)
+    save('tbptt_' + (tag or name), **out)
+
+
+def _tbptt_run(cfg, w, B, T, n_steps, lr, seed):
+    """tbptt_goldens' trajectory again (used for the thread-count self-consistency run)."""
+    m, _ = build_ref(cfg, w)
+    rp = _RowwisePredictor(m, B)
+    params = [p for _, p in rp.named_parameters()]
+    hidden = []
+
+    def on_step():
+        hidden.append([np.concatenate([r.hidden_states[rnn].numpy() for r in rp.rows], 1)
+                       for rnn in m.frame_level_rnns])
+    opt = ref_optim.gradient_clipping(_Adam(params, lr=lr, on_step=on_step))
+    _, chunks = make_chunks(cfg, B, T, n_steps, seed + 11)
+    losses = []
+
+    def criterion(out, tgt):
+        loss = ref_nn.sequence_nll_loss_bits(out, tgt)
+        losses.append(float(loss))
+        return loss
+    data = [(torch.from_numpy(inp), torch.tensor([int(reset)] * B), torch.from_numpy(tgt),
+             torch.from_numpy(cnd), torch.from_numpy(spk)) for inp, reset, tgt, cnd, spk in chunks]
+    ref_trainer.Trainer(rp, criterion, opt, data, False, None).run(1)
+    return losses, opt.captured, [p.detach() for p in params], hidden
+
+
+def generation_long_goldens(name, n_seqs, num_cond, seed, gen_seed, tag, every=16):
+    """A long generation run (configs[2]'s model: 75 top-tier frames = 4,800 samples) with
+    the reference's multinomial noise replayed.  The noise (T x n x Q float32, ~10 MB) is
+    not stored: the fixture keeps torch's CPU generator state at loop start (the box
+    regenerates the identical draw with torch.set_rng_state + exponential_, checked against
+    the stored checksum), the full index stream, the log-probs at every `every`-th step, and
+    the near-tie statistics of the log-space draw over ALL steps."""
+    cfg = recipe.CONFIGS[name]
+    w = recipe.make_weights(cfg, seed)
+    m, _ = build_ref(cfg, w)
+    cond = recipe.synth_cond((num_cond, cfg['cond_dim']), seed + 3)
+    spk = 3 % cfg['spk_dim']
+    gen = ref_model.Generator(m, False)
+    rec = []
+    orig = m.sample_level_mlp.forward
+
+    def hooked(prev, upper):
+        o = orig(prev, upper)
+        rec.append(o.detach().clone())
+        return o
+    m.sample_level_mlp.forward = hooked
+    torch.manual_seed(gen_seed)
+    state = torch.get_rng_state()
+    devnull = open(os.devnull, 'w')
+    so = sys.stdout
+    sys.stdout = devnull
+    t0 = time.time()
+    try:
+        with torch.no_grad():
+            samples = gen(n_seqs, 0, cond, spk)
+    finally:
+        sys.stdout = so
+    t_ref = time.time() - t0
+    m.sample_level_mlp.forward = orig
+    L = recipe.lookback(cfg)
+    T = num_cond * L
+    logp = torch.cat(rec, 1).numpy()  # (n_seqs, T, Q)
+    samples = samples.numpy()
+    torch.set_rng_state(state)
+    q = torch.empty(T, n_seqs, cfg['q_levels']).exponential_(1).numpy()
+    p = np.exp(logp).astype(np.float32)
+    ratio = p.transpose(1, 0, 2) / q
+    idx = np.argmax(ratio, axis=-1).T
+    lut = ref_utils.udequantize(torch.arange(cfg['q_levels']), cfg['q_levels']).numpy()
+    assert np.array_equal(lut[idx], samples), 'noise replay does not reproduce the reference'
+    srt = np.sort(ratio, axis=-1)
+    rel = ((srt[..., -1] - srt[..., -2]) / srt[..., -1]).T      # (n_seqs, T)
+    logsp = np.argmax(logp.transpose(1, 0, 2).astype(np.float32) - np.log(q), axis=-1).T
+    n_diff = int((logsp != idx).sum())
+    steps = np.arange(0, T, every)
+    print('gen-long %s: T=%d n_seqs=%d ref %.1fs min margin %.3g, log-space draw differs at %d '
+          'of %d steps' % (name, T, n_seqs, t_ref, rel.min(), n_diff, idx.size))
+    save('genlong_' + tag, cond=cond, spk=np.array(spk), n_seqs=np.array(n_seqs),
+         weight_seed=np.array(seed), gen_seed=np.array(gen_seed),
+         rng_state=state.numpy(), noise_sum=np.array(q.astype(np.float64).sum()),
+         noise_head=q[:4].copy(), noise_tail=q[-4:].copy(),
+         idx=idx.astype(np.int16), logp_steps=steps, logp=logp[:, steps].copy(),
+         margin=rel.astype(np.float32), logspace_diff=np.array(n_diff),
+         ref_seconds=np.array(t_ref))
 
 
 def init_goldens():
@@ -460,6 +601,17 @@ def main():
         tbptt_goldens('t3', B=2, T=128, n_steps=3, seed=31)
         tbptt_goldens('t3r2wn', B=2, T=64, n_steps=3, seed=32)
         tbptt_goldens('t2', B=3, T=64, n_steps=3, seed=33)
+    if want('big4'):
+        # round 4: the measured dimensions, pinned to the reference itself
+        # configs[1]'s model at T = 1024 (reset chunk + 2 carried chunks, clip + Adam)
+        tbptt_goldens('big', B=2, T=1024, n_steps=3, seed=34, sampled=True, alt_threads=1)
+        # configs[0]: 2-tier dim 256, one speaker, T = 1024
+        tbptt_goldens('a', B=2, T=1024, n_steps=3, seed=35, sampled=True, alt_threads=1)
+        forward_goldens('a', B=2, T=1024, n_chunks=2, seed=36,
+                        keep_rows=list(range(0, 1024, 8)))
+        generation_goldens('a', n_seqs=2, num_cond=32, seed=37, gen_seed=13)
+        # configs[2]'s model: 2 rows x 75 top-tier frames = 4,800 samples
+        generation_long_goldens('big', n_seqs=2, num_cond=75, seed=38, gen_seed=14, tag='big')
     print('done in %.1fs' % (time.time() - t0))
 
 

@@ -161,4 +161,18 @@ CONFIGS = {
                     cond_dim=43, spk_dim=6, learn_h0=False),
     'big': dict(frame_sizes=[16, 4], n_rnn=1, dim=1024, q_levels=256, weight_norm=False,
                 cond_dim=43, spk_dim=6, learn_h0=True),
+    # configs[0]: 2-tier, dim 256, one speaker (train.py:201 counts speaker directories, so a
+    # single-speaker dataset gives spk_dim = 1), the train.py defaults otherwise
+    'a': dict(frame_sizes=[16], n_rnn=1, dim=256, q_levels=256, weight_norm=False,
+              cond_dim=43, spk_dim=1, learn_h0=True),
 }
+
+
+def sample_index(numel, name, k=4096):
+    """Fixed seeded subset of flat entries of a tensor (the large fixtures store these
+    entries, a sum and an L2 norm per tensor instead of the full tensor)."""
+    if numel <= k:
+        return np.arange(numel)
+    h = sum((i + 1) * ord(c) for i, c in enumerate(name)) & 0xFFFFFFFF
+    rng = np.random.Generator(np.random.PCG64(h))
+    return np.sort(rng.choice(numel, size=k, replace=False))

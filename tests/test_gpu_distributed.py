@@ -255,10 +255,11 @@ def test_dp_bf16_buckets_track_reference(hip):
         np.testing.assert_array_equal(got[0][1][k], got[1][1][k], err_msg=k)
 
 
-def _gen_worker(rank, world, port, name, dtype, q):
+def _gen_worker(rank, world, port, name, dtype, sampler, q):
     """Rank-sharded generation (model.shard_generate): each rank generates its contiguous
-    rows with the Philox noise of the global rows; the gathered batch equals the
-    single-process run's bit for bit."""
+    rows with the noise of the global rows (Philox, or the reference's torch CPU stream
+    drawn for the whole batch on every rank); the gathered batch equals the single-process
+    run's bit for bit."""
     try:
         sys.path[:0] = [HERE, os.path.join(HERE, 'golden'),
                         os.path.join(os.path.dirname(HERE),
@@ -278,10 +279,12 @@ def _gen_worker(rank, world, port, name, dtype, q):
         n, n_cond = 16, 2
         cond = recipe.synth_cond((n, n_cond, cfg['cond_dim']), 6)
         spk = np.arange(n) % cfg['spk_dim']
-        out = M.shard_generate(M.Generator(m, True), n, cond, spk, 99)
+        torch.manual_seed(7)
+        out = M.shard_generate(M.Generator(m, True), n, cond, spk, 99, sampler=sampler)
         full = None
         if rank == 0:
-            full = M.Generator(m, True)(n, 0, cond, spk, sampler='philox', seed=99)
+            torch.manual_seed(7)
+            full = M.Generator(m, True)(n, 0, cond, spk, sampler=sampler, seed=99)
             full = full.numpy()
         q.put((rank, out.numpy(), full, None))
         D.barrier()
@@ -293,9 +296,10 @@ def _gen_worker(rank, world, port, name, dtype, q):
         raise
 
 
-@pytest.mark.parametrize('name,dtype', [('t3', 'fp32'), ('big', 'bf16')])
-def test_sharded_generation_reproduces_single_process(hip, name, dtype):
-    got = _spawn(_gen_worker, (name, dtype))
+@pytest.mark.parametrize('name,dtype,sampler', [('t3', 'fp32', 'philox'), ('big', 'bf16', 'philox'),
+                                                ('t3', 'fp32', 'torch'), ('big', 'fp32', 'torch')])
+def test_sharded_generation_reproduces_single_process(hip, name, dtype, sampler):
+    got = _spawn(_gen_worker, (name, dtype, sampler))
     full = got[0][1]
     for rank in (0, 1):
         assert np.array_equal(got[rank][0], full), rank

@@ -26,7 +26,7 @@ def build(cfg, weights, dtype=torch.float32):
     return m.to(DEV), pred.to(DEV)
 
 
-@pytest.mark.parametrize('name', ['t2', 't3', 't3r2wn', 't4la', 't3_20_4', 'big'])
+@pytest.mark.parametrize('name', ['t2', 't3', 't3r2wn', 't4la', 't3_20_4', 'big', 'a'])
 def test_forward_golden(hip, name):
     g = golden('fwd_' + name)
     cfg = recipe.CONFIGS[name]
@@ -48,7 +48,7 @@ def test_forward_golden(hip, name):
                                            g['hidden_%d_tier%d' % (n, t)], atol=2e-5, rtol=0)
 
 
-@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn', 'big'])
+@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn', 'big', 'a'])
 @pytest.mark.parametrize('graph,persistent', [(True, True), (False, True), (True, False),
                                               (False, False)])
 def test_generation_golden(hip, name, graph, persistent):
