@@ -252,20 +252,38 @@ def kernels_block(r, dtype_peak):
     return ks
 
 
+def _pmc_file(pattern):
+    """(bytes, source) from the newest committed rocprofv3 PMC pass matching pattern
+    (profiles/r*_pmc_...txt: `avg_step_bytes` = 2 x FETCH_SIZE + WRITE_SIZE per step, gfx950
+    FETCH correction per MI355X_MICROARCH.md) whose `csrc_hash` line equals the hash of the
+    HIP sources this run's library is built from (samplernn_hip.csrc_hash); (None, reason)
+    when no pass was taken on these kernels."""
+    import glob
+    import samplernn_hip as H
+    want = H.csrc_hash()
+    seen = []
+    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', pattern)), reverse=True):
+        b, h = None, None
+        try:
+            for line in open(path):
+                f = line.split()
+                if len(f) == 2 and f[0] == 'avg_step_bytes':
+                    b = int(f[1])
+                elif len(f) == 2 and f[0] == 'csrc_hash':
+                    h = f[1]
+        except (OSError, ValueError):
+            continue
+        name = os.path.basename(path)
+        if b is not None and h == want:
+            return b, '%s (csrc %s)' % (name, h)
+        seen.append('%s at csrc %s' % (name, h))
+    return None, 'no PMC pass at csrc %s%s' % (want, (' (stale: %s)' % ', '.join(seen))
+                                              if seen else '')
+
+
 def pmc_traffic(site, rows):
-    """HBM bytes per step of a probed site from the round's committed rocprofv3 PMC passes
-    (profiles/r03_pmc_<site>_b<rows>.txt, `avg_step_bytes` = (2 x FETCH_SIZE + WRITE_SIZE) over
-    the site's launches of one step, gfx950 FETCH correction per MI355X_MICROARCH.md); None
-    when no pass was committed for this site and batch."""
-    path = os.path.join(ROOT, 'profiles', 'r03_pmc_%s_b%d.txt' % (site, rows))
-    try:
-        for line in open(path):
-            f = line.split()
-            if len(f) == 2 and f[0] == 'avg_step_bytes':
-                return int(f[1])
-    except (OSError, ValueError):
-        pass
-    return None
+    """HBM bytes per step of a probed site (tools/pmc_site.sh), attributed to HEAD's kernels."""
+    return _pmc_file('r*_pmc_%s_b%d.txt' % (site, rows))
 
 
 def gru_sweep_roofline(dev, B=128, D=1024, Fr=64, reps=5):
@@ -353,18 +371,11 @@ def run_gen(dev, n_seqs, n_cond, dtype, frame_sizes=(16, 4), cond_dim=43, row0=0
     return time.perf_counter() - t0, w_step
 
 
-def gen_traffic(path=os.path.join(ROOT, 'profiles', 'r03_pmc_gen.txt')):
+def gen_traffic():
     """HBM bytes per generation step of the bf16 loop (B = 128, D = 1024, FS = [16, 4]) from the
     committed rocprofv3 PMC passes (tools/pmc_gen.py: FETCH_SIZE kB x 2 + WRITE_SIZE kB over
-    every dispatch of the loop's kernels / samples generated)."""
-    try:
-        for line in open(path):
-            m = line.split()
-            if len(m) == 2 and m[0] == 'avg_step_bytes':
-                return int(m[1])
-    except (OSError, ValueError):
-        pass
-    return None
+    every dispatch of the loop's kernels / samples generated), attributed to HEAD's kernels."""
+    return _pmc_file('r*_pmc_gen.txt')
 
 
 def cpu_baseline(seconds_budget=30.0):
@@ -464,7 +475,7 @@ def main():
     roof = None
     if dom:
         roof = dict(ks[dom])
-        roof['traffic'] = pmc_traffic(dom, rows)
+        roof['traffic'], roof['traffic_source'] = pmc_traffic(dom, rows)
         roof['kernel'] = '%s; %.3f ms per step (%d launches; HIP events on the launching stream '\
                          'around each launch, over eager steps of the same run right after the '\
                          'timed graph replays)' % (SITE_NOTES.get(dom, dom), ks[dom]['ms_per_step'],
@@ -507,7 +518,7 @@ def main():
         import samplernn_hip as H
         rows_pg = H.gen_persistent_rows(gdt, args.gen_seqs, 1024, 16)
         log('gen %s: %.3f s, %.0f samples/s (%.1fx realtime)' % (dname, t, gs, gs / 16000))
-        return {'value': round(gs, 1), 'unit': 'samples/s', 'x_realtime': round(gs / 16000, 1),
+        line = {'value': round(gs, 1), 'unit': 'samples/s', 'x_realtime': round(gs / 16000, 1),
                 'x_realtime_per_gpu': round(gs / 16000 / N, 1), 'dtype': dname,
                 'seconds': round(t, 3), 'steps_per_s': round(steps_per_s, 1),
                 'us_per_step': round(1e6 / steps_per_s, 2),
@@ -523,9 +534,10 @@ def main():
                              'peak': MI355X_HBM_TBS * 1000, 'unit': 'GB/s',
                              'frac': round(bytes_step * steps_per_s / 1e9 /
                                            (MI355X_HBM_TBS * 1000), 4),
-                             'traffic': gen_traffic() if (dname == 'bf16' and tuple(frame_sizes)
-                                                          == (16, 4) and args.gen_seqs == 128)
-                                        else None}}
+                             'traffic': None, 'traffic_source': 'no PMC pass for this line'}}
+        if dname == 'bf16' and tuple(frame_sizes) == (16, 4) and args.gen_seqs == 128:
+            line['roofline']['traffic'], line['roofline']['traffic_source'] = gen_traffic()
+        return line
 
     gen = gen_fp32 = gen_e = None
     if not args.no_gen:

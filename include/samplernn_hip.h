@@ -202,6 +202,20 @@ int srnn_mlp_dtab3(int dtype, const void* da, int64_t ldda, const int64_t* x, in
  * returns 1 if a GEMM did since (host state; also clears a request no GEMM took).        */
 int srnn_gemm_amax_next(unsigned* amax);
 int srnn_gemm_amax_taken(void);
+/* srnn_gemm_amax_next, and the same GEMM also writes a column-blocked copy of its bf16
+ * output into blk[N / 4][M][4] (M x N bf16, caller-allocated); srnn_gemm_amax_taken()
+ * then returns 2.  The dTab scatter's operand layout (srnn_mlp_dtab4).                   */
+int srnn_gemm_amax_blk_next(unsigned* amax, void* blk);
+/* srnn_mlp_dtab3 with blk (device, may be NULL): the column-blocked copy of da
+ * (blk[D / 4][B * Tlen][4], srnn_gemm_amax_blk_next) the packed form reads instead of da
+ * (whole 128-B lines per load).  Same outputs bit for bit.  A sample histogram skewed past
+ * the packed form's precision bound (one value at > 65,536 positions) makes the exact
+ * 2^-40 form run instead; a non-finite da makes dTab and colsum NaN.  Replaces
+ * model.py:311-320's backward like srnn_mlp_dtab.                                         */
+int srnn_mlp_dtab4(int dtype, const void* da, int64_t ldda, const int64_t* x, int64_t ldx,
+                   int xoff, int B, int Tlen, void* dtab_out, int out_dtype, int D, int FS0, int Q,
+                   void* work, size_t work_bytes, float* colsum, int* colsum_done,
+                   const unsigned* amax_in, const void* blk, void* stream);
 /* Number of GEMMs srnn_gemm / srnn_gemm_bits handed to hipBLASLt so far in this process:
  * large plain bf16 problems (alpha, per-column bias, ReLU, beta 0, no mask; M N >= 4 Mi,
  * 2 M N K >= 2^33) run as the ROCm library GEMM (SRNN_BLASLT=0: the library's own gemm3

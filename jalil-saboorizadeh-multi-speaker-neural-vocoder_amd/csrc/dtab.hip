@@ -134,15 +134,22 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_fx_kernel(
 // bottom tier's upsampling (nn.py:33-43) -- from the same loaded rows, in fixed point.
 typedef unsigned dt_u32x4 __attribute__((ext_vector_type(4)));
 
+struct DtabStat;
+__device__ bool dtab_pk_declines(const DtabStat* st, const unsigned* amax_in, int* red);
+
 template <typename T, typename TO, bool DIRECT>
 __global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
     const T* __restrict__ da, int64_t ldda, const int64_t* __restrict__ x, int64_t ldx, int xoff,
     int Tlen, int B, int nb, int nrb, unsigned long long* __restrict__ fx, TO* __restrict__ out,
-    float* __restrict__ colsum, int D, int Q) {
+    float* __restrict__ colsum, int D, int Q, const DtabStat* __restrict__ gate,
+    const unsigned* __restrict__ gate_amax) {
     constexpr int CW = 4, FS = 16;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [Q][CW][FS]
     const int tid = threadIdx.x, lane = tid & 63;
+    // gate: the fallback behind the packed form (same statistics): runs only when that one
+    // declined (sample-value skew beyond its precision bound)
+    if (gate && !dtab_pk_declines(gate, gate_amax, reinterpret_cast<int*>(smem))) return;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nsl = gridDim.x / nrb;
     int slice, rb;
@@ -291,6 +298,31 @@ struct DtabStat {
     int count[256];                // positions per sample value q over the batch's windows
 };
 
+// Precision bound of the packed form: a term's rounding error is below 2^-(e+1) <=
+// amax * cmax / 2^31, so with cmax <= 2^16 it stays under amax * 2^-15 -- below the bf16
+// half-ulp (2^-9 relative) of every term of magnitude >= amax * 2^-6.  A histogram more
+// skewed than that (long silences at large B: one sample value at >64 Ki positions) makes
+// small-magnitude entries lose relative precision, so the exact 2^-40 form takes over.
+#define DTAB_PK_CMAX 65536
+
+// Workgroup-wide: the statistics' max count (red: 4 ints of LDS scratch, all threads call)
+__device__ __forceinline__ int dtab_cmax(const DtabStat* st, int* red) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    int cm = tid < 256 ? st->count[tid] : 0;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) cm = max(cm, __shfl_xor(cm, o));
+    if (tid < 256 && lane == 0) red[tid >> 6] = cm;
+    __syncthreads();
+    const int r = max(max(red[0], red[1]), max(red[2], red[3]));
+    __syncthreads();
+    return r;
+}
+
+__device__ bool dtab_pk_declines(const DtabStat* st, const unsigned* amax_in, int* red) {
+    const float amax = __uint_as_float(amax_in ? *amax_in : st->amax_bits);
+    return dtab_cmax(st, red) > DTAB_PK_CMAX && amax <= 3.402823466e38f;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void dtab_prep_kernel(const T* __restrict__ da, int64_t ldda,
                                                         int64_t nrows, int D,
@@ -364,11 +396,16 @@ __global__ __launch_bounds__(256) void dtab_prep_kernel(const T* __restrict__ da
 // when its batch comes up).  A batch of 16 atomics takes ~0.7 us of the CU's LDS pipeline
 // with 16 waves resident, less than an HBM load's latency under load, so a one-batch-ahead
 // load left the waves waiting on vmcnt between batches.
-template <typename T, int PD = 1>
+// BLK: da read from its column-blocked copy blk[D / 4][B * Tlen][4] (written by the da GEMM's
+// epilogue, gemm3.hip): a lane's 4-B pair is then part of one 128-B line per half-wave (16
+// consecutive rows x the slice's 4 columns), where the row-major da made one load
+// instruction touch 32 lines for 8 B each -- which cut the LDS atomic issue rate that bounds
+// this kernel from ~9.8 to ~6.3 per clock (tools/lds_atomic_probe4.hip).
+template <typename T, int PD = 1, bool BLK = false>
 __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
     const T* __restrict__ da, int64_t ldda, const int64_t* __restrict__ x, int64_t ldx, int xoff,
     int Tlen, int B, const DtabStat* __restrict__ st, const unsigned* __restrict__ amax_in,
-    bf16* __restrict__ out, float* __restrict__ colsum, int D, int Q) {
+    bf16* __restrict__ out, float* __restrict__ colsum, int D, int Q, const T* __restrict__ blk) {
     constexpr int CW = 4, FS = 16;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [Q][2][FS]
@@ -391,15 +428,20 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
     unsigned char* strip = reinterpret_cast<unsigned char*>(red + 4) + wave * 2 * WPB;
     for (int i = tid; i < nacc + CW * FS; i += DTAB_NT) acc[i] = 0ull;
     // ---- the scale: every workgroup derives the same e from the same statistics
-    {
-        int cm = tid < 256 ? st->count[tid] : 0;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) cm = max(cm, __shfl_xor(cm, o));
-        if (tid < 256 && lane == 0) red[tid >> 6] = cm;
-    }
-    __syncthreads();
-    const int cmax = max(max(red[0], red[1]), max(red[2], red[3]));
+    const int cmax = dtab_cmax(st, red);
     const float amax = __uint_as_float(amax_in ? *amax_in : st->amax_bits);
+    if (!(amax <= 3.402823466e38f)) {
+        // a non-finite gradient (NaN / inf in da): poison this slice's dTab and column sums
+        // instead of converting NaN to integers (the reference's NaN propagates likewise)
+        const float qn = __builtin_nanf("");
+        for (int i = tid; i < Q * FS * CW; i += DTAB_NT) {
+            const int cc = i % CW, qk = i / CW;
+            out[(int64_t)qk * D + c0 + cc] = __float2bfloat16(qn);
+        }
+        if (colsum && tid < CW * FS) colsum[(int64_t)(tid % FS) * D + c0 + tid / FS] = qn;
+        return;
+    }
+    if (cmax > DTAB_PK_CMAX) return;               // the exact form runs instead (gated)
     int e = 0;
     if (amax > 0.f && cmax > 0) {
         int ex;
@@ -421,11 +463,12 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
     for (int b2 = 2 * wave; b2 < B; b2 += 2 * (DTAB_NT / 64)) {
         const int b = b2 + h;
         const bool rv = b < B;
-        const T* drow = da + (int64_t)(rv ? b : b2) * Tlen * ldda + cA;
+        const T* drow = BLK ? blk + ((int64_t)(c0 >> 2) * B * Tlen + (int64_t)(rv ? b : b2) * Tlen) * 4 + 2 * p
+                            : da + (int64_t)(rv ? b : b2) * Tlen * ldda + cA;
         auto raw = [&](int pbase) -> uint32_t {
             const int t = pbase + li;
             if (!(rv && t < Tlen)) return 0u;                 // zero bits: a zero pair
-            return *reinterpret_cast<const uint32_t*>(drow + (int64_t)t * ldda);
+            return *reinterpret_cast<const uint32_t*>(drow + (int64_t)t * (BLK ? 4 : ldda));
         };
         auto conv = [&](uint32_t u) -> unsigned long long {
             const float gA = to_f(*reinterpret_cast<const T*>(&u));
@@ -584,7 +627,8 @@ static int pk_lds_bytes(int Q, int Tlen) {
 template <typename T, typename TO, bool DIRECT>
 static int launch_pos(const void* da, int64_t ldda, const int64_t* x, int64_t ldx, int xoff, int B,
                       int Tlen, unsigned long long* fx, void* out, float* colsum, int D, int Q,
-                      int nb, int nrb, hipStream_t s) {
+                      int nb, int nrb, hipStream_t s, const DtabStat* gate = nullptr,
+                      const unsigned* gate_amax = nullptr) {
     const int lds = pos_lds_bytes(Q, Tlen);
     const int nslices = cdiv(D, 4);
     auto k = dtab_pos_kernel<T, TO, DIRECT>;
@@ -595,7 +639,7 @@ static int launch_pos(const void* da, int64_t ldda, const int64_t* x, int64_t ld
         attr = true;
     }
     hipLaunchKernelGGL(k, dim3(nslices * nrb), dim3(DTAB_NT), lds, s, (const T*)da, ldda, x, ldx,
-                       xoff, Tlen, B, nb, nrb, fx, (TO*)out, colsum, D, Q);
+                       xoff, Tlen, B, nb, nrb, fx, (TO*)out, colsum, D, Q, gate, gate_amax);
     SRNN_LAUNCH_CHECK();
     return 0;
 }
@@ -622,11 +666,11 @@ static int dtab_pos(const void* da, int64_t ldda, const int64_t* x, int64_t ldx,
 // dtab_out (Q, FS0, D) in out_dtype; work: >= Q*FS0*D*8 bytes of device scratch.
 // colsum (optional, (FS0 * D) fp32): sum over batch rows of da rows t = j (mod FS0) at
 // [j * D + c]; *colsum_done (host) = 1 when it was written (the direct position-major path)
-extern "C" int srnn_mlp_dtab3(int dtype, const void* da, int64_t ldda, const int64_t* x,
+extern "C" int srnn_mlp_dtab4(int dtype, const void* da, int64_t ldda, const int64_t* x,
                               int64_t ldx, int xoff, int B, int Tlen, void* dtab_out,
                               int out_dtype, int D, int FS0, int Q, void* work, size_t work_bytes,
                               float* colsum, int* colsum_done, const unsigned* amax_in,
-                              void* stream) {
+                              const void* blk, void* stream) {
     SRNN_REQUIRE(Q <= 256, "dtab: q_levels must be <= 256 (byte indices)");
     const int64_t n = (int64_t)Q * FS0 * D;
     SRNN_REQUIRE(work && work_bytes >= (size_t)n * 8, "dtab: workspace too small");
@@ -649,21 +693,31 @@ extern "C" int srnn_mlp_dtab3(int dtype, const void* da, int64_t ldda, const int
         SRNN_LAUNCH_CHECK();
         static bool attr = false;
         if (!attr) {
-            SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_pk_kernel<bf16, 1>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               160 * 1024));
-            SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)dtab_pk_kernel<bf16, 4>,
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               160 * 1024));
+            for (const void* k : {(const void*)dtab_pk_kernel<bf16, 1>,
+                                  (const void*)dtab_pk_kernel<bf16, 4>,
+                                  (const void*)dtab_pk_kernel<bf16, 4, true>})
+                SRNN_CHECK_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                   160 * 1024));
             attr = true;
         }
-        // SRNN_DTAB_PD=1: the one-batch-ahead da load (default: four batches ahead)
+        // SRNN_DTAB_PD=1: the one-batch-ahead da load (default: four batches ahead);
+        // blk: the column-blocked copy of da (SRNN_DTAB_BLK=0 reads the row-major da)
         const char* pde = getenv("SRNN_DTAB_PD");
-        auto pk = (pde && pde[0] == '1') ? dtab_pk_kernel<bf16, 1> : dtab_pk_kernel<bf16, 4>;
+        const bool useblk = blk && !getenv_off("SRNN_DTAB_BLK");
+        auto pk = useblk ? dtab_pk_kernel<bf16, 4, true>
+                : (pde && pde[0] == '1') ? dtab_pk_kernel<bf16, 1> : dtab_pk_kernel<bf16, 4>;
         hipLaunchKernelGGL(pk, dim3(cdiv(D, 4)), dim3(DTAB_NT),
                            pk_lds_bytes(Q, Tlen), s, (const bf16*)da, ldda, x, ldx, xoff, Tlen, B,
-                           st, amax_in, (bf16*)dtab_out, colsum, D, Q);
+                           st, amax_in, (bf16*)dtab_out, colsum, D, Q, (const bf16*)blk);
         SRNN_LAUNCH_CHECK();
+        // the exact form behind it, gated on the same statistics: all of its workgroups
+        // return at once unless the packed form declined (a skewed sample histogram)
+        if (pos_lds_bytes(Q, Tlen) <= 160 * 1024) {
+            const int rc = launch_pos<bf16, bf16, true>(da, ldda, x, ldx, xoff, B, Tlen, nullptr,
+                                                        dtab_out, colsum, D, Q, B, 1, s, st,
+                                                        amax_in);
+            if (rc) return rc;
+        }
         if (colsum && colsum_done) *colsum_done = 1;
         return 0;
     }
@@ -708,6 +762,15 @@ convert:
                            (bf16*)dtab_out, n);
     SRNN_LAUNCH_CHECK();
     return 0;
+}
+
+extern "C" int srnn_mlp_dtab3(int dtype, const void* da, int64_t ldda, const int64_t* x,
+                              int64_t ldx, int xoff, int B, int Tlen, void* dtab_out,
+                              int out_dtype, int D, int FS0, int Q, void* work, size_t work_bytes,
+                              float* colsum, int* colsum_done, const unsigned* amax_in,
+                              void* stream) {
+    return srnn_mlp_dtab4(dtype, da, ldda, x, ldx, xoff, B, Tlen, dtab_out, out_dtype, D, FS0, Q,
+                          work, work_bytes, colsum, colsum_done, amax_in, nullptr, stream);
 }
 
 extern "C" int srnn_mlp_dtab2(int dtype, const void* da, int64_t ldda, const int64_t* x,

@@ -50,6 +50,9 @@ struct Gemm3Args {
     // optional: max |C| over the stored bf16 values, as float bits, atomicMax-ed here (the
     // packed dTab scatter's scale, dtab.hip); the word must be zero before the GEMM
     unsigned* amax;
+    // optional (with amax): a column-blocked copy of the bf16 output, [N / 4][M][4] -- the
+    // dTab scatter's operand (dtab.hip: one load instruction then reads whole lines)
+    bf16* blk;
 };
 
 namespace g3 {
@@ -312,6 +315,17 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
                     }
                     *reinterpret_cast<uint4*>(Cp + (int64_t)row * g.ldc + cbase + 32 * jp + coff) =
                         make_uint4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
+                    if constexpr (AMX) {
+                        if (g.blk) {
+                            // the same 8 columns as two 4-column blocks: 16 lanes (rows
+                            // rbase .. + 15) of a block write one contiguous 128-B line
+                            const int cb = (cbase + 32 * jp + coff) >> 2;
+                            bf16* bp = g.blk + ((int64_t)cb * g.M + row) * 4;
+                            *reinterpret_cast<uint2*>(bp) = make_uint2(pk[0][0], pk[0][1]);
+                            *reinterpret_cast<uint2*>(bp + (int64_t)g.M * 4) =
+                                make_uint2(pk[1][0], pk[1][1]);
+                        }
+                    }
                 }
             }
             if (mbo) {
@@ -390,7 +404,7 @@ __device__ __forceinline__ int g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8]
                                            int n0, int wm, int wn, int lane, int kb) {
     if constexpr (AMX) {
         g3_epilogue_t<TO, SW, false, false, true>(g, acc, m0, n0, wm, wn, lane, kb);
-        return 16;
+        return g.blk ? 48 : 16;                    // + the blocked copy's 2 stores per store
     }
     if constexpr (MB) {
         // the bit-mask kernels (their own instantiation: the plain epilogue keeps its registers)
@@ -790,6 +804,7 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
         char* nimg = smem + ((s + 1) & 1) * g3p::SLOT;
         if (SW && epi == 16) g3_wait_vm<16>();
         else if (SW && epi == 18) g3_wait_vm<18>();                        // + mask bits
+        else if (SW && epi == 48) g3_wait_vm<48>();                        // + blocked copy
         else if (SW && epi) g3_wait_vm<32>();
         else g3_wait_vm<0>();
         epi = 0;
@@ -1270,11 +1285,23 @@ static int& g3_amax_taken() {
     static int t = 0;
     return t;
 }
+static bf16*& g3_blk_pending() {
+    static bf16* p = nullptr;
+    return p;
+}
 
 int srnn_gemm_amax_pending() { return g3_amax_pending() != nullptr; }
 
 extern "C" int srnn_gemm_amax_next(unsigned* amax) {
     g3_amax_pending() = amax;
+    g3_blk_pending() = nullptr;
+    g3_amax_taken() = 0;
+    return 0;
+}
+
+extern "C" int srnn_gemm_amax_blk_next(unsigned* amax, void* blk) {
+    g3_amax_pending() = amax;
+    g3_blk_pending() = (bf16*)blk;
     g3_amax_taken() = 0;
     return 0;
 }
@@ -1282,6 +1309,7 @@ extern "C" int srnn_gemm_amax_next(unsigned* amax) {
 extern "C" int srnn_gemm_amax_taken(void) {
     const int t = g3_amax_taken();
     g3_amax_pending() = nullptr;
+    g3_blk_pending() = nullptr;
     g3_amax_taken() = 0;
     return t;
 }
@@ -1314,6 +1342,7 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     g.diag = env_flag("SRNN_G3DIAG", 0);
     g.mbi = mbi; g.ldmbi = ldmbi; g.mbo = mbo; g.ldmbo = ldmbo;
     g.amax = nullptr;
+    g.blk = nullptr;
     const int tiles = (M / g3::BM) * (N / g3::BN);
     const bool plain = beta == 0.f && !bias && !relu && !mask && !mbi && !mbo &&
                        out_dtype == SRNN_F32;
@@ -1352,8 +1381,11 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     if (g3_amax_pending() && beta == 0.f && !mbi && !mbo && (kca || kcb) &&
         K % g3p::BK == 0 && g3_mode() <= 2 && (g3_mode() != 0)) {
         g.amax = g3_amax_pending();
+        // the blocked copy needs whole 4-column blocks (N % 256 == 0 holds here)
+        g.blk = g3_blk_pending();
         g3_amax_pending() = nullptr;
-        g3_amax_taken() = 1;
+        g3_blk_pending() = nullptr;
+        g3_amax_taken() = g.blk ? 2 : 1;
     }
     return launch3_layout<bf16, true>(g, kca, kcb, s);
 }

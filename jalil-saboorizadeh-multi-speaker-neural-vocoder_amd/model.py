@@ -746,10 +746,15 @@ def mlp_backward(ctx, dlogp, nll=None):
     # d(upper) in upper's dtype: bf16 when the bottom tier hands the MLP a bf16 upper.  A
     # bf16 da1 also gets max |da1| from the GEMM's epilogue (the packed dTab scatter's
     # scale), so the scatter needs no pass of its own over da1
-    amax = None
+    amax = blk = None
     if ctx.udt == torch.bfloat16:
         amax = torch.zeros(1, device=dev, dtype=torch.int32)
-        H.lib().call('srnn_gemm_amax_next', H.ptr(amax))
+        if FS0 == 16 and D % 256 == 0 and os.environ.get('SRNN_DTAB_BLK', '1') != '0':
+            # ... and a column-blocked copy [D/4][M][4] of da1, the scatter's operand
+            blk = torch.empty((D // 4, M, 4), device=dev, dtype=torch.bfloat16)
+            H.lib().call('srnn_gemm_amax_blk_next', H.ptr(amax), H.ptr(blk))
+        else:
+            H.lib().call('srnn_gemm_amax_next', H.ptr(amax))
     Wh, tB = (W_t[0], True) if W_t is not None else (W_hid, False)
     ev = H.roof_begin()
     if m1 is not None:
@@ -757,8 +762,12 @@ def mlp_backward(ctx, dlogp, nll=None):
     else:
         da1 = H.gemm(da2, Wh, transB=tB, mask=a1, out_dtype=ctx.udt)          # (M, D)
     H.roof_end('mlp_da1_gemm', ev, 2.0 * M * D * D)
-    if amax is not None and not H.lib().dll.srnn_gemm_amax_taken():
-        amax = None
+    if amax is not None:
+        taken = H.lib().dll.srnn_gemm_amax_taken()
+        if taken != 2:
+            blk = None
+        if not taken:
+            amax = None
     # folded embedding . conv backward: dTab[q][k][:] += da1[t] for x_{t+k} = q
     dtabT = torch.empty((Q, FS0 * D), device=dev, dtype=T)
     work = torch.empty(Q * FS0 * D, device=dev, dtype=torch.int64)
@@ -767,9 +776,10 @@ def mlp_backward(ctx, dlogp, nll=None):
     colsum = torch.empty(FS0 * D, device=dev, dtype=torch.float32)
     done = ctypes.c_int(0)
     ev = H.roof_begin()
-    H.lib().call('srnn_mlp_dtab3', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.stride(0), 0, B,
+    H.lib().call('srnn_mlp_dtab4', H.dcode(da1), H.ptr(da1), D, H.ptr(x), x.stride(0), 0, B,
                  Tl, H.ptr(dtabT), H.dcode(T), D, FS0, Q, H.ptr(work), work.numel() * 8,
-                 H.ptr(colsum), ctypes.byref(done), H.ptr(amax), st())
+                 H.ptr(colsum), ctypes.byref(done), H.ptr(amax), H.ptr(blk), st())
+    blk = None
     # algorithmic bytes: da1 and the index window read once, dTab^T and the column sums
     # written once
     H.roof_end('dtab_scatter', ev, B * Tl * D * da1.element_size() +

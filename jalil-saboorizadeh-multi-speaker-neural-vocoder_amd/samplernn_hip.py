@@ -52,7 +52,10 @@ _SIGS = {
                        ctypes.POINTER(_I), _P],
     'srnn_mlp_dtab3': [_I, _P, _L, _P, _L, _I, _I, _I, _P, _I, _I, _I, _I, _P, _SZ, _P,
                        ctypes.POINTER(_I), _P, _P],
+    'srnn_mlp_dtab4': [_I, _P, _L, _P, _L, _I, _I, _I, _P, _I, _I, _I, _I, _P, _SZ, _P,
+                       ctypes.POINTER(_I), _P, _P, _P],
     'srnn_gemm_amax_next': [_P],
+    'srnn_gemm_amax_blk_next': [_P, _P],
     'srnn_logsoftmax_nll': [_P, _L, _P, _L, _I, _L, _I, _P, _P, _L, _P, _I, _L, _F, _P],
     'srnn_logsoftmax_bwd': [_P, _L, _P, _L, _L, _I, _P, _I, _L, _P],
     'srnn_nll_fwd': [_P, _L, _P, _L, _I, _L, _P, _P],
@@ -363,6 +366,26 @@ def gru_seq_supported(dtype, B, D):
 
 
 # ------------------------------------------------------------------ helpers
+def csrc_hash():
+    """Content hash of the HIP sources the library is built from (csrc/*.hip, *.hpp, *.h,
+    *.cpp and the C-ABI header): 16 hex digits.  Profiles record it, so a committed counter
+    pass is only attributed to the kernels it measured (bench.py's roofline.traffic)."""
+    import hashlib
+    here = os.path.dirname(os.path.abspath(__file__))
+    csrc = os.path.join(here, 'csrc')
+    files = sorted(f for f in os.listdir(csrc) if f.endswith(('.hip', '.hpp', '.h', '.cpp')))
+    h = hashlib.sha256()
+    for f in files:
+        h.update(f.encode())
+        with open(os.path.join(csrc, f), 'rb') as fh:
+            h.update(fh.read())
+    hdr = os.path.join(os.path.dirname(here), 'include', 'samplernn_hip.h')
+    if os.path.exists(hdr):
+        with open(hdr, 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 def ptr(t):
     """Device/host pointer of a tensor (None -> NULL).  A plain int: ctypes converts it for
     c_void_p arguments and struct fields without building an object per call."""

@@ -80,33 +80,36 @@ class Trainer(object):
         self.graph_steps = 0        # steps replayed from a graph (tests, bench.py)
         self._no_graph = set()      # step kinds whose capture failed
 
+    # ---- plugin schedule (trainer/__init__.py:28-60).  One min-heap per unit ('iteration',
+    # 'epoch', 'batch', 'update') of (next due time, registration order within the unit,
+    # plugin): a plugin first fires when the unit's clock reaches its interval, and after
+    # firing at time t it is due again at t + interval (of its LAST trigger for that unit);
+    # plugins due at the same time fire in registration order.  The lists stay reachable as
+    # self.plugin_queues, as in the reference.
+    @staticmethod
+    def _triggers(plugin):
+        ti = plugin.trigger_interval
+        return ti if isinstance(ti, list) else [ti]
+
     def register_plugin(self, plugin):
         plugin.register(self)
-        intervals = plugin.trigger_interval
-        if not isinstance(intervals, list):
-            intervals = [intervals]
-        for (duration, unit) in intervals:
-            queue = self.plugin_queues[unit]
-            queue.append((duration, len(queue), plugin))
+        for every, unit in self._triggers(plugin):
+            heap = self.plugin_queues[unit]
+            heapq.heappush(heap, (every, len(heap), plugin))
 
     def call_plugins(self, queue_name, time, *args):
-        args = (time,) + args
-        queue = self.plugin_queues[queue_name]
-        if len(queue) == 0:
-            return
-        while queue[0][0] <= time:
-            plugin = queue[0][2]
-            getattr(plugin, queue_name)(*args)
-            for trigger in plugin.trigger_interval:
-                if trigger[1] == queue_name:
-                    interval = trigger[0]
-            new_item = (time + interval, queue[0][1], plugin)
-            heapq.heappushpop(queue, new_item)
+        heap = self.plugin_queues[queue_name]
+        while heap and heap[0][0] <= time:
+            _, order, plugin = heap[0]
+            getattr(plugin, queue_name)(time, *args)
+            every = [n for n, unit in self._triggers(plugin) if unit == queue_name][-1]
+            heapq.heapreplace(heap, (time + every, order, plugin))
 
     def run(self, epochs=1):
-        for q in self.plugin_queues.values():
-            heapq.heapify(q)
-        for self.epochs in range(self.epochs + 1, self.epochs + int(epochs) + 1):
+        for heap in self.plugin_queues.values():
+            heapq.heapify(heap)        # (a no-op: registration keeps each list a heap)
+        first = self.epochs + 1
+        for self.epochs in range(first, first + int(epochs)):
             self.train()
             if self.scheduler is not None:
                 self.scheduler.step()

@@ -528,6 +528,27 @@ def generation_long_goldens(name, n_seqs, num_cond, seed, gen_seed, tag, every=1
          ref_seconds=np.array(t_ref))
 
 
+from make_golden_plugins import RecPlugin as _RecPlugin, PLUGIN_TRIGGERS  # noqa: E402
+
+
+def plugin_order_goldens():
+    """The reference Trainer's plugin schedule (trainer/__init__.py:28-50): the order in which
+    plugins with various intervals/units fire over 12 iterations and 3 epochs."""
+    log = []
+    tr = ref_trainer.Trainer(None, None, None, [], False, None)
+    for i, trig in enumerate(PLUGIN_TRIGGERS):
+        tr.register_plugin(_RecPlugin(i, trig, log))
+    for q in tr.plugin_queues.values():
+        __import__('heapq').heapify(q)
+    for it in range(1, 13):
+        tr.call_plugins('batch', it)
+        tr.call_plugins('iteration', it)
+        tr.call_plugins('update', it)
+        if it % 4 == 0:
+            tr.call_plugins('epoch', it // 4)
+    save('plugin_order', log=np.array(log, dtype=np.int64))
+
+
 def init_goldens():
     """a13: parameter init recipe (RNG consumption order) -> checksums."""
     out = {}
@@ -574,6 +595,8 @@ def main():
         ulaw_goldens(exhaustive=not a.skip_exhaustive)
     if want('init'):
         init_goldens()
+    if want('plugins'):
+        plugin_order_goldens()
     if want('wav'):
         samples_wav_kat()
     if want('fwd'):

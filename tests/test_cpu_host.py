@@ -196,3 +196,22 @@ def test_custom_ops_registered_with_fake_kernels():
         assert loss.shape == ()
         d = torch.ops.srnn.dequant(torch.zeros(B, 5, dtype=torch.long), 256, 2.0, 0)
         assert d.dtype == torch.float32 and tuple(d.shape) == (B, 5)
+
+
+def test_plugin_schedule_matches_reference():
+    """The Trainer's plugin heaps fire plugins in the reference's order (first due at the
+    interval, re-armed at time + interval, ties in registration order; the reference's own
+    Trainer recorded tests/golden/plugin_order.npz over the same calls)."""
+    import make_golden_plugins as P
+    from trainer import Trainer
+    log = []
+    tr = Trainer(None, None, None, [], False, None)
+    for i, trig in enumerate(P.PLUGIN_TRIGGERS):
+        tr.register_plugin(P.RecPlugin(i, trig, log))
+    for it in range(1, 13):
+        tr.call_plugins('batch', it)
+        tr.call_plugins('iteration', it)
+        tr.call_plugins('update', it)
+        if it % 4 == 0:
+            tr.call_plugins('epoch', it // 4)
+    assert np.array_equal(np.array(log, dtype=np.int64), golden('plugin_order')['log'])

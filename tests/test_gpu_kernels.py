@@ -781,6 +781,115 @@ def test_mlp_dtab_packed_bf16(hip, monkeypatch, B, Tl, skew):
     assert e_pk <= 1.5 * e_ex + 1e-12
 
 
+def _dtab4(hip, da, x, B, Tl, blk=None, amax=None):
+    import ctypes
+    FS0, Q, D = 16, 256, da.shape[1]
+    work = torch.empty(Q * FS0 * D, device=DEV, dtype=torch.int64)
+    tab = torch.empty(Q, FS0, D, device=DEV, dtype=torch.bfloat16)
+    colsum = torch.full((FS0 * D,), 7.0, device=DEV)
+    done = ctypes.c_int(-1)
+    hip.lib().call('srnn_mlp_dtab4', hip.BF16, hip.ptr(da), D, hip.ptr(x), x.shape[1], 0, B, Tl,
+                   hip.ptr(tab), hip.BF16, D, FS0, Q, hip.ptr(work), work.numel() * 8,
+                   hip.ptr(colsum), ctypes.byref(done), hip.ptr(amax), hip.ptr(blk), hip.stream())
+    torch.cuda.synchronize()
+    assert done.value == 1
+    return tab.cpu(), colsum.cpu()
+
+
+@pytest.mark.parametrize('B,Tl', [(64, 1024), (3, 37)])
+def test_mlp_dtab_blocked_operand_bit_identical(hip, B, Tl):
+    """srnn_mlp_dtab4 reading the column-blocked copy blk[D/4][B*Tl][4] gives the same dTab and
+    column sums as reading the row-major da, bit for bit."""
+    D = 1024
+    g = torch.Generator().manual_seed(B + Tl)
+    x = torch.randint(0, 256, (B, Tl + 15), generator=g).to(DEV)
+    da = (torch.randn(B * Tl, D, generator=g) * 1e-3).to(DEV, torch.bfloat16)
+    blk = da.reshape(B * Tl, D // 4, 4).permute(1, 0, 2).contiguous()
+    t0, c0 = _dtab4(hip, da, x, B, Tl)
+    t1, c1 = _dtab4(hip, da, x, B, Tl, blk=blk)
+    assert torch.equal(t0, t1) and torch.equal(c0, c1)
+
+
+def test_gemm_writes_blocked_copy(hip):
+    """srnn_gemm_amax_blk_next: the ReLU-masked bf16 GEMM producing da1 also writes its output
+    column-blocked ([N/4][M][4]) and max |C|; the copy is the output, permuted, bit for bit
+    (the da1 GEMM's shape class: M = B T rows, a 256-tile grid that fills the chip)."""
+    M, N, K = 65536, 1024, 512
+    g = torch.Generator().manual_seed(5)
+    A = (torch.randn(M, K, generator=g)).to(DEV, torch.bfloat16)
+    W = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    mask = torch.randn(M, N, generator=g).to(DEV, torch.bfloat16)
+    amax = torch.zeros(1, device=DEV, dtype=torch.int32)
+    blk = torch.full((N // 4, M, 4), float('nan'), device=DEV, dtype=torch.bfloat16)
+    hip.lib().call('srnn_gemm_amax_blk_next', hip.ptr(amax), hip.ptr(blk))
+    C = hip.gemm(A, W, transB=True, mask=mask, out_dtype=torch.bfloat16)
+    taken = hip.lib().dll.srnn_gemm_amax_taken()
+    torch.cuda.synchronize()
+    assert taken == 2
+    ref = C.reshape(M, N // 4, 4).permute(1, 0, 2)
+    assert torch.equal(blk.view(torch.int16), ref.contiguous().view(torch.int16))
+    assert amax.view(torch.float32).item() == C.float().abs().max().item()
+
+
+def test_mlp_dtab_skew_takes_exact_form(hip):
+    """A sample histogram past the packed form's precision bound (one value at > 65,536
+    positions: long silences at large B) makes the gated exact 2^-40 form produce dTab:
+    bit-identical to SRNN_DTAB_PACK=0's output."""
+    import os
+    B, Tl, D = 128, 1024, 1024
+    g = torch.Generator().manual_seed(11)
+    x = torch.randint(0, 256, (B, Tl + 15), generator=g)
+    x[torch.rand(x.shape, generator=g) < 0.6] = 128
+    assert int(torch.bincount(x.reshape(-1)).max()) > 65536
+    x = x.to(DEV)
+    da = (torch.randn(B * Tl, D, generator=g) * 1e-4).to(DEV, torch.bfloat16)
+    t_gate, c_gate = _dtab4(hip, da, x, B, Tl)
+    os.environ['SRNN_DTAB_PACK'] = '0'
+    try:
+        t_ex, c_ex = _dtab4(hip, da, x, B, Tl)
+    finally:
+        del os.environ['SRNN_DTAB_PACK']
+    assert torch.equal(t_gate, t_ex) and torch.equal(c_gate, c_ex)
+
+
+def test_mlp_dtab_nonfinite_poisons(hip):
+    """A NaN in da (packed form): dTab and the column sums come out NaN, not integers."""
+    B, Tl, D = 4, 256, 1024
+    g = torch.Generator().manual_seed(12)
+    x = torch.randint(0, 256, (B, Tl + 15), generator=g).to(DEV)
+    da = (torch.randn(B * Tl, D, generator=g) * 1e-3).to(DEV, torch.bfloat16)
+    da[5, 17] = float('nan')
+    t, c = _dtab4(hip, da, x, B, Tl)
+    assert torch.isnan(t.float()).all() and torch.isnan(c).all()
+
+
+def test_dtab_blocked_step_bit_identical(hip, monkeypatch):
+    """A bf16 TBPTT step at D = 1024 with the da1 GEMM's blocked copy feeding the scatter
+    (default) equals the row-major-operand step (SRNN_DTAB_BLK=0) bit for bit."""
+    import model as M
+    import nn as snn
+    outs = []
+    for flag in ('0', '1'):
+        monkeypatch.setenv('SRNN_DTAB_BLK', flag)
+        torch.manual_seed(3)
+        m = M.SampleRNN([16, 4], 1, 1024, True, 256, True, False, 43, 6)
+        m.compute_dtype = torch.bfloat16
+        pred = M.Predictor(m).to(DEV)
+        B, T, L = 4, 1024, 64
+        g = torch.Generator().manual_seed(4)
+        inp = torch.randint(0, 256, (B, L + T - 1), generator=g).to(DEV)
+        tgt = torch.randint(0, 256, (B, T), generator=g).to(DEV)
+        cond = torch.rand(B, T // L, 43, generator=g).to(DEV)
+        spk = torch.arange(B).reshape(-1, 1).to(DEV) % 6
+        loss = snn.sequence_nll_loss_bits(pred(inp, True, cond, spk), tgt)
+        loss.backward()
+        outs.append({k: p.grad.detach().cpu().clone() for k, p in pred.named_parameters()
+                     if p.grad is not None})
+    assert outs[0].keys() == outs[1].keys()
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
+
+
 def test_fused_upsampling_bias_grad_in_step(hip):
     """A bf16 TBPTT step at D = 1024 takes the bottom tier's upsampling bias gradient from the
     MLP's dTab pass (no separate column sum), and it equals the column sum of d(upper)."""

@@ -6,12 +6,22 @@ WRITE_SIZE kB, divided by the samples generated (16 per persistent launch).
 
   python tools/pmc_gen.py FETCH_DB WRITE_DB > profiles/r02_pmc_gen.txt
 """
+import os
 import sqlite3
 import sys
 
 LOOP = ('gen_mlp_kernel', 'skinny_kernel', 'gru_cell_ring_kernel', 'tier_input_tiled_kernel',
         'fold_gru_kernel',
         'advance_kernel', 'gen_noise_kernel')
+
+
+
+def _csrc_hash():
+    """samplernn_hip.csrc_hash(): the kernels these counters were taken on."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, 'jalil-saboorizadeh-multi-speaker-neural-vocoder_amd'))
+    import samplernn_hip
+    return samplernn_hip.csrc_hash()
 
 
 def per_kernel(db, ctr):
@@ -45,6 +55,7 @@ def main(fdb, wdb):
         print('%-70s %6d %14.1f %12.1f' % (k[:70], nf, 2 * sf, sw))
     print('generation steps %d (16 per persistent launch, %d launches)' % (steps, launches))
     print('avg_step_bytes %d' % int(round(tot * 1024 / max(steps, 1))))
+    print('csrc_hash %s' % _csrc_hash())
 
 
 if __name__ == '__main__':

@@ -6,8 +6,18 @@ requests at 64 B) + WRITE_SIZE kB, summed over the kernels the site launches onc
   python tools/pmc_site.py SITE ROWS FETCH_DB WRITE_DB kernel1 [kernel2 ...]
       > profiles/r03_pmc_<SITE>_b<ROWS>.txt      (read back by bench.py pmc_traffic)
 """
+import os
 import sqlite3
 import sys
+
+
+
+def _csrc_hash():
+    """samplernn_hip.csrc_hash(): the kernels these counters were taken on."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, 'jalil-saboorizadeh-multi-speaker-neural-vocoder_amd'))
+    import samplernn_hip
+    return samplernn_hip.csrc_hash()
 
 
 def per_kernel(db, ctr, names):
@@ -41,6 +51,7 @@ def main(site, rows, fdb, wdb, names):
         tot += mf + mw
         print('%-40s %6d %14.1f %12.1f' % (k, nf, mf, mw))
     print('avg_step_bytes %d' % int(round(tot * 1024)))
+    print('csrc_hash %s' % _csrc_hash())
 
 
 if __name__ == '__main__':
