@@ -490,6 +490,18 @@ def main():
                 r, N, peak, 'configs[1]: the same step at B=128 rows on one GPU')
             extra['config_b']['kernels'] = kernels_block(r, peak)
             log('config_b: %.2f ms/step' % r['ms_per_step'])
+        if N == 1 and args.dtype == 'bf16':
+            # the same step with every GEMM on the hand-written kernels (hipBLASLt off):
+            # the kernel-quality number for the hand-written path alone
+            os.environ['SRNN_BLASLT'] = '0'
+            try:
+                r = run_tbptt(dev, D, rows, args.steps, args.warmup, dtype, probe=False)
+            finally:
+                del os.environ['SRNN_BLASLT']
+            extra['handwritten_only'] = tbptt_summary(
+                r, N, peak, 'the headline step with SRNN_BLASLT=0: every GEMM on the '
+                'hand-written gemm3 / gemm2 / skinny kernels, no vendor library kernel')
+            log('handwritten_only: %.2f ms/step' % r['ms_per_step'])
         if not (not strong and rows == 64) and not (strong and rows == 64):
             r = run_tbptt(dev, D, 64, args.steps, args.warmup, dtype)
             extra['weak_64'] = tbptt_summary(

@@ -321,6 +321,11 @@ int srnn_step_advance(int64_t* dstep, int n, void* stream);
  * distributed step; this feeds distributed.GradAllReduce's RCCL all-reduce.   */
 int srnn_pack_grads(int ntensors, const float* const* src, const int64_t* n,
                     const int64_t* dst_off, void* flat, int dtype, void* stream);
+/* bf16 copies of n fp32 tensors (dst[t][j] = bf16(src[t][j]), j < n[t]) in one launch per 64
+ * tensors: ZeRO-1 data parallelism refreshes every parameter's bf16 copy after the parameter
+ * all-gather (the reference's replicated Adam, optim.py:4-21, sharded over ranks).          */
+int srnn_cast_multi(int ntensors, const float* const* src, void* const* dst, const int64_t* n,
+                    void* stream);
 
 /* ---- autoregressive generation (Generator.__call__, model.py:445-520) --------------- */
 typedef struct SrnnTier {

@@ -330,12 +330,15 @@ __global__ __launch_bounds__(256) void dtab_prep_kernel(const T* __restrict__ da
                                                         int64_t ldx, int xoff, int W, int B,
                                                         int nb_da, DtabStat* __restrict__ st) {
     __shared__ int hist[256];
-    __shared__ float wmax[4];
+    __shared__ unsigned wmax[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     if ((int)blockIdx.x < nb_da) {
-        // max |da| over this block's rows (16-B loads of 8 bf16 / 4 fp32 where aligned)
+        // max |da| over this block's rows (16-B loads of 8 bf16 / 4 fp32 where aligned), as
+        // the magnitude's float bits: an unsigned max keeps NaN (above inf above every finite
+        // value) where fmaxf would drop it
         constexpr int V = 16 / sizeof(T);
-        float m = 0.f;
+        unsigned m = 0u;
+        auto mag = [](float x) { return __float_as_uint(x) & 0x7fffffffu; };
         const int64_t r0 = nrows * blockIdx.x / nb_da, r1 = nrows * (blockIdx.x + 1) / nb_da;
         const int nv = D / V;
         if (std::is_same<T, bf16>::value && ldda == D && D % V == 0) {
@@ -360,7 +363,7 @@ __global__ __launch_bounds__(256) void dtab_prep_kernel(const T* __restrict__ da
                 for (int k = 0; k < 4; ++k) take(u[k]);
             }
             for (; j < n; j += 256) take(p[j]);
-            m = __uint_as_float(mm << 16);
+            m = mm << 16;
         } else
         for (int64_t r = r0; r < r1; ++r) {
             const T* row = da + r * ldda;
@@ -368,18 +371,16 @@ __global__ __launch_bounds__(256) void dtab_prep_kernel(const T* __restrict__ da
                 const uint4 u = *reinterpret_cast<const uint4*>(row + (int64_t)j * V);
                 const T* e = reinterpret_cast<const T*>(&u);
 #pragma unroll
-                for (int k = 0; k < V; ++k) m = fmaxf(m, fabsf(to_f(e[k])));
+                for (int k = 0; k < V; ++k) m = max(m, mag(to_f(e[k])));
             }
-            for (int j = nv * V + tid; j < D; j += 256) m = fmaxf(m, fabsf(to_f(row[j])));
+            for (int j = nv * V + tid; j < D; j += 256) m = max(m, mag(to_f(row[j])));
         }
 #pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
         if (lane == 0) wmax[wave] = m;
         __syncthreads();
-        if (tid == 0) {
-            const float b = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
-            atomicMax(&st->amax_bits, __float_as_uint(b));
-        }
+        if (tid == 0)
+            atomicMax(&st->amax_bits, max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3])));
         return;
     }
     // histogram of one batch row's window of sample values

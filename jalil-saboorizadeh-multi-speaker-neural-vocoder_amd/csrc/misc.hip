@@ -1119,6 +1119,51 @@ extern "C" int srnn_pack_grads(int ntensors, const float* const* src, const int6
     return 0;
 }
 
+// bf16 copies of n fp32 tensors in ONE launch (ZeRO-1 data parallelism, distributed.py: after the
+// parameter all-gather, the other ranks' shards of every parameter refresh its bf16 copy).
+struct CastMulti {
+    int nt;
+    int boff[PACK_MT + 1];
+    const float* src[PACK_MT];
+    bf16* dst[PACK_MT];
+    int64_t n[PACK_MT];
+};
+
+__global__ __launch_bounds__(256) void cast_multi_kernel(CastMulti a) {
+    int t = 0;
+    while (t + 1 < a.nt && a.boff[t + 1] <= (int)blockIdx.x) ++t;
+    t = __builtin_amdgcn_readfirstlane(t);
+    const float* __restrict__ src = a.src[t];
+    bf16* __restrict__ dst = a.dst[t];
+    const int64_t n = a.n[t];
+    const int64_t j0 = (int64_t)(blockIdx.x - a.boff[t]) * 2048;
+    for (int64_t j = j0 + threadIdx.x; j < n && j < j0 + 2048; j += 256) dst[j] = __float2bfloat16(src[j]);
+}
+
+extern "C" int srnn_cast_multi(int ntensors, const float* const* src, void* const* dst,
+                               const int64_t* n, void* stream) {
+    SRNN_REQUIRE(ntensors >= 0, "cast_multi: bad arguments");
+    for (int t0 = 0; t0 < ntensors;) {
+        CastMulti a;
+        a.nt = 0;
+        a.boff[0] = 0;
+        int t = t0;
+        for (; t < ntensors && a.nt < PACK_MT; ++t) {
+            if (n[t] <= 0) continue;
+            SRNN_REQUIRE(src[t] && dst[t], "cast_multi: null tensor");
+            const int k = a.nt++;
+            a.src[k] = src[t]; a.dst[k] = (bf16*)dst[t]; a.n[k] = n[t];
+            a.boff[k + 1] = a.boff[k] + (int)((n[t] + 2047) / 2048);
+        }
+        t0 = t;
+        if (a.nt == 0) continue;
+        hipLaunchKernelGGL(cast_multi_kernel, dim3((unsigned)a.boff[a.nt]), dim3(256), 0,
+                           (hipStream_t)stream, a);
+        SRNN_LAUNCH_CHECK();
+    }
+    return 0;
+}
+
 extern "C" int srnn_adam_clip(float* p, float* g, float* m, float* v, void* p_bf16,
                               int64_t n, float clip_lo, float clip_hi, double lr, double beta1,
                               double beta2, double eps, int64_t step, void* stream) {

@@ -134,8 +134,19 @@ class GradAllReduce:
     """
 
     def __init__(self, bucket_mb=64, group=None, overlap_groups=None, grad_dtype=None,
-                 defer=None):
+                 defer=None, zero=None, force=None):
         self.bucket_bytes = int(bucket_mb * (1 << 20))
+        # ZeRO-1 (fused device path only): reduce-scatter the buckets, clamp + Adam on this
+        # rank's shard, all-gather the parameters (see _zero_* below); SRNN_DP_ZERO=0 turns it off
+        self.zero = os.environ.get('SRNN_DP_ZERO', '1') != '0' if zero is None else bool(zero)
+        # force: run the bucket path even in a one-rank group (tests of the collectives and
+        # their graph capture on a one-GPU box); SRNN_DP_FORCE=1
+        self.force = os.environ.get('SRNN_DP_FORCE', '0') == '1' if force is None else force
+        self._zplan = None          # ZeRO: key -> (bucket, offs, total, shard) of the fused path
+        self._pflat = {}            # ZeRO: key -> flat fp32 parameter buffer (params are views)
+        self._gshard = {}           # ZeRO: key -> this rank's reduced gradient shard
+        self.zero_shadows = []      # ZeRO: (param, bf16 copy) pairs the fused step left stale
+        self.zero_ok = False        # set by optim.gradient_clipping when its step is the fused one
         self.defer = os.environ.get('SRNN_DP_DEFER', '1') != '0' if defer is None else defer
         self._deferred = []         # ready buckets waiting for the next sweep's enqueue
         self._after_ref = None
@@ -150,7 +161,7 @@ class GradAllReduce:
         self._fence_ref = None
         self.reduced = None         # fused path: ([(param, view)], dtype, scale) of the step
         if overlap_groups is not None and dist.is_available() and dist.is_initialized() and \
-                dist.get_world_size(group) > 1:
+                (dist.get_world_size(group) > 1 or self.force):
             self._install(overlap_groups)
 
     # ---- bucketing
@@ -168,13 +179,25 @@ class GradAllReduce:
             buckets.append(cur)
         return buckets
 
-    @staticmethod
-    def _offsets(bucket):
+    def _offsets(self, bucket):
         offs, off = [], 0
         for p in bucket:
             offs.append(off)
             off += (p.numel() + _ALIGN - 1) // _ALIGN * _ALIGN
+        if self._zero_on(bucket):
+            # equal 64-element-aligned shards (the pieces of a parameter a shard holds then
+            # start 256-B aligned for the fused Adam's vector accesses)
+            q = _ALIGN * self._n()
+            off = (off + q - 1) // q * q
         return offs, off
+
+    def _n(self):
+        return dist.get_world_size(self.group)
+
+    def _zero_on(self, bucket):
+        # only under the fused device clip + Adam (optim.gradient_clipping sets zero_ok), which
+        # reads the shards; any other optimizer gets fully reduced gradients in p.grad
+        return self.zero and self.zero_ok and bucket[0].is_cuda
 
     def _flat(self, key, bucket, flag):
         offs, total = self._offsets(bucket)
@@ -214,13 +237,38 @@ class GradAllReduce:
             for p, o in zip(bucket, offs):
                 if p.grad is not None:
                     flat[o:o + p.numel()].copy_(p.grad.reshape(-1))
+        if self._zero_on(bucket):
+            # ZeRO-1: this rank receives only the SUM of its shard
+            S = total // self._n()
+            sh = self._gshard.get(key)
+            if sh is None or sh.numel() != S or sh.dtype != flat.dtype:
+                sh = torch.empty(S, dtype=flat.dtype, device=flat.device)
+                self._gshard[key] = sh
+            if dist.get_backend(self.group) == 'nccl':
+                work = dist.reduce_scatter_tensor(sh, flat[:total], op=dist.ReduceOp.SUM,
+                                                  group=self.group, async_op=async_op)
+            else:        # gloo has no reduce-scatter: reduce everything, keep the shard
+                work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group,
+                                       async_op=async_op)
+            return (flat, offs, total, key), work
         work = dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
-        return (flat, offs, total), work
+        return (flat, offs, total, key), work
 
     def _finish(self, bucket, rec, n, fused, views):
-        flat, offs, total = rec
+        flat, offs, total, key = rec
         if flat.numel() > total:        # the carried failure flag: any rank's -> this rank's
             _flag_from(flat[total:total + 1])
+        if fused and self._zero_on(bucket):
+            S = total // n
+            r = dist.get_rank(self.group)
+            sh = self._gshard[key]
+            if dist.get_backend(self.group) != 'nccl':
+                sh.copy_(flat[r * S:(r + 1) * S])
+            self._zero_params(key, bucket, offs, total)
+            views.append(('zero', key, bucket, offs, r * S, S, sh))
+            for p in bucket:
+                p.grad = None           # the local gradient was packed: release it
+            return
         if fused:
             for p, o in zip(bucket, offs):
                 views.append((p, flat[o:o + p.numel()].view(p.shape)))
@@ -311,7 +359,8 @@ class GradAllReduce:
         buckets and publish (param, view) pairs, the dtype and the 1 / world scale in
         self.reduced; otherwise write the means back into p.grad."""
         self.reduced = None
-        if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        if not (dist.is_available() and dist.is_initialized()) or \
+                (dist.get_world_size() == 1 and not self.force):
             return
         n = dist.get_world_size(self.group)
         views = []
@@ -322,12 +371,14 @@ class GradAllReduce:
             late = [idx for idx in range(len(self._groups)) if idx not in self._pending]
             self._deferred = []                       # (launched below, in index order)
             dev = self._groups[0][1][0].is_cuda
+            zero = self._zero_on(self._groups[0][1])
             for idx in late:                          # grads that never arrived this step
                 key, bucket = self._groups[idx]
                 self._pending[idx] = self._launch(key, bucket, True,
-                                                  flag=dev and idx == late[-1])
+                                                  flag=dev and not zero and idx == late[-1])
             solo = None
-            if dev and not late:
+            if dev and (zero or not late):
+                # (ZeRO: a shard holds 1/N of a bucket, so the flag travels on its own)
                 if self._flag_buf is None:
                     self._flag_buf = torch.zeros(1, device=self._groups[0][1][0].device)
                 _flag_to(self._flag_buf)
@@ -346,12 +397,81 @@ class GradAllReduce:
         else:
             params = [p for g in optimizer.param_groups for p in g['params'] if p.requires_grad]
             buckets = self._split(params)
+            zero = bool(buckets) and self._zero_on(buckets[0]) and fused
+            if zero:
+                if self._flag_buf is None:
+                    self._flag_buf = torch.zeros(1, device=buckets[0][0].device)
+                _flag_to(self._flag_buf)
+                dist.all_reduce(self._flag_buf, op=dist.ReduceOp.SUM, group=self.group)
+                _flag_from(self._flag_buf)
             for bi, bucket in enumerate(buckets):
                 dev = bucket[0].is_cuda
-                rec, _ = self._launch(bi, bucket, False, flag=dev and bi == len(buckets) - 1)
+                rec, _ = self._launch(bi, bucket, False,
+                                      flag=dev and not zero and bi == len(buckets) - 1)
                 self._finish(bucket, rec, n, fused and dev, views)
-        if views:
+        if views and views[0][0] == 'zero':
+            self.reduced = ('zero', views, views[0][6].dtype, 1.0 / n)
+        elif views:
             self.reduced = (views, views[0][1].dtype, 1.0 / n)
+
+
+    # ---- ZeRO-1 (reduce-scatter -> sharded clamp + Adam -> all-gather; the same
+    # bytes on xGMI as the all-reduce, 1/N of the optimizer's HBM traffic per rank).  The
+    # clamp is elementwise (optim.py:11-13) and Adam is elementwise too, so updating each
+    # rank's shard of the SUMMED gradient (scaled by 1/N) and gathering the parameters gives
+    # every rank exactly the replicated update.
+    def _zero_params(self, key, bucket, offs, total):
+        """Parameters of a ZeRO bucket become views of one flat fp32 buffer (once), so the
+        all-gather writes them in place."""
+        pf = self._pflat.get(key)
+        if pf is not None and all(p.data_ptr() == pf[o:].data_ptr()
+                                  for p, o in zip(bucket, offs)):
+            return
+        pf = torch.zeros(total, dtype=torch.float32, device=bucket[0].device)
+        with torch.no_grad():
+            for p, o in zip(bucket, offs):
+                if p.dtype != torch.float32 or not p.is_contiguous():
+                    raise NotImplementedError('ZeRO-1: contiguous fp32 parameters only')
+                v = pf[o:o + p.numel()]
+                v.copy_(p.data.reshape(-1))
+                p.data = v.view(p.shape)
+        self._pflat[key] = pf
+
+    def after_update(self):
+        """After the fused clamp + Adam updated this rank's shards (ZeRO-1): all-gather every
+        bucket's parameters in place, then refresh the parameters' bf16 copies.  The current
+        stream waits for the gathers (a stream-level wait: the next forward is ordered after
+        them without a host synchronisation)."""
+        red = self.reduced
+        if red is None or red[0] != 'zero':
+            return
+        import ctypes
+        import samplernn_hip as H
+        n = self._n()
+        nccl = dist.get_backend(self.group) == 'nccl'
+        works = []
+        for _, key, bucket, offs, s0, S, _sh in red[1]:
+            pf = self._pflat[key]
+            if nccl:
+                works.append(dist.all_gather_into_tensor(pf, pf[s0:s0 + S], group=self.group,
+                                                         async_op=True))
+            else:
+                parts = list(pf.split(S))
+                dist.all_gather(parts, pf[s0:s0 + S].clone(), group=self.group)
+        for w in works:
+            w.wait()
+        src, dst, cnt, ps = [], [], [], []
+        for p, sh in self.zero_shadows:
+            src.append(H.ptr(p))
+            dst.append(H.ptr(sh))
+            cnt.append(p.numel())
+            ps.append(p)
+        if src:
+            k = len(src)
+            H.lib().call('srnn_cast_multi', k, (ctypes.c_void_p * k)(*src),
+                         (ctypes.c_void_p * k)(*dst), (ctypes.c_int64 * k)(*cnt), H.stream())
+            for p in ps:
+                H.shadow_refreshed(p)
 
 
 def _flag_to(dst):

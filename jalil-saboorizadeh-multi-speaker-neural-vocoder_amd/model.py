@@ -749,7 +749,7 @@ def mlp_backward(ctx, dlogp, nll=None):
     amax = blk = None
     if ctx.udt == torch.bfloat16:
         amax = torch.zeros(1, device=dev, dtype=torch.int32)
-        if FS0 == 16 and D % 256 == 0 and os.environ.get('SRNN_DTAB_BLK', '1') != '0':
+        if FS0 == 16 and D % 256 == 0 and os.environ.get('SRNN_DTAB_BLK', '0') == '1':
             # ... and a column-blocked copy [D/4][M][4] of da1, the scatter's operand
             blk = torch.empty((D // 4, M, 4), device=dev, dtype=torch.bfloat16)
             H.lib().call('srnn_gemm_amax_blk_next', H.ptr(amax), H.ptr(blk))

@@ -73,8 +73,22 @@ def _fused_adam_step(optimizer, lo, hi, reduced=None, dsteps=None):
     read in place instead of p.grad.  dsteps (DeviceSteps): take the step count from the
     device counters (re-seeded from the host count when they disagree) and advance them."""
     import custom_ops  # noqa: F401  (registers srnn::adam_clip_)
-    rv = {id(p): v for p, v in reduced[0]} if reduced else None
-    gscale = reduced[2] if reduced else 1.0
+    zero = reduced is not None and reduced[0] == 'zero'
+    if zero:
+        # ZeRO-1 (distributed.GradAllReduce): this rank updates only its shard of each bucket;
+        # pieces[id(p)] = [(a, b, gradient view)] -- elements [a, b) of p and their reduced sums
+        pieces = {}
+        for _, key, bucket, offs, s0, S, sh in reduced[1]:
+            for p, o in zip(bucket, offs):
+                a, b = max(o, s0), min(o + p.numel(), s0 + S)
+                if b > a:
+                    pieces.setdefault(id(p), []).append((a - o, b - o, sh[a - s0:b - s0]))
+        zero_shadows = []
+        rv = None
+        gscale = reduced[3]
+    else:
+        rv = {id(p): v for p, v in reduced[0]} if reduced else None
+        gscale = reduced[2] if reduced else 1.0
     capturing = torch.cuda.is_current_stream_capturing()
     uniform = True
     for gi, group in enumerate(optimizer.param_groups):
@@ -92,8 +106,8 @@ def _fused_adam_step(optimizer, lo, hi, reduced=None, dsteps=None):
                 st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
             # a None grad goes to the kernel as NULL = all-zero (no zero-fill launch)
-            if rv is None and p.grad is not None and (not p.grad.is_contiguous() or
-                                                      p.grad.dtype != torch.float32):
+            if rv is None and not zero and p.grad is not None and (not p.grad.is_contiguous() or
+                                                                   p.grad.dtype != torch.float32):
                 p.grad = p.grad.float().contiguous()
             if not (p.is_contiguous() and p.dtype == torch.float32):
                 raise NotImplementedError('fused clip+Adam: contiguous fp32 parameters only')
@@ -117,6 +131,22 @@ def _fused_adam_step(optimizer, lo, hi, reduced=None, dsteps=None):
             shadows = [H.shadow_of(p) for p, _ in items]
             ev = H.roof_begin()
             nel = sum(p.numel() for p, _ in items)
+            if zero:
+                # the shard's pieces; every bf16 copy is refreshed after the parameter
+                # all-gather (GradAllReduce.after_update), not here
+                zero_shadows += [(p, sh) for (p, _), sh in zip(items, shadows) if sh is not None]
+                pp, gg, mm, vv = [], [], [], []
+                for p, s in items:
+                    for a, b, gv in pieces.get(id(p), ()):
+                        pp.append(p.view(-1)[a:b])
+                        gg.append(gv)
+                        mm.append(s['exp_avg'].view(-1)[a:b])
+                        vv.append(s['exp_avg_sq'].view(-1)[a:b])
+                torch.ops.srnn.adam_clip_(pp, gg, mm, vv, [None] * len(pp), float(gscale),
+                                          float(lo), float(hi), float(group['lr']), float(b1),
+                                          float(b2), float(group['eps']), step, dstep)
+                H.roof_end('adam_clip', ev, sum(t.numel() for t in pp) * 32)
+                continue
             grads = [p.grad for p, _ in items] if rv is None else [rv.get(id(p)) for p, _ in items]
             # the registered op srnn::adam_clip_ (custom_ops.py)
             torch.ops.srnn.adam_clip_([p for p, _ in items], grads,
@@ -135,6 +165,7 @@ def _fused_adam_step(optimizer, lo, hi, reduced=None, dsteps=None):
         dsteps.uniform = uniform
         torch.ops.srnn.step_advance_(dsteps.t)
         dsteps.mirror = [None if m is None else m + 1 for m in dsteps.mirror]
+    return zero_shadows if zero else None
 
 
 def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
@@ -159,6 +190,8 @@ def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
 
         def step(self, closure):
             if self._fused():
+                if hasattr(self.grad_sync, 'zero_ok'):
+                    self.grad_sync.zero_ok = True     # ZeRO-1 shards are read by this step
                 with torch.enable_grad():
                     loss = closure()
                 reduced = None
@@ -174,8 +207,15 @@ def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
                     self.dsteps = DeviceSteps(optimizer, optimizer.param_groups[0]['params'][0].device)
                     self.dsteps.mirror = [None] * len(optimizer.param_groups)
                 with torch.no_grad():
-                    _fused_adam_step(optimizer, min, max, reduced, self.dsteps)
+                    zs = _fused_adam_step(optimizer, min, max, reduced, self.dsteps)
+                    if zs is not None:       # ZeRO-1: gather the updated shards
+                        self.grad_sync.zero_shadows = zs
+                        self.grad_sync.after_update()
+                        self.grad_sync.zero_shadows = []
                 return loss
+
+            if hasattr(self.grad_sync, 'zero_ok'):
+                self.grad_sync.zero_ok = False            # full reductions into p.grad
 
             def closure_wrapper():
                 loss = closure()

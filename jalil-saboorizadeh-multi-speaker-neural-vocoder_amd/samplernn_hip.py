@@ -55,6 +55,7 @@ _SIGS = {
     'srnn_mlp_dtab4': [_I, _P, _L, _P, _L, _I, _I, _I, _P, _I, _I, _I, _I, _P, _SZ, _P,
                        ctypes.POINTER(_I), _P, _P, _P],
     'srnn_gemm_amax_next': [_P],
+    'srnn_cast_multi': [_I, _P, _P, _P, _P],
     'srnn_gemm_amax_blk_next': [_P, _P],
     'srnn_logsoftmax_nll': [_P, _L, _P, _L, _I, _L, _I, _P, _P, _L, _P, _I, _L, _F, _P],
     'srnn_logsoftmax_bwd': [_P, _L, _P, _L, _L, _I, _P, _I, _L, _P],

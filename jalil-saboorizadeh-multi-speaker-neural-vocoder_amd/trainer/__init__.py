@@ -295,7 +295,10 @@ class Trainer(object):
             out_loss[0], out_loss[1] = out.data, loss.data
             return loss
         try:
-            with torch.cuda.graph(g):     # a private memory pool per step kind
+            # a private memory pool per step kind; thread-local capture mode, so other
+            # threads' HIP calls (the RCCL process group's watchdog querying its events under
+            # data parallelism) do not invalidate the capture
+            with torch.cuda.graph(g, capture_error_mode='thread_local'):
                 self.optimizer.step(closure)
                 for rnn, b in zip(rnns, bufs):
                     h = model.hidden_states[rnn]

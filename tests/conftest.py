@@ -40,39 +40,50 @@ def genlong_noise(g, q_levels=256):
     return q
 
 
-# Tolerances for the sampled TBPTT fixtures (tbptt_big / tbptt_a).  Step 0 (fresh weights)
-# is the forward + backward at the fixture's dims: every sampled gradient within
-# atol + rtol |g|.  From the first Adam update on, the trajectory is chaotic at the rounding
-# level: near-zero gradients flip sign under fp32 summation-order noise and Adam (first
-# steps ~ lr * sign(g)) moves those weights by +-lr.  make_golden.py measured the reference
-# against ITSELF (1 vs 8 threads, alt_* keys): at D = 1024 its step-2 gradients differ beyond
-# 1e-4 + 1e-3|g| at up to 1.5 % of entries (relative L2 1.8e-2, max 3.5e-4), its final
-# parameters beyond 2e-4 at 0.1 % (max 9.2e-4 = ~lr), its step-2 hidden state by 9.1e-3.
-# The later-step bounds below are those measured self-drifts with a ~3x margin.
-DRIFT = dict(grad_viol=0.05, grad_rel_l2=0.05, grad_max=2e-3,
-             param_viol=0.01, param_max=3e-3, param_rel_l2=5e-3)
+# Tolerances for the sampled TBPTT fixtures (tbptt_big / tbptt_a): the REFERENCE's own
+# sensitivity, measured by make_golden.py.  It reran the reference's trajectory NPERT = 6
+# times from the same weights perturbed by one ulp each (random signs) -- the rounding-level
+# difference any other fp32 implementation has in every op -- and stored, per quantity, the
+# envelope over those runs of the max and L2 distance to the unperturbed run (env_max /
+# env_l2).  At D = 1024 such a perturbation flips a few ReLU masks of the sample-level MLP
+# (pre-activations within rounding of zero): the chunk-0 gradient rows of those units move
+# by ~1e-4, Adam's sign-driven first steps turn that into +-lr weight moves, and by chunk 2
+# the reference differs from itself by ~0.04-0.12 in the hidden states and ~2e-4 in the
+# loss.  (The thread-count rerun, alt_* keys, perturbs only MKL's reduction order and moves
+# far less.)  A result passes when its distance to the reference is within FLOOR x that
+# envelope plus the strict tolerance of the quantity.
+FLOOR = 3.0
 
 
-def assert_sampled_close(got, g, key, name, atol, rtol, max_viol=0.0, max_abs=None,
-                         max_rel_l2=1e-3):
-    """Compare a full tensor against a sampled fixture entry (seeded sample + L2 norm):
-    at most max_viol of the sampled entries outside atol + rtol |ref|, none beyond
-    max_abs, and the sample's relative L2 difference and the tensor's L2 norm within
-    max_rel_l2."""
+def within_floor(got, ref, g, key, atol, rtol=0.0):
+    """|got - ref| <= FLOOR env(key) (max and L2 over the entries) + atol + rtol max|ref|."""
+    import numpy as np
+    got, ref = (np.asarray(x, dtype=np.float64).ravel() for x in (got, ref))
+    d = np.abs(got - ref)
+    em, el = float(g['env_max/' + key]), float(g['env_l2/' + key])
+    lim = FLOOR * em + atol + rtol * np.abs(ref).max()
+    assert d.max() <= lim, '%s: max |diff| %.3g > %.3g (perturbed reference %.3g)' % (
+        key, d.max(), lim, em)
+    l2 = np.sqrt((d * d).sum())
+    lim2 = FLOOR * el + atol * np.sqrt(d.size) + rtol * np.sqrt((ref * ref).sum())
+    assert l2 <= lim2, '%s: L2 |diff| %.3g > %.3g (perturbed reference %.3g)' % (
+        key, l2, lim2, el)
+
+
+def within_floor_sampled(got, g, key, name, atol, rtol=0.0):
+    """within_floor on a sampled fixture entry: got is the full tensor."""
     import numpy as np
     import recipe
     a = np.asarray(got, dtype=np.float32).ravel()
     idx = recipe.sample_index(a.size, name)
-    r = g['smp_%s/%s' % (key, name)]
-    d = np.abs(a[idx].astype(np.float64) - r)
-    bad = d > atol + rtol * np.abs(r)
-    msg = '%s %s: %d/%d outside %.3g + %.3g|ref|, max diff %.3g' % (
-        key, name, int(bad.sum()), d.size, atol, rtol, float(d.max()))
-    assert bad.mean() <= max_viol, msg
-    if max_abs is not None:
-        assert d.max() <= max_abs, msg
-    rn = np.sqrt((r.astype(np.float64) ** 2).sum())
-    assert np.sqrt((d * d).sum()) <= max_rel_l2 * rn + atol, msg + ' (sample relative L2)'
-    f = a.astype(np.float64)
-    l2 = float(g['l2_%s/%s' % (key, name)])
-    assert abs(np.sqrt((f * f).sum()) - l2) <= max_rel_l2 * l2 + atol, msg + ' (L2 norm)'
+    within_floor(a[idx], g['smp_%s/%s' % (key, name)], g, '%s/%s' % (key, name), atol, rtol)
+
+
+@pytest.fixture(scope='session')
+def hip():
+    """The product HIP library; GPU tests fail loudly if it cannot be loaded."""
+    import torch
+    assert torch.cuda.is_available(), 'gpu test needs a GPU'
+    import samplernn_hip
+    samplernn_hip.lib()  # raises if the .so is missing
+    return samplernn_hip

@@ -420,6 +420,44 @@ def tbptt_goldens(name, B, T, n_steps, seed, lr=1e-3, sampled=False, tag=None, a
             finally:
                 torch.set_num_threads(nt)
             a_losses, a_grads, a_params, a_hidden = alt
+            # ... and from one-ulp perturbations of every initial weight (random signs, NPERT
+            # seeds): any other fp32 implementation differs from the reference by rounding of
+            # this order in every op; at D = 1024 that is enough to flip a few ReLU masks of
+            # the sample-level MLP (pre-activations within rounding of 0), whose gradient rows
+            # then differ by ~1e-4 and drive Adam's sign-driven first steps apart.  Stored:
+            # the envelope over the runs of each quantity's max |diff| and L2 |diff| from the
+            # reference (env_max / env_l2), over the same sampled entries the fixture keeps.
+            env = {}
+
+            def envelope(key, a, r):
+                d = np.abs(np.asarray(a, np.float64).ravel() - np.asarray(r, np.float64).ravel())
+                e0, e1 = env.get(key, (0.0, 0.0))
+                env[key] = (max(e0, float(d.max())), max(e1, float(np.sqrt((d * d).sum()))))
+            for pr in range(NPERT):
+                rng = np.random.Generator(np.random.PCG64(seed + 999 + pr))
+                wp = {k: np.nextafter(v, np.where(rng.random(v.shape) < 0.5, -np.inf, np.inf)
+                                      .astype(np.float32)).astype(np.float32)
+                      for k, v in w.items()}
+                p_losses, p_grads, p_params, p_hidden = _tbptt_run(cfg, wp, B, T, n_steps, lr,
+                                                                   seed)
+                envelope('losses', p_losses, losses)
+                for s, grads in enumerate(p_grads):
+                    for k, gg in zip(names, grads):
+                        a = gg.numpy().ravel()
+                        envelope('grad_%d/%s' % (s, k), a[recipe.sample_index(a.size, k)],
+                                 out['smp_grad_%d/%s' % (s, k)])
+                for k, pp in zip(names, p_params):
+                    a = pp.numpy().ravel()
+                    envelope('param_final/' + k, a[recipe.sample_index(a.size, k)],
+                             out['smp_param_final/' + k])
+                for s, hs in enumerate(p_hidden):
+                    for t, h in enumerate(hs):
+                        envelope('hidden_%d_tier%d' % (s, t), h, out['hidden_%d_tier%d' % (s, t)])
+                print('  perturbation %d: losses %s' % (pr, p_losses))
+            out['npert'] = np.array(NPERT)
+            for k, (emax, el2) in env.items():
+                out['env_max/' + k] = np.array(emax)
+                out['env_l2/' + k] = np.array(el2)
             out['alt_threads'] = np.array(alt_threads)
             out['alt_losses'] = np.array(a_losses)
             for s, grads in enumerate(a_grads):
@@ -441,6 +479,9 @@ def tbptt_goldens(name, B, T, n_steps, seed, lr=1e-3, sampled=False, tag=None, a
             [r.hidden_states[rnn].numpy() for r in rp.rows], 1)
     print('tbptt %s losses' % name, losses)
     save('tbptt_' + (tag or name), **out)
+
+
+NPERT = 6
 
 
 def _tbptt_run(cfg, w, B, T, n_steps, lr, seed):

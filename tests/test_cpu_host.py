@@ -215,3 +215,10 @@ def test_plugin_schedule_matches_reference():
         if it % 4 == 0:
             tr.call_plugins('epoch', it // 4)
     assert np.array_equal(np.array(log, dtype=np.int64), golden('plugin_order')['log'])
+
+
+def test_gpu_fixture_is_defined():
+    """Every GPU test takes the session fixture `hip` from conftest.py (it fails loudly when the
+    HIP library cannot load): guard against losing it."""
+    import conftest
+    assert hasattr(conftest, 'hip') and callable(conftest.genlong_noise)

@@ -218,7 +218,7 @@ def test_fence_waits_every_pending_reduction_and_unregisters():
 def test_bucket_offsets_aligned():
     import distributed as D
     ps = [torch.nn.Parameter(torch.zeros(n)) for n in (3, 64, 65, 1)]
-    offs, total = D.GradAllReduce._offsets(ps)
+    offs, total = D.GradAllReduce(zero=False)._offsets(ps)
     assert offs == [0, 64, 128, 256] and total == 320
 
 

@@ -31,7 +31,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, name, overlap, q):
+def _worker(rank, world, port, name, overlap, zero, q):
     try:
         sys.path[:0] = [HERE, os.path.join(HERE, 'golden'),
                         os.path.join(os.path.dirname(HERE),
@@ -53,7 +53,7 @@ def _worker(rank, world, port, name, overlap, q):
         m, pred = build(cfg, recipe.make_weights(cfg, int(g['weight_seed'])))
         B = int(g['B'])
         rows = D.shard_rows(B)
-        sync = D.GradAllReduce(bucket_mb=0.01,
+        sync = D.GradAllReduce(bucket_mb=0.01, zero=zero,
                                overlap_groups=D.readiness_groups(pred) if overlap else None)
         opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=float(g['lr'])),
                                       grad_sync=sync)
@@ -85,15 +85,18 @@ def _worker(rank, world, port, name, overlap, q):
         raise
 
 
-@pytest.mark.parametrize('overlap', [True, False])
-def test_dp_two_ranks_match_reference_full_batch(hip, overlap):
+@pytest.mark.parametrize('overlap,zero', [(True, True), (False, True), (True, False),
+                                          (False, False)])
+def test_dp_two_ranks_match_reference_full_batch(hip, overlap, zero):
+    """zero: ZeRO-1 (each rank clamps + updates its shard of the summed gradient, then the
+    parameters are all-gathered) or the replicated update after an all-reduce."""
     from conftest import golden
     name = 't3'
     g = golden('tbptt_' + name)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, overlap, q))
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, name, overlap, zero, q))
              for r in range(2)]
     for p in procs:
         p.start()
@@ -117,7 +120,7 @@ def test_dp_two_ranks_match_reference_full_batch(hip, overlap):
         np.testing.assert_array_equal(got[0][1][k], got[1][1][k], err_msg=k)
 
 
-def _flag_worker(rank, world, port, overlap, dtype, q):
+def _flag_worker(rank, world, port, overlap, dtype, zero, q):
     """Rank 0 raises its persistent-sweep failure flag before a step: the flag rides in the
     last gradient bucket, so BOTH ranks' fused clip+Adam skip the update (weights and moments
     unchanged) and both ranks' checks raise (distributed.py, persist.hip)."""
@@ -140,7 +143,7 @@ def _flag_worker(rank, world, port, overlap, dtype, q):
         cfg = recipe.CONFIGS['t3']
         m, pred = build(cfg, recipe.make_weights(cfg, int(g['weight_seed'])))
         rows = D.shard_rows(int(g['B']))
-        sync = D.GradAllReduce(bucket_mb=0.01, grad_dtype=dtype,
+        sync = D.GradAllReduce(bucket_mb=0.01, grad_dtype=dtype, zero=zero,
                                overlap_groups=D.readiness_groups(pred) if overlap else None)
         opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3),
                                       grad_sync=sync)
@@ -207,8 +210,9 @@ def _spawn(target, extra, world=2, timeout=150):
 
 @pytest.mark.parametrize('overlap', [True, False])
 @pytest.mark.parametrize('dtype', ['fp32', 'bf16'])
-def test_dp_failure_flag_skips_every_rank(hip, overlap, dtype):
-    got = _spawn(_flag_worker, (overlap, dtype))
+@pytest.mark.parametrize('zero', [True, False])
+def test_dp_failure_flag_skips_every_rank(hip, overlap, dtype, zero):
+    got = _spawn(_flag_worker, (overlap, dtype, zero))
     for rank in (0, 1):
         unchanged, raised = got[rank]
         assert unchanged, 'rank %d moved its weights / moments on a failed step' % rank
@@ -221,7 +225,7 @@ def _bf16_bucket_worker(rank, world, port, q):
     tolerance of the reference's full-batch fp32 trajectory."""
     try:
         os.environ['SRNN_DP_GRAD_DTYPE'] = 'bf16'
-        _worker(rank, world, port, 't3', True, q)
+        _worker(rank, world, port, 't3', True, True, q)
     except Exception:
         raise
 
@@ -303,3 +307,95 @@ def test_sharded_generation_reproduces_single_process(hip, name, dtype, sampler)
     full = got[0][1]
     for rank in (0, 1):
         assert np.array_equal(got[rank][0], full), rank
+
+
+def _graph_dp_worker(port, q):
+    """ONE rank over nccl (RCCL) with the bucket path forced (SRNN_DP_FORCE=1) and graph mode
+    under DP (SRNN_GRAPH_DP=1): the Trainer captures the whole data-parallel step -- the
+    reduce-scatters, the sharded clamp + Adam and the parameter all-gathers of ZeRO-1 --
+    into the HIP graph and replays it.  Returns the losses, the final parameters and the
+    number of replayed steps; the caller compares them with a plain single-process run."""
+    try:
+        sys.path[:0] = [HERE, os.path.join(HERE, 'golden'),
+                        os.path.join(os.path.dirname(HERE),
+                                     'jalil-saboorizadeh-multi-speaker-neural-vocoder_amd')]
+        os.environ.update(SRNN_DP_FORCE='1', SRNN_GRAPH_DP='1')
+        import torch.distributed as dist
+        torch.cuda.set_device(0)
+        dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % port, rank=0,
+                                world_size=1, device_id=torch.device('cuda', 0))
+        out = _run_graph_steps(dp=True)
+        q.put(out + (None,))
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((None, None, None, traceback.format_exc()))
+        raise
+
+
+def _run_graph_steps(dp):
+    import distributed as D
+    import nn as snn
+    import optim
+    import recipe
+    import samplernn_hip as H
+    from conftest import golden
+    from test_gpu_parity import build
+    from trainer import Trainer
+    H.lib()
+    g = golden('tbptt_t3')
+    cfg = recipe.CONFIGS['t3']
+    m, pred = build(cfg, recipe.make_weights(cfg, int(g['weight_seed'])), torch.bfloat16)
+    sync = D.GradAllReduce(bucket_mb=0.01, overlap_groups=D.readiness_groups(pred)) if dp \
+        else None
+    opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3), grad_sync=sync)
+    B = int(g['B'])
+    losses = []
+    criterion = snn.sequence_nll_loss_bits      # (graph mode captures only the bits loss)
+    dev = 'cuda'
+    chunks = [(torch.from_numpy(g['input_%d' % s]).to(dev),
+               torch.tensor([int(g['reset_%d' % s])] * B),
+               torch.from_numpy(g['target_%d' % s]).to(dev),
+               torch.from_numpy(g['cond_%d' % s]).to(dev),
+               torch.from_numpy(g['spk_%d' % s]).to(dev)) for s in range(3)]
+    # reset chunk, then 5 carried chunks: the carried kind is captured on its 2nd occurrence
+    data = [chunks[0]] + [(c[0], torch.zeros(B, dtype=torch.long)) + c[2:]
+                          for c in (chunks[1], chunks[2]) * 3][:5]
+
+    class _Loss:
+        trigger_interval = [(1, 'iteration')]
+
+        def register(self, tr):
+            pass
+
+        def iteration(self, it, inp, tgt, out, loss):
+            losses.append(float(loss))
+    tr = Trainer(pred, criterion, opt, data, True, None)
+    tr.register_plugin(_Loss())
+    tr.run(1)
+    torch.cuda.synchronize()
+    H.check_persistent_errors()
+    # (numpy, not tensors: CPU tensors sent through a multiprocessing queue are shared by
+    #  file descriptor, which dies with the worker)
+    params = {k: p.detach().cpu().numpy().copy() for k, p in pred.named_parameters()}
+    return losses, params, tr.graph_steps
+
+
+def test_graph_captured_dp_step_over_rccl(hip):
+    """The data-parallel step (ZeRO-1 reduce-scatter / sharded Adam / all-gather over RCCL)
+    captured in the HIP graph and replayed equals the single-process bf16 step bit for bit
+    (one rank: the SUM of one shard is the gradient itself, scale 1)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_graph_dp_worker, args=(_free_port(), q))
+    p.start()
+    losses, params, replays, err = q.get(timeout=150)
+    p.join(timeout=30)
+    assert err is None, err
+    assert p.exitcode == 0
+    assert replays >= 3, replays
+    ref_losses, ref_params, ref_replays = _run_graph_steps(dp=False)
+    assert ref_replays >= 3
+    assert losses == ref_losses
+    for k in ref_params:
+        np.testing.assert_array_equal(params[k], ref_params[k], err_msg=k)

@@ -157,36 +157,30 @@ def test_log_space_draw_equals_ratio_draw_on_goldens(name):
 
 @pytest.mark.parametrize('name', ['a', 'big'])
 def test_oracle_tbptt_sampled(name):
-    """3 TBPTT chunks through the oracle vs the reference's Trainer at T = 1024: losses 2e-5,
-    step 0 strict, later steps within the reference's own measured drift (conftest.DRIFT)."""
-    from conftest import assert_sampled_close, DRIFT
+    """3 TBPTT chunks through the oracle vs the reference's Trainer at T = 1024: losses,
+    hidden states, gradients and final parameters within 3x the reference's own distance
+    under a one-ulp weight perturbation plus the strict tolerances (conftest.within_floor)."""
+    from conftest import within_floor, within_floor_sampled
     g = golden('tbptt_' + name)
     cfg = recipe.CONFIGS[name]
     m = O.from_state_dict(cfg, recipe.make_weights(cfg, int(g['weight_seed'])))
     names = [str(s) for s in g['names']]
     opt = O.OracleAdam([m.p[k] for k in names], lr=float(g['lr']))
-    hid_tol = (2e-6, 1e-4, 3e-2)
+    losses = []
     for s in range(int(g['n_steps'])):
         batch = (torch.from_numpy(g['input_%d' % s]), bool(g['reset_%d' % s]),
                  torch.from_numpy(g['target_%d' % s]), torch.from_numpy(g['cond_%d' % s]),
                  torch.from_numpy(g['spk_%d' % s]))
         loss, grads = O.tbptt_step(m, opt, names, batch)
-        assert abs(loss - g['losses'][s]) < 2e-5
+        losses.append(loss)
         for k, gr in zip(names, grads):
-            if s == 0:
-                assert_sampled_close(gr.numpy(), g, 'grad_0', k, atol=2e-5, rtol=1e-4,
-                                     max_rel_l2=1e-5)
-            else:
-                assert_sampled_close(gr.numpy(), g, 'grad_%d' % s, k, atol=1e-4, rtol=1e-3,
-                                     max_viol=DRIFT['grad_viol'], max_abs=DRIFT['grad_max'],
-                                     max_rel_l2=DRIFT['grad_rel_l2'])
+            within_floor_sampled(gr.numpy(), g, 'grad_%d' % s, k, 2e-5, 1e-4)
         for t in range(len(cfg['frame_sizes'])):
-            np.testing.assert_allclose(m.hidden[t].numpy(), g['hidden_%d_tier%d' % (s, t)],
-                                       atol=hid_tol[s], rtol=0)
+            key = 'hidden_%d_tier%d' % (s, t)
+            within_floor(m.hidden[t].numpy(), g[key], g, key, 2e-6)
+    within_floor(losses, g['losses'], g, 'losses', 2e-5)
     for k in names:
-        assert_sampled_close(m.p[k].detach().numpy(), g, 'param_final', k, atol=2e-4, rtol=0,
-                             max_viol=DRIFT['param_viol'], max_abs=DRIFT['param_max'],
-                             max_rel_l2=DRIFT['param_rel_l2'])
+        within_floor_sampled(m.p[k].detach().numpy(), g, 'param_final', k, 1e-4)
 
 
 def test_oracle_forward_a():
@@ -222,24 +216,18 @@ def test_log_space_draw_near_tie_rate_long():
 
 
 @pytest.mark.parametrize('name', ['a', 'big'])
-def test_reference_self_drift_within_bounds(name):
-    """The later-chunk tolerances (conftest.DRIFT) cover the reference's drift from ITSELF
-    (the same trajectory at 1 vs 8 threads, recorded by make_golden.py)."""
-    from conftest import assert_sampled_close, DRIFT
+def test_reference_thread_drift_within_floor(name):
+    """The reference rerun at 1 thread (MKL reduction order changed, alt_* keys) stays within
+    the floor the one-ulp perturbations set: they are the larger rounding-level disturbance,
+    so they are the one the tolerances are built on."""
+    from conftest import within_floor
     g = golden('tbptt_' + name)
     names = [str(s) for s in g['names']]
-    np.testing.assert_allclose(g['alt_losses'], g['losses'], atol=1e-4, rtol=0)
+    within_floor(g['alt_losses'], g['losses'], g, 'losses', 1e-4)
     for s in range(1, int(g['n_steps'])):
         for k in names:
-            a = g['smp_alt_grad_%d/%s' % (s, k)]
-            # the alt run's sample stands in for the full tensor (same indices); its L2
-            # norm is checked from the stored value
-            r = g['smp_grad_%d/%s' % (s, k)]
-            d = np.abs(a.astype(np.float64) - r)
-            assert (d > 1e-4 + 1e-3 * np.abs(r)).mean() <= DRIFT['grad_viol']
-            assert d.max() <= DRIFT['grad_max']
-            l2, l2a = float(g['l2_grad_%d/%s' % (s, k)]), float(g['l2_alt_grad_%d/%s' % (s, k)])
-            assert abs(l2 - l2a) <= DRIFT['grad_rel_l2'] * l2 + 1e-4
+            key = 'grad_%d/%s' % (s, k)
+            within_floor(g['smp_alt_' + key], g['smp_' + key], g, key, 1e-4, 1e-3)
     for k in names:
-        d = np.abs(g['smp_alt_param_final/' + k].astype(np.float64) - g['smp_param_final/' + k])
-        assert (d > 2e-4).mean() <= DRIFT['param_viol'] and d.max() <= DRIFT['param_max']
+        key = 'param_final/' + k
+        within_floor(g['smp_alt_' + key], g['smp_' + key], g, key, 2e-4)

@@ -18,6 +18,9 @@ def main():
     ap.add_argument('first', type=int)
     ap.add_argument('last', type=int)
     ap.add_argument('--marker', default='adam_clip_multi_kernel')
+    ap.add_argument('--sequence', action='store_true',
+                    help='also list step FIRST kernel by kernel (start offset, duration)')
+    ap.add_argument('--span', type=int, default=1, help='steps the sequence covers')
     a = ap.parse_args()
     c = sqlite3.connect(a.db)
     rows = list(c.execute('select name, start, end from kernels order by start'))
@@ -42,6 +45,15 @@ def main():
     for k, (cnt, tot) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
         print('%-90s %8.1f %10.4f %10.2f %5.1f%%' % (k, cnt / n, tot / n / 1e6, tot / cnt / 1e3,
                                                     100.0 * tot / wall))
+    if a.sequence:
+        s0 = marks[a.first - 1][2] if a.first > 0 else rows[0][1]
+        s1 = marks[a.first + a.span - 1][2]
+        print('\n# steps %d..%d in launch order: start offset us, duration us, kernel'
+              % (a.first, a.first + a.span - 1))
+        for name, s, e in rows:
+            if s0 <= s and e <= s1:
+                print('%9.1f %8.1f  %s' % ((s - s0) / 1e3, (e - s) / 1e3,
+                                          name.split('(')[0].replace('void ', '')[:100]))
 
 
 if __name__ == '__main__':
