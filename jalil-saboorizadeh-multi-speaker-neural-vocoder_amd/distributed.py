@@ -474,6 +474,19 @@ class GradAllReduce:
                 H.shadow_refreshed(p)
 
 
+def zero_pieces(numels, offs, s0, S):
+    """ZeRO-1 shard map of one bucket: the parameters at flat offsets `offs` (numels
+    elements each) intersected with this rank's shard [s0, s0 + S) of the flat index space ->
+    [(parameter index, first element, end element, offset into the shard)].  Every element
+    of every parameter lies in exactly one rank's shard (tests/test_distributed_cpu.py)."""
+    out = []
+    for i, (n, o) in enumerate(zip(numels, offs)):
+        a, b = max(o, s0), min(o + n, s0 + S)
+        if b > a:
+            out.append((i, a - o, b - o, a - s0))
+    return out
+
+
 def _flag_to(dst):
     """dst (1-element fp32 / bf16 device tensor) = this rank's persistent-sweep failure flag."""
     import samplernn_hip as H

@@ -77,12 +77,11 @@ def _fused_adam_step(optimizer, lo, hi, reduced=None, dsteps=None):
     if zero:
         # ZeRO-1 (distributed.GradAllReduce): this rank updates only its shard of each bucket;
         # pieces[id(p)] = [(a, b, gradient view)] -- elements [a, b) of p and their reduced sums
+        import distributed as Dd
         pieces = {}
         for _, key, bucket, offs, s0, S, sh in reduced[1]:
-            for p, o in zip(bucket, offs):
-                a, b = max(o, s0), min(o + p.numel(), s0 + S)
-                if b > a:
-                    pieces.setdefault(id(p), []).append((a - o, b - o, sh[a - s0:b - s0]))
+            for i, a, b, so in Dd.zero_pieces([p.numel() for p in bucket], offs, s0, S):
+                pieces.setdefault(id(bucket[i]), []).append((a, b, sh[so:so + b - a]))
         zero_shadows = []
         rv = None
         gscale = reduced[3]

@@ -243,3 +243,29 @@ def test_ready_buckets_wait_for_the_next_sweep():
     assert launched == [(0, 0)] and sync._deferred == [1]
     sync.close()
     assert sync._after_ref is None
+
+
+@pytest.mark.parametrize('world', [1, 2, 3, 8])
+def test_zero_shards_cover_every_element_once(world):
+    """ZeRO-1's shard map (distributed.zero_pieces over GradAllReduce's 64-aligned, world-padded
+    bucket layout): across the ranks every element of every parameter is updated exactly once,
+    pieces start 64-element aligned (16-B vector access in the fused Adam), and each piece's
+    gradient offset points at the same flat element."""
+    import distributed as D
+    sizes = [3, 64, 65, 1, 1000, 4096, 7]
+    ps = [torch.nn.Parameter(torch.zeros(n)) for n in sizes]
+    # the bucket layout GradAllReduce._offsets builds for a ZeRO bucket: 64-aligned offsets,
+    # total padded to a multiple of 64 x world (the padding step needs device parameters
+    # there, so it is restated here)
+    offs, raw = D.GradAllReduce(zero=False)._offsets(ps)
+    q = 64 * world
+    total = (raw + q - 1) // q * q
+    assert total % (64 * world) == 0
+    S = total // world
+    seen = [torch.zeros(n, dtype=torch.int32) for n in sizes]
+    for r in range(world):
+        for i, a, b, so in D.zero_pieces(sizes, offs, r * S, S):
+            assert a % 64 == 0 or a == 0
+            assert offs[i] + a == r * S + so          # gradient view = the same flat element
+            seen[i][a:b] += 1
+    assert all(bool((x == 1).all()) for x in seen)
