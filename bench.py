@@ -174,7 +174,7 @@ def run_tbptt(dev, dist_mod, rows, steps, warmup, dtype, probe=True):
     m, pred = make_model(dtype)
     pred = pred.to(dev)
     sync = dist_mod.GradAllReduce(overlap_groups=dist_mod.readiness_groups(pred)) \
-        if dist_mod.world() > 1 else None
+        if dist_mod.world() > 1 or os.environ.get('SRNN_DP_FORCE', '0') == '1' else None
     opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3), grad_sync=sync)
     n_probe = min(steps, 5) if probe else 0
     batches = gpu_batches(synth_batches(rows, T, L, warmup + steps + n_probe,

@@ -45,13 +45,17 @@ def device_index():
 def init(backend=None):
     """Initialise the process group from torchrun's env (no-op for a single process).
     Backend: 'nccl' (= RCCL on ROCm) when GPUs are present, else 'gloo';
-    SRNN_DIST_BACKEND overrides (e.g. gloo for a rehearsal on one GPU)."""
-    if world() <= 1 or (dist.is_available() and dist.is_initialized()):
+    SRNN_DIST_BACKEND overrides (e.g. gloo for a rehearsal on one GPU); SRNN_DP_FORCE=1 also
+    builds a one-rank group (the DP step's collectives measured on a one-GPU box)."""
+    if (world() <= 1 and os.environ.get('SRNN_DP_FORCE', '0') != '1') or \
+            (dist.is_available() and dist.is_initialized()):
         return
     if backend is None:
         backend = os.environ.get('SRNN_DIST_BACKEND') or \
             ('nccl' if torch.cuda.device_count() > 0 else 'gloo')
     os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    for k, v in (('RANK', '0'), ('WORLD_SIZE', '1'), ('MASTER_PORT', '29533')):
+        os.environ.setdefault(k, v)             # a forced one-rank group outside torchrun
     if backend == 'nccl':
         torch.cuda.set_device(device_index())
         dist.init_process_group(backend, device_id=torch.device('cuda', device_index()))

@@ -244,11 +244,22 @@ def gradient_clipping(optimizer, min=-1, max=1, grad_sync=None):
         # ---- graph mode (trainer/__init__.py): the step replayed from a captured graph
         def graph_ready(self):
             """True when the step can be captured: the fused path with device step counters
-            whose groups each share one step count, no data-parallel gradient hook (its
-            collectives run on side streams) unless SRNN_GRAPH_DP=1."""
+            whose groups each share one step count.  Under data parallelism the collectives
+            are captured too (RCCL supports stream capture; tests/test_gpu_distributed.py
+            test_graph_captured_dp_step_over_rccl) when the process group is 'nccl' -- gloo's
+            host-side collectives cannot be -- unless SRNN_GRAPH_DP=0."""
             if not self._fused() or self.dsteps is None or not self.dsteps.uniform:
                 return False
-            return self.grad_sync is None or os.environ.get('SRNN_GRAPH_DP', '0') == '1'
+            if self.grad_sync is None:
+                return True
+            mode = os.environ.get('SRNN_GRAPH_DP', 'auto')
+            if mode == '0':
+                return False
+            if mode == '1':
+                return True
+            import torch.distributed as dist
+            return dist.is_available() and dist.is_initialized() and \
+                dist.get_backend() == 'nccl'
 
         def graph_signature(self):
             """What a captured step baked in: hyper-parameters (kernel arguments) and the

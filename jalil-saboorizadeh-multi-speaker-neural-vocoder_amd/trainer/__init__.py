@@ -22,8 +22,9 @@ replayed, later ones replay.  The batch is copied into static input buffers and 
 hidden state lives in static buffers the graph reads and rewrites; the Adam step count is
 read from a device counter (optim.DeviceSteps) so replays keep the bias correction exact.
 Anything a captured step cannot honour falls back to the eager step: roofline probes on
-(bench.py's per-kernel timing), a data-parallel gradient hook (unless SRNN_GRAPH_DP=1), a
-model without the Predictor's hidden-state carry, and any criterion other than the
+(bench.py's per-kernel timing), a data-parallel gradient hook over gloo (RCCL collectives
+are captured; SRNN_GRAPH_DP=0 keeps any DP step eager), a model without the Predictor's
+hidden-state carry, and any criterion other than the
 reference's `nn.sequence_nll_loss_bits` (user code runs inside the capture and may
 synchronise, e.g. read the loss with .item(); SRNN_GRAPH=force captures it anyway, and a
 capture that fails rolls the step's host state back and runs it eagerly).  After a replay
