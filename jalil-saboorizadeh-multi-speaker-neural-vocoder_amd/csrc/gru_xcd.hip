@@ -70,12 +70,14 @@ struct GruXArgs {
                                                     // invalid): 1 no output stores, 2 no gi loads
 };
 
-template <int UPW, int MT>
+// DC: D at compile time (0: a.D) -- at D = 1024 the unit-validity selects and the hand-off
+// offsets fold to constants (245 -> 186-226 VGPRs, no scalar spills at MT = 2 / 4)
+template <int UPW, int MT, int DC = 0>
 __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     using namespace gx;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int D = a.D, B = a.B, RV = a.RV;
+    const int D = DC ? DC : a.D, B = a.B, RV = a.RV;
     const int NU = D / UK, KW = NW < NU ? NW : NU;
     // double-buffered by the (step, tile) parity: one barrier per (step, tile)
     float* red = (float*)smem;                                  // [2][KW][NT][4][PS]
@@ -555,7 +557,8 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
     using namespace gx;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int D = a.D, B = a.B, RV = a.RV;
+    constexpr int D = UPW * 64;                                 // the host picks UPW = D / 64
+    const int B = a.B, RV = a.RV;
     constexpr int KW = NW;                                      // NU' = D / 8 = UPW * NW
     constexpr int NTB = 2;
     float* red = (float*)smem;                                  // [2][KW][NTB][4][PS]
@@ -881,13 +884,16 @@ extern "C" int srnn_gru_xcd_fwd2(int dtype, int B, int D, int Fr, const float* g
         {gru_xcd_fwd_kernel<1, 1>, gru_xcd_fwd_kernel<1, 2>, gru_xcd_fwd_kernel<1, 4>},
         {gru_xcd_fwd_kernel<2, 1>, gru_xcd_fwd_kernel<2, 2>, gru_xcd_fwd_kernel<2, 4>},
         {gru_xcd_fwd_kernel<4, 1>, gru_xcd_fwd_kernel<4, 2>, gru_xcd_fwd_kernel<4, 4>}};
-    const FwdK k = ks[ui][mi];
-    static bool attr[3][3] = {};
-    if (!attr[ui][mi]) {
+    static const FwdK k1024[3] = {gru_xcd_fwd_kernel<4, 1, 1024>, gru_xcd_fwd_kernel<4, 2, 1024>,
+                                  gru_xcd_fwd_kernel<4, 4, 1024>};
+    const FwdK k = D == 1024 && env_flag("SRNN_GX_DC", 1) ? k1024[mi] : ks[ui][mi];
+    static bool attr[4][3] = {};
+    const int ai = k == ks[ui][mi] ? ui : 3;
+    if (!attr[ai][mi]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize,
                                            160 * 1024));
-        attr[ui][mi] = true;
+        attr[ai][mi] = true;
     }
     hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
     SRNN_LAUNCH_CHECK();

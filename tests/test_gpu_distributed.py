@@ -309,17 +309,17 @@ def test_sharded_generation_reproduces_single_process(hip, name, dtype, sampler)
         assert np.array_equal(got[rank][0], full), rank
 
 
-def _graph_dp_worker(port, q):
+def _graph_dp_worker(port, zero, q):
     """ONE rank over nccl (RCCL) with the bucket path forced (SRNN_DP_FORCE=1) and graph mode
     under DP (SRNN_GRAPH_DP=1): the Trainer captures the whole data-parallel step -- the
-    reduce-scatters, the sharded clamp + Adam and the parameter all-gathers of ZeRO-1 --
-    into the HIP graph and replays it.  Returns the losses, the final parameters and the
+    bucket all-reduces, or with zero the reduce-scatters, the sharded clamp + Adam and the
+    parameter all-gathers of ZeRO-1 -- into the HIP graph and replays it.  Returns the losses, the final parameters and the
     number of replayed steps; the caller compares them with a plain single-process run."""
     try:
         sys.path[:0] = [HERE, os.path.join(HERE, 'golden'),
                         os.path.join(os.path.dirname(HERE),
                                      'jalil-saboorizadeh-multi-speaker-neural-vocoder_amd')]
-        os.environ.update(SRNN_DP_FORCE='1', SRNN_GRAPH_DP='1')
+        os.environ.update(SRNN_DP_FORCE='1', SRNN_GRAPH_DP='1', SRNN_DP_ZERO='1' if zero else '0')
         import torch.distributed as dist
         torch.cuda.set_device(0)
         dist.init_process_group('nccl', init_method='tcp://127.0.0.1:%d' % port, rank=0,
@@ -381,13 +381,14 @@ def _run_graph_steps(dp):
     return losses, params, tr.graph_steps
 
 
-def test_graph_captured_dp_step_over_rccl(hip):
-    """The data-parallel step (ZeRO-1 reduce-scatter / sharded Adam / all-gather over RCCL)
-    captured in the HIP graph and replayed equals the single-process bf16 step bit for bit
-    (one rank: the SUM of one shard is the gradient itself, scale 1)."""
+@pytest.mark.parametrize('zero', [False, True])
+def test_graph_captured_dp_step_over_rccl(hip, zero):
+    """The data-parallel step (bucket all-reduces, or ZeRO-1's reduce-scatter / sharded Adam /
+    all-gather, over RCCL) captured in the HIP graph and replayed equals the single-process
+    bf16 step bit for bit (one rank: the SUM of one shard is the gradient itself, scale 1)."""
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    p = ctx.Process(target=_graph_dp_worker, args=(_free_port(), q))
+    p = ctx.Process(target=_graph_dp_worker, args=(_free_port(), zero, q))
     p.start()
     losses, params, replays, err = q.get(timeout=150)
     p.join(timeout=30)

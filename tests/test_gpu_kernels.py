@@ -395,6 +395,37 @@ def test_gru_xcd_layouts_bit_identical(hip, D):
             assert torch.equal(a, b[r0:r0 + n]), (r0, n, i)
 
 
+@pytest.mark.parametrize('B', [512, 256, 128])
+def test_gru_xcd_fwd_compile_time_d_bit_identical(hip, B, monkeypatch):
+    """The D = 1024 forward instantiations (D at compile time, gru_xcd_fwd_kernel<4, MT,
+    1024>, the training path's) give the runtime-D kernel's bits at every tile count."""
+    T = torch.bfloat16
+    D, Fr = 1024, 7
+    g = torch.Generator().manual_seed(B + 11)
+    whh = (torch.randn(3 * D, D, generator=g) * 0.03).to(DEV, T)
+    bhh = (torch.randn(3 * D, generator=g) * 0.1).to(DEV)
+    gi = (torch.randn(B, Fr, 3 * D, generator=g) * 0.5).to(DEV)
+    h0 = (torch.randn(B, D, generator=g) * 0.5).to(DEV)
+    nf = hip.gru_xcd_work_bytes(T, B, D)
+    outs = []
+    for dc in ('1', '0'):
+        monkeypatch.setenv('SRNN_GX_DC', dc)
+        wf = torch.empty(nf, device=DEV, dtype=torch.uint8)
+        out = torch.empty((B, Fr, D), device=DEV)
+        outT = torch.empty((B, Fr, D), device=DEV, dtype=T)
+        gt = torch.empty((B, Fr, 4 * D), device=DEV)
+        hp = torch.empty((B, Fr, D), device=DEV, dtype=T)
+        hip.lib().call('srnn_gru_xcd_fwd2', hip.BF16, B, D, Fr, hip.ptr(gi), Fr * 3 * D, 3 * D,
+                       hip.ptr(h0), hip.ptr(whh), hip.ptr(bhh), hip.ptr(out), hip.ptr(outT),
+                       Fr * D, D, hip.ptr(gt), Fr * 4 * D, 4 * D, hip.ptr(hp), hip.ptr(wf), nf,
+                       hip.stream())
+        torch.cuda.synchronize()
+        assert hip.lib().dll.srnn_gru_xcd_error(hip.ptr(wf)) == 0
+        outs.append([x.cpu() for x in (out, outT, gt, hp)])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize('B,D,Fr', [(128, 1024, 16), (64, 1024, 5), (100, 256, 9)])
 def test_gru_seq_bwd_matches_steps(hip, B, D, Fr):
     """Persistent whole-sequence GRU backward == Fr per-step backward launches, bit for bit."""

@@ -2,6 +2,9 @@
 being off under DP): cProfile over eager Trainer.train chunks at ROWS rows.
 
   SRNN_GRAPH=0 python tools/host_prof.py [rows] [steps]  > gpurun_out/host_prof.txt
+
+SRNN_DP_FORCE=1 adds the data-parallel gradient hook over a one-rank RCCL group (as
+bench.py does); SRNN_GRAPH=1 profiles the graph replays instead of eager steps.
 """
 import cProfile
 import io
@@ -28,7 +31,12 @@ def main():
     dev = torch.device('cuda', 0)
     m, pred = bench.make_model(torch.bfloat16)
     pred = pred.to(dev)
-    opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3))
+    sync = None
+    if os.environ.get('SRNN_DP_FORCE', '0') == '1':
+        import distributed as D
+        D.init()
+        sync = D.GradAllReduce(overlap_groups=D.readiness_groups(pred))
+    opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3), grad_sync=sync)
     batches = bench.gpu_batches(bench.synth_batches(rows, bench.T_SEQ, 64, 3 + steps, 0), dev)
     tr = Trainer(pred, snn.sequence_nll_loss_bits, opt, batches[:3], True, None)
     tr.train()
