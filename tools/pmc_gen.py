@@ -46,7 +46,7 @@ def main(fdb, wdb):
     steps = 16 * launches
     tot = 0.0
     print('# HBM traffic of the generation loop (bf16, B = 128, D = 1024, FS = [16, 4]), '
-          'tools/gen_prof.py 128 20 under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE')
+          'tools/gen_prof.py bf16 20 under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE')
     print('# kernel  dispatches  FETCH kB x2  WRITE kB  (totals over the run)')
     for k in sorted(set(f) | set(w)):
         nf, sf = f.get(k, (0, 0.0))

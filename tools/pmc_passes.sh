@@ -7,7 +7,7 @@ out=${1:-gpurun_out/pmc}
 R=$PWD
 mkdir -p $out
 export TMPDIR=/tmp
-gen="python3 $R/tools/gen_prof.py 128 8 1 bf16"
+gen="python3 $R/tools/gen_prof.py bf16 8"
 tb="python3 $R/bench.py --steps 2 --warmup 1 --no-gen --no-cpu"
 timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d $R/$out/gen_fetch -o run -- $gen > $R/$out/gen_fetch.log 2>&1
 timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d $R/$out/gen_write -o run -- $gen > $R/$out/gen_write.log 2>&1
