@@ -191,8 +191,12 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
                 // (row l & 15, k = 32 u + 8 (l >> 4) + 0..3) at l * 16 and its second at
                 // 1 KiB + l * 16, so each poll instruction reads 1 KiB of whole lines (the
                 // row-major image took 16 half lines per instruction)
+                // (RV < 16, B < 128: a lane of a padding row -- lrow >= RV, never stored --
+                //  reads nothing: its offset is past the buffer's range, so the load returns
+                //  zeros without a memory access, and the poll moves RV / 16 of the bytes)
                 const uint32_t base = (uint32_t)(((size_t)(t & 1) * bufw +
-                                                  (size_t)(g * MT + m) * RG * DG) * 8) + lane * 16u;
+                                                  (size_t)(g * MT + m) * RG * DG) * 8) +
+                                      (lrow < RV ? lane * 16u : 0x80000000u);
                 uint32_t w[UPW][4];
                 int spins = 0;
                 for (;;) {
@@ -215,6 +219,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
                         ok &= !v || ((x[j][0].y == tag) & (x[j][0].w == tag) &
                                      (x[j][1].y == tag) & (x[j][1].w == tag));
                     }
+                    ok |= lrow >= RV;
                     if (__all(ok)) break;
                     if (hx_spin_fail(spins, a.err, lane, a.poll_sleep, a.spin_limit)) break;
                 }
@@ -643,7 +648,9 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
             uint4 x[UPW];
             int spins = 0;
             // (made opaque per step, see the unpacked kernel)
-            uint32_t lb = (uint32_t)(wave * 64 + lane) * 16u;
+            // (a padding-row lane, lrow >= RV: out-of-range offset, zeros without a memory
+            //  access -- see the forward)
+            uint32_t lb = lrow < RV ? (uint32_t)(wave * 64 + lane) * 16u : 0x80000000u;
             asm volatile("" : "+v"(lb));
             for (;;) {
 #pragma unroll
@@ -653,6 +660,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
 #pragma unroll
                 for (int j = 0; j < UPW; ++j)
                     ok &= ((x[j].y >> 16) == tag) & ((x[j].w >> 16) == tag);
+                ok |= lrow >= RV;
                 if (__all(ok)) break;
                 if (hx_spin_fail(spins, a.err, lane, 1, a.spin_limit)) break;
             }
