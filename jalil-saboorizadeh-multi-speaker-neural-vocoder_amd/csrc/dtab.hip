@@ -286,8 +286,9 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
 // sample value q, the number of positions holding q (an accumulator entry (q, k, c) sums at
 // most count(q) terms); e = floor(log2(2^30 / (amax * max_q count(q)))) bounds every sum by
 // 2^30 + count/2.  Exact integer arithmetic, so the result is deterministic and independent
-// of the atomics' order, like the 2^-40 form; its resolution is relative to amax (2^-30 of
-// amax * max count per sum, orders of magnitude below the bf16 rounding of the output).
+// of the atomics' order, like the 2^-40 form; its resolution is absolute, 2^-(e+1) per term
+// (amax * max count / 2^31): below the bf16 rounding of terms near amax, not of small ones --
+// the bound and the gate that keeps it are below (DTAB_PK_CMAX).
 //
 // Lanes: (row half h, column pair p, row residue li); a wave walks TWO batch rows at once
 // (lanes 0-31 row b, 32-63 row b + 1), each half with its own broadcast index read, so one
