@@ -502,6 +502,15 @@ def main():
                 r, N, peak, 'the headline step with SRNN_BLASLT=0: every GEMM on the '
                 'hand-written gemm3 / gemm2 / skinny kernels, no vendor library kernel')
             log('handwritten_only: %.2f ms/step' % r['ms_per_step'])
+        if N > 1 and strong:
+            # weak scaling beside the strong-scaling headline: each rank keeps the N = 1 line's
+            # 512 rows (global batch 512 N), so per-GPU work is the headline's and only the
+            # all-reduce is added (scaling efficiency = this value / (N x the N = 1 value))
+            r = run_tbptt(dev, D, GLOBAL_B, args.steps, args.warmup, dtype, probe=False)
+            extra['weak_512'] = tbptt_summary(
+                r, N, peak, '512 rows per GPU x %d GPU (global batch %d, weak scaling)'
+                % (N, GLOBAL_B * N))
+            log('weak_512: %.2f ms/step' % r['ms_per_step'])
         if not (not strong and rows == 64) and not (strong and rows == 64):
             r = run_tbptt(dev, D, 64, args.steps, args.warmup, dtype)
             extra['weak_64'] = tbptt_summary(

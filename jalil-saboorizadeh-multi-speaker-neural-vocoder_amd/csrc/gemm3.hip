@@ -1196,6 +1196,16 @@ static int g3_mode() {
     return v;
 }
 
+static int g3_ncu() {
+    static int ncu = 0;
+    if (!ncu) {
+        int dev = 0;
+        SRNN_CHECK_HIP(hipGetDevice(&dev));
+        SRNN_CHECK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    return ncu;
+}
+
 template <typename TO, bool KCA, bool KCB, bool SW>
 static int launch3(const Gemm3Args& g, hipStream_t s) {
     // mode 0: 32-deep 5-slot ring; 1: 64-deep pair mode; 2 (default): pair mode when an
@@ -1203,7 +1213,15 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
     const int mode = g3_mode();
     const bool k64 = (g.K / g.ksplit) % g3p::BK == 0;
     const bool pp = mode == 3 && k64;
-    const bool q = mode == 4;
+    // mode 2 also takes the ring ping-pong for the NN shapes with enough tiles for two rounds
+    // (A k-contiguous, B n-contiguous, plain output): measured on the step's upsampling
+    // dX (32768 x 1024 x 16384: 1090 -> 900 us) and GRU dX (32768 x 1024 x 3072: 247 -> 204 us);
+    // at one round of tiles (8192 x 1024 x 3072 / 4096) the pair mode stays ahead
+    // (profiles/r04_gemm_modes_b512.txt)
+    const int units = (g.M / g3::BM) * (g.N / g3::BN) * g.ksplit;
+    const bool q = mode == 4 ||
+                   (mode == 2 && KCA && !KCB && g.ksplit == 1 && !g.mbi && !g.mbo && !g.amax &&
+                    !g.mask && units >= 2 * g3_ncu() && env_flag("SRNN_G3_NNQ", 1));
     const bool pair = !pp && !q && (mode == 1 || (mode == 2 && (KCA || KCB))) && k64;
     // unit-1 fragment prefetch (gemm3p PF): measured 14 % faster on the bf16 NT shapes (MLP
     // hidden forward, upsampling forward, B = 512), 3 % on NN; slower on the fp32-output NT
@@ -1235,13 +1253,7 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds));
         attr[ki] = true;
     }
-    static int ncu = 0;
-    if (!ncu) {
-        int dev = 0;
-        SRNN_CHECK_HIP(hipGetDevice(&dev));
-        SRNN_CHECK_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    const int units = (g.M / g3::BM) * (g.N / g3::BN) * g.ksplit;
+    const int ncu = g3_ncu();
     dim3 grid(units < ncu ? units : ncu);
     hipLaunchKernelGGL(k, grid, dim3(g3::NT), lds, s, g);
     SRNN_LAUNCH_CHECK();

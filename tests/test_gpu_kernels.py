@@ -93,6 +93,38 @@ def test_gemm3_256_kernel(hip, out_dtype, transA, transB, M, N, K, epi):
 
 
 @pytest.mark.parametrize('out_dtype', [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize('epi', ['plain', 'bias_relu', 'cin'])
+def test_gemm3_nn_ring_pingpong(hip, monkeypatch, out_dtype, epi):
+    """NN shapes with two rounds of 256x256 tiles take gemm3's ring ping-pong schedule
+    (gemm3q_kernel) on the hand-written path: the same MFMA order as the pair schedule
+    (SRNN_G3_NNQ=0), so the same bits, and the fp32 product of the bf16 operands."""
+    dtype = torch.bfloat16
+    M, N, K = 8192, 4096, 512                  # 32 x 16 = 512 tiles, K-contiguous A, N-major B
+    A, B = _rand(M, K, seed=1), _rand(K, N, seed=2)
+    Ad, Bd = A.to(DEV, dtype), B.to(DEV, dtype)
+    ref = Ad.float().cpu() @ Bd.float().cpu()
+    kw = dict(tile=5, out_dtype=out_dtype)
+    if epi == 'bias_relu':
+        bias = _rand(N, seed=3)
+        kw.update(bias=bias.to(DEV), relu=True)
+        ref = (ref + bias).clamp_min(0)
+    elif epi == 'cin':
+        cin = _rand(M, N, seed=4)
+        kw.update(cin=cin.to(DEV), beta=0.5)
+        ref = ref + 0.5 * cin
+
+    def run(q):
+        monkeypatch.setenv('SRNN_G3_NNQ', '1' if q else '0')
+        out = hip.gemm(Ad, Bd, **kw)
+        torch.cuda.synchronize()
+        return out.float().cpu()
+    q, pair = run(True), run(False)
+    assert torch.equal(q, pair)
+    tol = 2e-3 * np.sqrt(K) if out_dtype == torch.float32 else 1e-2 * np.sqrt(K)
+    torch.testing.assert_close(q, ref, atol=tol, rtol=1e-2)
+
+
+@pytest.mark.parametrize('out_dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('transA,transB', [(0, 0), (0, 1), (1, 0), (1, 1)])
 @pytest.mark.parametrize('M,N,K,epi', [(4096, 2048, 1024, 'bias_relu'), (2048, 4096, 1024, 'bias'),
                                        (4096, 1024, 2048, 'plain')])
