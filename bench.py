@@ -13,7 +13,11 @@ Default workload = configs[3]: global batch 512 stream rows sharded over the N r
 (512 / N rows per GPU, strong scaling; N = 1 is the whole 512-row batch on one GPU).  Beside
 it the line carries
   * `config_b` (N = 1): configs[1], 128 rows on one GPU;
+  * `handwritten_only` (N = 1, bf16): the headline step with every GEMM on the hand-written
+    kernels (SRNN_BLASLT=0);
   * `weak_64`: 64 rows per GPU (weak scaling at configs[3]'s 8-GPU share);
+  * `weak_512` (N > 1): 512 rows per GPU, global batch 512 N (weak scaling at the N = 1
+    headline's per-GPU work: only the all-reduce is added);
   * `roofline`: the step's DOMINANT kernel (largest time per step among the probed launch
     sites: GRU sweeps, dTab scatter, MLP hidden GEMM, fused clip + Adam), measured with HIP
     events on the launching stream around each launch over eager steps of the same run (a
