@@ -24,7 +24,7 @@ it the line carries
     replayed graph runs the same kernels); `kernels` lists every probed site;
     `step_mfma`: executed MFMA work of the whole step / step time / bf16 peak;
   * generation throughput of configs[2] (`gen` bf16 persistent loop, `gen_fp32` the reference
-    precision) and configs[4] (`gen_config_e`), rows sharded over ranks (each rank its
+    precision) and configs[4] (`gen_config_e`, `gen_config_e_fp32`), rows sharded over ranks (each rank its
     contiguous 1/N share of the utterances, no collective in the loop);
   * `cpu_baseline`: the oracle (torch-CPU restatement) on the host cores, bounded samples of
     the TBPTT step at configs[1]'s batch and of generation at configs[2]'s.
@@ -564,7 +564,7 @@ def main():
             line['roofline']['traffic'], line['roofline']['traffic_source'] = gen_traffic()
         return line
 
-    gen = gen_fp32 = gen_e = None
+    gen = gen_fp32 = gen_e = gen_e_fp32 = None
     if not args.no_gen:
         gen = gen_line(args.gen_dtype)
         if args.gen_dtype != 'fp32' and not args.no_gen_fp32:
@@ -574,6 +574,9 @@ def main():
             # GPUs = 128 per GPU, 188 cond rows x 256 = 48,128 samples each
             gen_e = gen_line(args.gen_dtype, (16, 4, 4), 86, 188,
                              '4-tier dim1024 FS=[16,4,4] look-ahead')
+            if args.gen_dtype != 'fp32' and not args.no_gen_fp32:
+                gen_e_fp32 = gen_line('fp32', (16, 4, 4), 86, 188,
+                                      '4-tier dim1024 FS=[16,4,4] look-ahead')
 
     cpu = None
     if D.rank() == 0 and N == 1 and not args.no_cpu:
@@ -594,7 +597,7 @@ def main():
                 'eager_host_enqueue_ms_per_step': summ['eager_host_enqueue_ms_per_step'],
                 'roofline': roof, 'kernels': ks, 'step_mfma': summ['step_mfma'],
                 'cpu_baseline': cpu, 'gen': gen, 'gen_fp32': gen_fp32,
-                'gen_config_e': gen_e, 'gru_sweep': gru,
+                'gen_config_e': gen_e, 'gen_config_e_fp32': gen_e_fp32, 'gru_sweep': gru,
                 'final_loss': summ['final_loss']}
         line.update(extra)
         print(json.dumps(line), flush=True)

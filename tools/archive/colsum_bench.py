@@ -6,7 +6,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..',
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', '..',
                                 'jalil-saboorizadeh-multi-speaker-neural-vocoder_amd'))
 import samplernn_hip as H  # noqa: E402
 

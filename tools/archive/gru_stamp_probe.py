@@ -2,13 +2,13 @@
 thread 0 stamps s_memrealtime after the poll, the MMA + reduction write, the barrier, the
 gate math + publish and the output stores of every (step, tile)); B = 512 (4 tiles per group)
 and B = 128, D = 1024, 64 frames, bf16.
-  SRNN_GRU_DIAG=1 python tools/gru_stamp_probe.py [B]"""
+  SRNN_GRU_DIAG=1 python tools/archive/gru_stamp_probe.py [B]"""
 import os
 import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, 'jalil-saboorizadeh-multi-speaker-neural-vocoder_amd'))
 import samplernn_hip as H  # noqa: E402
 

@@ -7,5 +7,5 @@ bash tools/gsteps.sh \
  "240 SRNN_GX_GPK=0 $B > gpurun_out/r04x_b512_0.json 2> gpurun_out/r04x_b512_0.err" \
  "240 $B --batch 64 > gpurun_out/r04x_b64.json 2> gpurun_out/r04x_b64.err" \
  "240 SRNN_GX_GPK=0 $B --batch 64 > gpurun_out/r04x_b64_0.json 2> gpurun_out/r04x_b64_0.err" \
- "150 SRNN_GRU_DIAG=1 python -u tools/gru_stamp_probe.py 512 > gpurun_out/r04x_gru512.txt 2>&1" \
- "150 SRNN_GRU_DIAG=1 python -u tools/gru_stamp_probe.py 128 > gpurun_out/r04x_gru128.txt 2>&1"
+ "150 SRNN_GRU_DIAG=1 python -u tools/archive/gru_stamp_probe.py 512 > gpurun_out/r04x_gru512.txt 2>&1" \
+ "150 SRNN_GRU_DIAG=1 python -u tools/archive/gru_stamp_probe.py 128 > gpurun_out/r04x_gru128.txt 2>&1"

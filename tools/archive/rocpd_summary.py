@@ -1,7 +1,7 @@
 """Summarise a rocprofv3 SQLite output (run_results.db, the ROCm 7.x default format).
 
-  python tools/rocpd_summary.py stats DB [N]          -> kernel_stats CSV (rocprofv3 --stats form)
-  python tools/rocpd_summary.py pmc DB NAME_SUBSTR    -> per-dispatch counter values of matching
+  python tools/archive/rocpd_summary.py stats DB [N]          -> kernel_stats CSV (rocprofv3 --stats form)
+  python tools/archive/rocpd_summary.py pmc DB NAME_SUBSTR    -> per-dispatch counter values of matching
                                                          kernels + their average (kB for *_SIZE)
 """
 import csv

@@ -1,14 +1,14 @@
 """Launch only the bench's dominant kernel (same shape/dtype/epilogue as bench.py's roofline
 leg) so that rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) see it in isolation.
 
-  rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run -- python tools/roofline_kernel.py
+  rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run -- python tools/archive/roofline_kernel.py
 """
 import os
 import sys
 
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
