@@ -206,6 +206,14 @@ int srnn_gemm_amax_taken(void);
  * output into blk[N / 4][M][4] (M x N bf16, caller-allocated); srnn_gemm_amax_taken()
  * then returns 2.  The dTab scatter's operand layout (srnn_mlp_dtab4).                   */
 int srnn_gemm_amax_blk_next(unsigned* amax, void* blk);
+/* Ask the next bf16-output GEMM that runs on the 256 x 256 gemm3 pair path (model.py:320's
+ * da2 = (dz W_out) * relu', whose column sums are the hidden layer's bias gradient,
+ * model.py:317's Conv1d bias) to also write the column sums of its stored bf16 output per
+ * 128-row block into part[M / 128][N] (fp32, caller-allocated; every entry written once, no
+ * zeroing needed); the caller sums the M / 128 rows.  srnn_gemm_csum_taken() returns 1 if a
+ * GEMM did since (host state; also clears a request no GEMM took).                        */
+int srnn_gemm_csum_next(float* part);
+int srnn_gemm_csum_taken(void);
 /* srnn_mlp_dtab3 with blk (device, may be NULL): the column-blocked copy of da
  * (blk[D / 4][B * Tlen][4], srnn_gemm_amax_blk_next) the packed form reads instead of da
  * (whole 128-B lines per load).  Same outputs bit for bit.  A sample histogram skewed past

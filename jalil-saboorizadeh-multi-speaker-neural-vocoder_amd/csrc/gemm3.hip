@@ -53,6 +53,10 @@ struct Gemm3Args {
     // optional (with amax): a column-blocked copy of the bf16 output, [N / 4][M][4] -- the
     // dTab scatter's operand (dtab.hip: one load instruction then reads whole lines)
     bf16* blk;
+    // optional (srnn_gemm_csum_next): column sums of the stored bf16 output per 128-row
+    // block, csp[M / 128][N] fp32 (each entry written once; the caller sums the blocks) --
+    // the bias gradient of the layer whose output gradient this GEMM produces
+    float* csp;
 };
 
 namespace g3 {
@@ -161,7 +165,7 @@ __device__ __forceinline__ void g3_store4(bf16* p, const float (&v)[4]) {
 // epilogue of one finished tile (registers -> C); zeroes the accumulators
 // AMX: also reduce max |C| into g.amax (its own instantiation: tracking the max in the
 // plain epilogue pushed the main loops past 256 VGPRs -- ~100 spilled)
-template <typename TO, bool SW, bool CIN, bool MB = false, bool AMX = false>
+template <typename TO, bool SW, bool CIN, bool MB = false, bool AMX = false, bool CS = false>
 __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
                                               int n0, int wm, int wn, int lane, int kb) {
     if constexpr (!SW) {
@@ -231,6 +235,13 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
     unsigned short* mbo = MB ? g.mbo : nullptr;
     const int g4 = (lane >> 4) * 4;
     unsigned amx = 0u;
+    float cs[CS ? 4 : 1][4];                   // CS: the lane's 16 columns summed over its rows
+    if constexpr (CS) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cs[j][e] = 0.f;
+    }
     // the mask in two halves of 16 fragments (register budget): two waits per tile
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -295,6 +306,10 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
                                        ((unsigned)__bfloat16_as_ushort(__float2bfloat16(v[2 * e + 1])) << 16);
                             if constexpr (AMX)
                                 amx = max(amx, max(pk[t][e] & 0x7fffu, (pk[t][e] >> 16) & 0x7fffu));
+                            if constexpr (CS) {        // the stored (bf16-rounded) values
+                                cs[j][2 * e] += __uint_as_float(pk[t][e] << 16);
+                                cs[j][2 * e + 1] += __uint_as_float(pk[t][e] & 0xffff0000u);
+                            }
                         }
                         if (mbo) {
                             // value > 0 of the stored bf16: 0x0001 .. 0x7f80 (no -0, no NaN)
@@ -383,6 +398,26 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
             }
         }
     }
+    if constexpr (CS) {
+        // sum over the 16 lanes of a DPP row (the wave's 16 rows of each i; every lane ends
+        // with a total, in a fixed order), then lane q of the row stores column (q >> 2) * 16
+        // + (q & 3) of its group: one 4-B store per lane, 64 columns per wave -- exactly one
+        // store more per tile (g3_epilogue's count)
+        float o = 0.f;
+        const int q = lane & 15;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float x = cs[j][e];
+                x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x128, 0xf, 0xf, false));
+                x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x124, 0xf, 0xf, false));
+                x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x122, 0xf, 0xf, false));
+                x += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x121, 0xf, 0xf, false));
+                o = (q == j * 4 + e) ? x : o;
+            }
+        g.csp[(int64_t)((m0 + wm * 128) / 128) * g.N + n0 + wn * 64 + g4 + (q >> 2) * 16 + (q & 3)] = o;
+    }
     if (AMX && g.amax) {
         // (one atomic per wave and tile, younger than the epilogue's stores: the callers'
         //  counted DMA waits then cover one store more than needed -- safe)
@@ -399,9 +434,14 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 // Returns the number of stores each wave issued (SW path): the main loops' counted DMA
 // waits leave exactly that many younger stores in flight, so the count must be exact -- a
 // larger allowance would let a stage's DMA pieces still be outstanding at the read.
-template <typename TO, bool SW, bool MB = false, bool AMX = false>
+template <typename TO, bool SW, bool MB = false, bool AMX = false, bool CS = false>
 __device__ __forceinline__ int g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
                                            int n0, int wm, int wn, int lane, int kb) {
+    if constexpr (CS && sizeof(TO) == 2 && SW) {
+        // the column-sum kernels (bf16 out, no Cin, no bit masks, no max |C|)
+        g3_epilogue_t<TO, SW, false, false, false, true>(g, acc, m0, n0, wm, wn, lane, kb);
+        return 17;
+    }
     if constexpr (AMX) {
         g3_epilogue_t<TO, SW, false, false, true>(g, acc, m0, n0, wm, wn, lane, kb);
         return g.blk ? 48 : 16;                    // + the blocked copy's 2 stores per store
@@ -683,7 +723,7 @@ __device__ __forceinline__ bf16x8 g3p_frag(const char* img, int f0, int u, int l
 // MFMAs run (3 reads after each of its last four MFMA rows), so the unit-1 MFMAs do not wait
 // for a burst of 12 LDS reads.
 template <typename TO, bool KCA, bool KCB, bool SW, bool MB = false, bool PF = false,
-          bool AMX = false>
+          bool AMX = false, bool CS = false>
 __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -791,7 +831,7 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
         if (++ktc == nk) {
             int m0, n0, kb;
             unit(ic, m0, n0, kb);
-            epi = (g.diag & 8) ? 0 : g3_epilogue<TO, SW, MB, AMX>(g, acc, m0, n0, wm, wn, lane, kb);
+            epi = (g.diag & 8) ? 0 : g3_epilogue<TO, SW, MB, AMX, CS>(g, acc, m0, n0, wm, wn, lane, kb);
             ktc = 0;
             ++ic;
         }
@@ -803,6 +843,7 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
         const char* img = smem + (s & 1) * g3p::SLOT;
         char* nimg = smem + ((s + 1) & 1) * g3p::SLOT;
         if (SW && epi == 16) g3_wait_vm<16>();
+        else if (SW && epi == 17) g3_wait_vm<17>();                        // + column sums
         else if (SW && epi == 18) g3_wait_vm<18>();                        // + mask bits
         else if (SW && epi == 48) g3_wait_vm<48>();                        // + blocked copy
         else if (SW && epi) g3_wait_vm<32>();
@@ -1219,9 +1260,9 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
     // at one round of tiles (8192 x 1024 x 3072 / 4096) the pair mode stays ahead
     // (profiles/r04_gemm_modes_b512.txt)
     const int units = (g.M / g3::BM) * (g.N / g3::BN) * g.ksplit;
-    const bool q = mode == 4 ||
+    const bool q = !g.csp && (mode == 4 ||
                    (mode == 2 && KCA && !KCB && g.ksplit == 1 && !g.mbi && !g.mbo && !g.amax &&
-                    !g.mask && units >= 2 * g3_ncu() && env_flag("SRNN_G3_NNQ", 1));
+                    !g.mask && units >= 2 * g3_ncu() && env_flag("SRNN_G3_NNQ", 1)));
     const bool pair = !pp && !q && (mode == 1 || (mode == 2 && (KCA || KCB))) && k64;
     // unit-1 fragment prefetch (gemm3p PF): measured 14 % faster on the bf16 NT shapes (MLP
     // hidden forward, upsampling forward, B = 512), 3 % on NN; slower on the fp32-output NT
@@ -1238,6 +1279,10 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
         if (g.mbi || g.mbo) {        // ReLU bit masks (srnn_gemm3_try admits modes 0-2 only)
             k = pair ? gemm3p_kernel<TO, KCA, KCB, SW, true> : gemm3_kernel<TO, KCA, KCB, SW, true>;
             ki += 4;
+        } else if (g.csp && pair) {   // column sums wanted (srnn_gemm_csum_next)
+            k = pf ? gemm3p_kernel<TO, KCA, KCB, SW, false, true, false, true>
+                   : gemm3p_kernel<TO, KCA, KCB, SW, false, false, false, true>;
+            ki = pf ? 12 : 11;
         } else if (g.amax && pair) {  // max |C| wanted (srnn_gemm_amax_next)
             // (SRNN_G3_AMX_PF: with the unit-1 fragment prefetch as well)
             const int amx_pf = env_flag("SRNN_G3_AMX_PF", 0);
@@ -1246,8 +1291,9 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
             ki = amx_pf ? 10 : 9;
         }
     }
+    SRNN_REQUIRE(!g.csp || pair, "gemm3: column sums need the pair-mode kernel");
     const int lds = (pp || pair) ? g3p::LDS : g3::LDS;
-    static bool attr[11] = {};
+    static bool attr[13] = {};
     if (!attr[ki]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -1318,6 +1364,31 @@ extern "C" int srnn_gemm_amax_blk_next(unsigned* amax, void* blk) {
     return 0;
 }
 
+// column-sum request for the next bf16-output GEMM that takes the gemm3 pair path
+static float*& g3_csum_pending() {
+    static float* p = nullptr;
+    return p;
+}
+static int& g3_csum_taken() {
+    static int t = 0;
+    return t;
+}
+
+int srnn_gemm_csum_pending() { return g3_csum_pending() != nullptr; }
+
+extern "C" int srnn_gemm_csum_next(float* part) {
+    g3_csum_pending() = part;
+    g3_csum_taken() = 0;
+    return 0;
+}
+
+extern "C" int srnn_gemm_csum_taken(void) {
+    const int t = g3_csum_taken();
+    g3_csum_pending() = nullptr;
+    g3_csum_taken() = 0;
+    return t;
+}
+
 extern "C" int srnn_gemm_amax_taken(void) {
     const int t = g3_amax_taken();
     g3_amax_pending() = nullptr;
@@ -1355,6 +1426,7 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     g.mbi = mbi; g.ldmbi = ldmbi; g.mbo = mbo; g.ldmbo = ldmbo;
     g.amax = nullptr;
     g.blk = nullptr;
+    g.csp = nullptr;
     const int tiles = (M / g3::BM) * (N / g3::BN);
     const bool plain = beta == 0.f && !bias && !relu && !mask && !mbi && !mbo &&
                        out_dtype == SRNN_F32;
@@ -1398,6 +1470,14 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
         g3_amax_pending() = nullptr;
         g3_blk_pending() = nullptr;
         g3_amax_taken() = g.blk ? 2 : 1;
+    }
+    // column sums (srnn_gemm_csum_next): the pair-mode kernels' plain bf16 epilogue only
+    // (no Cin, bit masks or max |C|); M % 128 == 0 holds here
+    if (g3_csum_pending() && !g.amax && beta == 0.f && !mbi && !mbo && (kca || kcb) &&
+        K % g3p::BK == 0 && (g3_mode() == 1 || g3_mode() == 2)) {
+        g.csp = g3_csum_pending();
+        g3_csum_pending() = nullptr;
+        g3_csum_taken() = 1;
     }
     return launch3_layout<bf16, true>(g, kca, kcb, s);
 }

@@ -56,3 +56,5 @@ int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int
                     hipStream_t s);
 // gemm3.hip: a max |C| request (srnn_gemm_amax_next) waits for the next bf16 gemm3 launch
 int srnn_gemm_amax_pending();
+// gemm3.hip: a column-sum request (srnn_gemm_csum_next) waits for the next bf16 gemm3 launch
+int srnn_gemm_csum_pending();

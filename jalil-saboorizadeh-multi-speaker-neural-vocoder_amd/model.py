@@ -34,7 +34,7 @@ import samplernn_hip as H
 
 verbose = False
 # (tests) how often a fused side result was consumed, and which recurrence kernels ran
-_STATS = {'fused_colsum': 0, 'fused_lp': 0, 'gru_xcd_fwd': 0, 'gru_xcd_bwd': 0, 'gru_seq': 0,
+_STATS = {'fused_colsum': 0, 'fused_lp': 0, 'csum_epi': 0, 'gru_xcd_fwd': 0, 'gru_xcd_bwd': 0, 'gru_seq': 0,
           'gru_cell_steps': 0, 'gru_cell_bwd_steps': 0}
 
 
@@ -735,14 +735,25 @@ def mlp_backward(ctx, dlogp, nll=None):
     ctx.W_t = None
     # (M, D) = dz . W_out, through W_out^T (D, Q) when the forward made it
     Wo, tB = (W_t[1], True) if W_t is not None else (W_out, False)
+    # bf16: the da2 GEMM's epilogue also sums its stored columns per 128-row block (the
+    # hidden layer's bias gradient) -- one pass over da2 fewer than a separate column sum
+    csp = None
+    if T == torch.bfloat16 and M % 256 == 0 and os.environ.get('SRNN_CSUM_EPI', '1') != '0':
+        csp = torch.empty((M // 128, D), device=dev, dtype=torch.float32)
+        H.lib().call('srnn_gemm_csum_next', H.ptr(csp))
     if m2 is not None:
         da2 = H.gemm(dz, Wo, transB=tB, mask_bits=m2, out_dtype=T)
     else:
         da2 = H.gemm(dz, Wo, transB=tB, mask=a2, out_dtype=T)
+    if csp is not None and not H.lib().dll.srnn_gemm_csum_taken():
+        csp = None
+    if csp is not None:
+        _STATS['csum_epi'] += 1
     ev = H.roof_begin()
     dW_hid = H.gemm(da2, a1, transA=True)                            # (D, D)
     H.roof_end('mlp_dw_hid_gemm', ev, 2.0 * M * D * D)
-    db_hid = H.colsum(da2, M, D)
+    db_hid = H.colsum(csp, M // 128, D) if csp is not None else H.colsum(da2, M, D)
+    csp = None
     # d(upper) in upper's dtype: bf16 when the bottom tier hands the MLP a bf16 upper.  A
     # bf16 da1 also gets max |da1| from the GEMM's epilogue (the packed dTab scatter's
     # scale), so the scatter needs no pass of its own over da1

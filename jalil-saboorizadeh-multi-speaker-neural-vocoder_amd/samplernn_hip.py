@@ -57,6 +57,7 @@ _SIGS = {
     'srnn_gemm_amax_next': [_P],
     'srnn_cast_multi': [_I, _P, _P, _P, _P],
     'srnn_gemm_amax_blk_next': [_P, _P],
+    'srnn_gemm_csum_next': [_P],
     'srnn_logsoftmax_nll': [_P, _L, _P, _L, _I, _L, _I, _P, _P, _L, _P, _I, _L, _F, _P],
     'srnn_logsoftmax_bwd': [_P, _L, _P, _L, _L, _I, _P, _I, _L, _P],
     'srnn_nll_fwd': [_P, _L, _P, _L, _I, _L, _P, _P],
@@ -135,7 +136,8 @@ class _Lib:
         # query entry points called on .dll directly (pointers are passed as plain ints, so
         # every pointer argument needs its declared type)
         for name, args in (('srnn_gru_xcd_error', [_P]), ('srnn_persistent_error_take', []),
-                           ('srnn_gemm_amax_taken', []), ('srnn_blaslt_calls', [])):
+                           ('srnn_gemm_amax_taken', []), ('srnn_gemm_csum_taken', []),
+                           ('srnn_blaslt_calls', [])):
             fn = getattr(self.dll, name)
             fn.argtypes = args
             fn.restype = _I
@@ -181,7 +183,7 @@ def exported_symbols():
                             'srnn_gen_persistent_rows', 'srnn_gru_xcd_work_bytes',
                             'srnn_gru_xcd_bwd_work_bytes', 'srnn_gru_xcd_error',
                             'srnn_persistent_error_take', 'srnn_gemm_amax_taken',
-                            'srnn_blaslt_calls']
+                            'srnn_gemm_csum_taken', 'srnn_blaslt_calls']
 
 
 # Callbacks run just before a persistent sweep (gru_xcd / gru_seq) is enqueued.  Such a sweep

@@ -66,6 +66,8 @@ def test_bench_bf16_step_matches_fp32(hip, B):
     assert M._STATS['gru_xcd_bwd'] > before['gru_xcd_bwd']
     assert M._STATS['gru_cell_steps'] == before['gru_cell_steps']
     assert M._STATS['gru_cell_bwd_steps'] == before['gru_cell_bwd_steps']
+    # ... and the hidden layer's bias gradient came from the da2 GEMM's epilogue
+    assert M._STATS['csum_epi'] > before['csum_epi']
     print('losses fp32', l32, 'bf16', l16)
     np.testing.assert_allclose(l16, l32, rtol=3e-4, atol=0)
     assert g16.keys() == g32.keys()
@@ -88,3 +90,33 @@ def test_bench_bf16_step_matches_fp32(hip, B):
         # scatter carries the recurrences' roundings (measured <= 6.8 %, cos >= 0.9977)
         dense = k.startswith(('model.sample_level_mlp.hidden', 'model.sample_level_mlp.output'))
         assert rel < (0.01 if dense else 0.085) and cos >= 0.997, (k, rel, cos)
+
+
+def test_bf16_csum_epilogue_vs_column_pass(hip, monkeypatch):
+    """configs[1] bf16 chunk: the hidden layer's bias gradient from the da2 GEMM's epilogue
+    column sums (default) against a separate column-sum pass over da2 (SRNN_CSUM_EPI=0):
+    every other gradient unchanged (bit-identical, or within 1e-6 where a gradient is an fp32
+    atomic scatter), the bias gradient within fp32 summation-order rounding (1e-4 of the
+    largest entry)."""
+    import bench
+    import model as M
+    B, T, L = 128, 1024, 64
+    batches = bench.gpu_batches(bench.synth_batches(B, T, L, 1, 0), DEV)
+    before = M._STATS['csum_epi']
+    _, g_epi = _run(torch.bfloat16, batches)
+    assert M._STATS['csum_epi'] > before
+    monkeypatch.setenv('SRNN_CSUM_EPI', '0')
+    mid = M._STATS['csum_epi']
+    _, g_pass = _run(torch.bfloat16, batches)
+    assert M._STATS['csum_epi'] == mid
+    key = 'model.sample_level_mlp.hidden.bias'
+    for k in g_pass:
+        if k != key and not torch.equal(g_epi[k], g_pass[k]):
+            # (the speaker-embedding gradient is a row scatter of fp32 atomics: run-to-run
+            #  rounding; everything else is bit-reproducible)
+            x, y = g_epi[k].double(), g_pass[k].double()
+            print('%s differs run to run: max |diff| %.3g' % (k, (x - y).abs().max()))
+            assert (x - y).abs().max() <= 1e-6 * y.abs().max(), k
+    a, b = g_epi[key].double(), g_pass[key].double()
+    print('hidden bias grad: max |diff| %.3g, max |g| %.3g' % ((a - b).abs().max(), b.abs().max()))
+    assert (a - b).abs().max() <= 1e-4 * b.abs().max()

@@ -1449,3 +1449,47 @@ def test_gemm_amax_request(hip):
     hip.lib().call('srnn_gemm_amax_next', hip.ptr(amax))
     hip.gemm(a[:64, :64].contiguous(), w[:64, :64].contiguous(), out_dtype=torch.bfloat16)
     assert hip.lib().dll.srnn_gemm_amax_taken() == 0
+
+
+@pytest.mark.parametrize('form', ['nt_mask', 'nn_plain', 'nt_bias_relu'])
+def test_gemm_csum_request(hip, form):
+    """srnn_gemm_csum_next: the next bf16-output GEMM on the gemm3 pair path also writes the
+    column sums of the bf16 values it stored, per 128-row block (part[M / 128][N]): each block
+    row equals the fp64 sum of those stored values within fp32 rounding (128 terms), and the
+    product itself is bit-identical to the same GEMM without the request.  nt_mask is the
+    MLP's da2 = (dz W_out^T) * relu' form (model.py:320); nn_plain a shape that otherwise takes
+    the ring ping-pong (the request keeps it on the pair kernel).  A bit-mask GEMM and a
+    small GEMM leave the request untaken."""
+    g = torch.Generator().manual_seed(12)
+    M, N, K = (8192, 1024, 256) if form != 'nn_plain' else (8192, 4096, 512)
+    a = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    kw = dict(out_dtype=torch.bfloat16)
+    if form == 'nn_plain':
+        w = (torch.randn(K, N, generator=g) * 0.05).to(DEV, torch.bfloat16)
+    else:
+        w = (torch.randn(N, K, generator=g) * 0.05).to(DEV, torch.bfloat16)
+        kw['transB'] = True
+    if form == 'nt_mask':
+        kw['mask'] = (torch.rand(M, N, generator=g) > 0.5).to(DEV, torch.bfloat16)
+    elif form == 'nt_bias_relu':
+        kw.update(bias=torch.randn(N, generator=g).to(DEV), relu=True)
+    plain = hip.gemm(a, w, **kw)
+    part = torch.full((M // 128, N), float('nan'), device=DEV)
+    hip.lib().call('srnn_gemm_csum_next', hip.ptr(part))
+    c = hip.gemm(a, w, **kw)
+    assert hip.lib().dll.srnn_gemm_csum_taken() == 1
+    torch.cuda.synchronize()
+    assert torch.equal(c, plain)
+    ref = c.double().reshape(M // 128, 128, N).sum(1)
+    mag = c.double().abs().reshape(M // 128, 128, N).sum(1)
+    err = (part.double() - ref).abs()
+    assert torch.isfinite(part).all()
+    assert (err <= 128 * 2.0 ** -24 * mag + 1e-30).all(), float((err / (mag + 1e-30)).max())
+    # bit masks (their own kernels) and a small GEMM do not take the request
+    bits = torch.zeros((M, N // 16), device=DEV, dtype=torch.int16)
+    hip.lib().call('srnn_gemm_csum_next', hip.ptr(part))
+    hip.gemm(a, w, mask_bits=bits, **{k: v for k, v in kw.items() if k != 'mask'})
+    assert hip.lib().dll.srnn_gemm_csum_taken() == 0
+    hip.lib().call('srnn_gemm_csum_next', hip.ptr(part))
+    hip.gemm(a[:64, :64].contiguous(), a[:64, :64].contiguous(), out_dtype=torch.bfloat16)
+    assert hip.lib().dll.srnn_gemm_csum_taken() == 0
