@@ -283,6 +283,10 @@ int srnn_gather_rows(const float* table, int64_t ldt, const int64_t* idx, int64_
                      void* out, int out_dtype, int64_t ldo, void* stream);
 int srnn_scatter_add_rows(float* table, int64_t ldt, const int64_t* idx, int64_t n, int cols,
                           const float* src, int64_t lds, void* stream);
+/* table[q,:] += sum_{r: idx[r]==q} src[r,:] in r order, q < trows -- the speaker-embedding
+   backward (model.py:203-207, nn.Embedding's gradient) without atomics: deterministic     */
+int srnn_index_add_rows(float* table, int64_t ldt, int trows, const int64_t* idx, int64_t n,
+                        int cols, const float* src, int64_t lds, void* stream);
 int srnn_axpby(float* out, const float* a, const float* b, float alpha, float beta, int64_t n,
                void* stream);
 int srnn_add_bcast_rows(float* x, const float* v, int B, int F, int D, int64_t ldv, void* stream);

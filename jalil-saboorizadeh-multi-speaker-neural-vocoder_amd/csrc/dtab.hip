@@ -681,7 +681,10 @@ extern "C" int srnn_mlp_dtab4(int dtype, const void* da, int64_t ldda, const int
     if (colsum_done) *colsum_done = 0;
     if (dtype == SRNN_BF16 && out_dtype == SRNN_BF16 && FS0 == 16 && Q == 256 && D % 8 == 0 &&
         ldda % 8 == 0 &&
-        cdiv(D, 4) >= 192 && pk_lds_bytes(Q, Tlen) <= 160 * 1024 && (int64_t)B * Tlen > 0 &&
+        cdiv(D, 4) >= 192 && pk_lds_bytes(Q, Tlen) <= 160 * 1024 &&
+        // the packed kernel writes nothing when the histogram is too skewed for its scale and
+        // leaves dTab to the gated exact form: take it only where that form fits too
+        pos_lds_bytes(Q, Tlen) <= 160 * 1024 && (int64_t)B * Tlen > 0 &&
         work_bytes >= sizeof(DtabStat) && !getenv_off("SRNN_DTAB_PACK")) {
         DtabStat* st = (DtabStat*)work;
         SRNN_CHECK_HIP(hipMemsetAsync(st, 0, sizeof(DtabStat), s));
@@ -714,12 +717,9 @@ extern "C" int srnn_mlp_dtab4(int dtype, const void* da, int64_t ldda, const int
         SRNN_LAUNCH_CHECK();
         // the exact form behind it, gated on the same statistics: all of its workgroups
         // return at once unless the packed form declined (a skewed sample histogram)
-        if (pos_lds_bytes(Q, Tlen) <= 160 * 1024) {
-            const int rc = launch_pos<bf16, bf16, true>(da, ldda, x, ldx, xoff, B, Tlen, nullptr,
-                                                        dtab_out, colsum, D, Q, B, 1, s, st,
-                                                        amax_in);
-            if (rc) return rc;
-        }
+        const int rc = launch_pos<bf16, bf16, true>(da, ldda, x, ldx, xoff, B, Tlen, nullptr,
+                                                    dtab_out, colsum, D, Q, B, 1, s, st, amax_in);
+        if (rc) return rc;
         if (colsum && colsum_done) *colsum_done = 1;
         return 0;
     }

@@ -637,6 +637,31 @@ extern "C" int srnn_scatter_add_rows(float* table, int64_t ldt, const int64_t* i
     return 0;
 }
 
+// table[q, :] += sum over r with idx[r] == q of src[r, :], in r order: the embedding backward
+// (speaker rows, model.py:203-207) without atomics, so the gradient is the same bits on every
+// run.  One thread per table entry walks the n source rows (n = batch rows: a few hundred).
+__global__ void index_add_rows_kernel(float* __restrict__ table, int64_t ldt, int trows,
+                                      const int64_t* __restrict__ idx, int64_t n, int cols,
+                                      const float* __restrict__ src, int64_t lds) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= (int64_t)trows * cols) return;
+    const int q = (int)(e / cols), c = (int)(e % cols);
+    float acc = table[(int64_t)q * ldt + c];
+    for (int64_t r = 0; r < n; ++r)
+        if (idx[r] == q) acc += src[r * lds + c];
+    table[(int64_t)q * ldt + c] = acc;
+}
+
+extern "C" int srnn_index_add_rows(float* table, int64_t ldt, int trows, const int64_t* idx,
+                                   int64_t n, int cols, const float* src, int64_t lds,
+                                   void* stream) {
+    if ((int64_t)trows * cols <= 0 || n <= 0) return 0;
+    hipLaunchKernelGGL(index_add_rows_kernel, dim3(cdiv((int64_t)trows * cols, 256)), dim3(256),
+                       0, (hipStream_t)stream, table, ldt, trows, idx, n, cols, src, lds);
+    SRNN_LAUNCH_CHECK();
+    return 0;
+}
+
 // out = alpha * a + beta * b  (fp32, elementwise; out may alias a or b)
 __global__ void axpby_kernel(float* out, const float* a, const float* b, float alpha, float beta,
                              int64_t n) {

@@ -586,7 +586,7 @@ def tier_backward(ctx, dY, need_h0):
         db_s = H.colsum(dspk, B, D)
         demb = H.gemm(dspkT, W_s)                                    # (B, S)
         dE = torch.zeros((S, S), device=dev, dtype=torch.float32)
-        H.lib().call('srnn_scatter_add_rows', H.ptr(dE), S, H.ptr(spk_flat), B, S,
+        H.lib().call('srnn_index_add_rows', H.ptr(dE), S, S, H.ptr(spk_flat), B, S,
                      H.ptr(demb), S, st())
         grads += [dE]
         grads += nn.weight_grad_to_params(mod.spk_expand, dW_s.reshape(D, S, 1))

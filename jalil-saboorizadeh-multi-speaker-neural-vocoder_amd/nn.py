@@ -173,10 +173,48 @@ def concat_init(tensor, inits):
 FUSED_NLL = os.environ.get('SRNN_FUSED_NLL', '1') != '0'
 
 
+_NLL_ARGS = ('weight', 'size_average', 'ignore_index', 'reduce', 'reduction')
+
+
+def _nll_options(args, kwargs):
+    """nll_loss's optional arguments (weight, size_average, ignore_index, reduce, reduction),
+    positional or keyword as the reference passes them through (nn.py:66-70) -> a dict."""
+    if len(args) > len(_NLL_ARGS):
+        raise TypeError('sequence_nll_loss_bits: too many positional arguments')
+    opts = dict(zip(_NLL_ARGS, args))
+    for k, v in kwargs.items():
+        if k not in _NLL_ARGS:
+            raise TypeError('sequence_nll_loss_bits: unexpected keyword argument %r' % k)
+        if k in opts:
+            raise TypeError('sequence_nll_loss_bits: got multiple values for %r' % k)
+        opts[k] = v
+    return opts
+
+
 def sequence_nll_loss_bits(input, target, *args, **kwargs):
-    """nn.py:66-70: mean NLL of log-probs (B, T, Q) x log2(e), on the HIP kernels."""
-    if args or kwargs:
-        raise NotImplementedError('sequence_nll_loss_bits: extra nll_loss arguments')
+    """nn.py:66-70: NLL of log-probs (B, T, Q) x log2(e).  The reference's call (train.py:
+    no extra arguments: the mean) runs on the HIP kernels (srnn::nll_bits); the optional
+    nll_loss arguments are passed through as the reference does.  reduction='sum' is the HIP
+    mean x rows; a class weight, an ignore_index that some target hits, or reduction='none'
+    (none of which the reference's training uses) go to torch's nll_loss on the same device
+    tensors."""
     H.need_cuda(input, target)
     import custom_ops
-    return custom_ops.nll_bits(input, target)          # the registered op srnn::nll_bits
+    if not (args or kwargs):
+        return custom_ops.nll_bits(input, target)      # the registered op srnn::nll_bits
+    opts = _nll_options(args, kwargs)
+    size_average, reduce_ = opts.pop('size_average', None), opts.pop('reduce', None)
+    if size_average is not None or reduce_ is not None:
+        reduction = torch.nn.modules.loss._Reduction.legacy_get_string(size_average, reduce_)
+    else:
+        reduction = opts.get('reduction', 'mean')
+    weight, ignore = opts.get('weight'), opts.get('ignore_index', -100)
+    n_classes = input.size(2)
+    # (targets are sample values in [0, Q): an ignore_index outside that never hits)
+    hits_ignore = 0 <= ignore < n_classes and bool((target == ignore).any())
+    if weight is None and not hits_ignore and reduction in ('mean', 'sum'):
+        loss = custom_ops.nll_bits(input, target)
+        return loss * target.numel() if reduction == 'sum' else loss
+    return torch.nn.functional.nll_loss(
+        input.reshape(-1, n_classes), target.reshape(-1), weight=weight, ignore_index=ignore,
+        reduction=reduction) * math.log(math.e, 2)

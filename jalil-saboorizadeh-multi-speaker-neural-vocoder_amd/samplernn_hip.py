@@ -68,6 +68,7 @@ _SIGS = {
     'srnn_copy2d': [_I, _I, _I, _I, _P, _L, _P, _L, _P],
     'srnn_gather_rows': [_P, _L, _P, _L, _I, _P, _I, _L, _P],
     'srnn_scatter_add_rows': [_P, _L, _P, _L, _I, _P, _L, _P],
+    'srnn_index_add_rows': [_P, _L, _I, _P, _L, _I, _P, _L, _P],
     'srnn_axpby': [_P, _P, _P, _F, _F, _L, _P],
     'srnn_add_bcast_rows': [_P, _P, _I, _I, _I, _L, _P],
     'srnn_segsum': [_P, _L, _I, _I, _I, _P, _P],

@@ -43,6 +43,24 @@ GRAPHS = os.environ.get('SRNN_GRAPH', '1') != '0'
 FORCE = os.environ.get('SRNN_GRAPH', '1') == 'force'
 
 
+def _capture_agreed(opt, ok):
+    """True iff the capture succeeded on every rank of the optimizer's data-parallel group
+    (MIN all-reduce of the local outcome, outside any capture); `ok` alone without one."""
+    sync = getattr(opt, 'grad_sync', None)
+    if sync is None:
+        return ok
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return ok
+    grp = getattr(sync, 'group', None)
+    if dist.get_world_size(grp) <= 1:
+        return ok
+    dev = 'cuda' if dist.get_backend(grp) == 'nccl' else 'cpu'
+    flag = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=grp)
+    return bool(flag.item())
+
+
 class _StepGraph:
     """One captured TBPTT step: the graph, its static inputs and outputs."""
 
@@ -295,6 +313,7 @@ class Trainer(object):
             loss.backward()
             out_loss[0], out_loss[1] = out.data, loss.data
             return loss
+        err = None
         try:
             # a private memory pool per step kind; thread-local capture mode, so other
             # threads' HIP calls (the RCCL process group's watchdog querying its events under
@@ -308,7 +327,16 @@ class Trainer(object):
                                            % (tuple(h.shape), h.dtype, tuple(b.shape)))
                     b.copy_(h)
         except Exception as e:  # noqa: BLE001 -- any capture failure: roll back, run eagerly
+            err = e
+        # under data parallelism every rank must take the same path after a capture attempt
+        # (one rank replaying captured collectives while another issues them eagerly would
+        # desynchronise the communicator): the ranks agree on the outcome, and a failure on
+        # any rank rolls every rank back to the eager step
+        if not _capture_agreed(opt, err is None) and err is None:
+            err = RuntimeError('capture failed on another rank')
+        if err is not None:
             import warnings
+            e = err
             torch.cuda.synchronize()
             model.hidden_states.clear()
             model.hidden_states.update(saved_hidden)

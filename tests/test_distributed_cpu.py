@@ -269,3 +269,43 @@ def test_zero_shards_cover_every_element_once(world):
             assert offs[i] + a == r * S + so          # gradient view = the same flat element
             seen[i][a:b] += 1
     assert all(bool((x == 1).all()) for x in seen)
+
+
+class _Sync:
+    group = None
+
+
+class _Opt:
+    grad_sync = _Sync()
+
+
+def _agree_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import distributed as D
+    from trainer import _capture_agreed
+    D.init(backend='gloo')
+    both_ok = _capture_agreed(_Opt(), True)
+    one_failed = _capture_agreed(_Opt(), rank != 1)
+    q.put((rank, both_ok, one_failed))
+    dist.destroy_process_group()
+
+
+def test_graph_capture_outcome_agreed_across_ranks():
+    """Trainer._capture under data parallelism: the ranks agree on the capture's outcome
+    (MIN all-reduce), so a capture failing on one rank sends EVERY rank back to the eager
+    step -- no rank replays captured collectives while another issues them eagerly (ADVICE
+    r04).  Without a process group the local outcome stands."""
+    from trainer import _capture_agreed
+    assert _capture_agreed(_Opt(), True) is True and _capture_agreed(_Opt(), False) is False
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(got) == [(0, True, False), (1, True, False)]

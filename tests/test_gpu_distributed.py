@@ -48,6 +48,9 @@ def _worker(rank, world, port, name, overlap, zero, q):
         from trainer import Trainer
         D.init(backend='gloo')
         H.lib()
+        if zero == 'nccl_emul':
+            D.dist = _NcclEmul(D.dist)
+            zero = True
         g = golden('tbptt_' + name)
         cfg = recipe.CONFIGS[name]
         m, pred = build(cfg, recipe.make_weights(cfg, int(g['weight_seed'])))
@@ -85,11 +88,48 @@ def _worker(rank, world, port, name, overlap, zero, q):
         raise
 
 
+class _Done:
+    def wait(self):
+        return True
+
+
+class _NcclEmul:
+    """torch.distributed as distributed.py sees it under RCCL, on a gloo group: get_backend
+    says 'nccl', so GradAllReduce takes its RCCL-only ZeRO branches (reduce_scatter_tensor into
+    the shard, the in-place all_gather_into_tensor of the flat parameters), and those two
+    collectives are restated with their documented semantics over gloo's all_reduce /
+    all_gather -- the shard offsets of the RCCL form are then checked against the reference's
+    full-batch trajectory without two GPUs."""
+
+    def __init__(self, real):
+        self._d = real
+
+    def __getattr__(self, k):
+        return getattr(self._d, k)
+
+    def get_backend(self, group=None):
+        return 'nccl'
+
+    def reduce_scatter_tensor(self, out, inp, op=None, group=None, async_op=False):
+        tmp = inp.clone()
+        self._d.all_reduce(tmp, op=self._d.ReduceOp.SUM, group=group)
+        r, S = self._d.get_rank(group), out.numel()
+        out.copy_(tmp[r * S:(r + 1) * S])
+        return _Done() if async_op else None
+
+    def all_gather_into_tensor(self, out, inp, group=None, async_op=False):
+        parts = list(out.split(inp.numel()))
+        self._d.all_gather(parts, inp.clone(), group=group)
+        return _Done() if async_op else None
+
+
 @pytest.mark.parametrize('overlap,zero', [(True, True), (False, True), (True, False),
-                                          (False, False)])
+                                          (False, False), (True, 'nccl_emul'),
+                                          (False, 'nccl_emul')])
 def test_dp_two_ranks_match_reference_full_batch(hip, overlap, zero):
     """zero: ZeRO-1 (each rank clamps + updates its shard of the summed gradient, then the
-    parameters are all-gathered) or the replicated update after an all-reduce."""
+    parameters are all-gathered) or the replicated update after an all-reduce; 'nccl_emul'
+    runs ZeRO-1's RCCL branches over gloo (_NcclEmul)."""
     from conftest import golden
     name = 't3'
     g = golden('tbptt_' + name)

@@ -844,7 +844,7 @@ def test_mlp_dtab_packed_bf16(hip, monkeypatch, B, Tl, skew):
     assert e_pk <= 1.5 * e_ex + 1e-12
 
 
-def _dtab4(hip, da, x, B, Tl, blk=None, amax=None):
+def _dtab4(hip, da, x, B, Tl, blk=None, amax=None, want_colsum=True):
     import ctypes
     FS0, Q, D = 16, 256, da.shape[1]
     work = torch.empty(Q * FS0 * D, device=DEV, dtype=torch.int64)
@@ -855,8 +855,10 @@ def _dtab4(hip, da, x, B, Tl, blk=None, amax=None):
                    hip.ptr(tab), hip.BF16, D, FS0, Q, hip.ptr(work), work.numel() * 8,
                    hip.ptr(colsum), ctypes.byref(done), hip.ptr(amax), hip.ptr(blk), hip.stream())
     torch.cuda.synchronize()
-    assert done.value == 1
-    return tab.cpu(), colsum.cpu()
+    if want_colsum:
+        assert done.value == 1
+        return tab.cpu(), colsum.cpu()
+    return tab.cpu(), (colsum.cpu() if done.value == 1 else None)
 
 
 @pytest.mark.parametrize('B,Tl', [(64, 1024), (3, 37)])
@@ -894,25 +896,39 @@ def test_gemm_writes_blocked_copy(hip):
     assert amax.view(torch.float32).item() == C.float().abs().max().item()
 
 
-def test_mlp_dtab_skew_takes_exact_form(hip):
+@pytest.mark.parametrize('B,Tl', [(128, 1024), (64, 2048), (16, 9000)])
+def test_mlp_dtab_skew_takes_exact_form(hip, B, Tl):
     """A sample histogram past the packed form's precision bound (one value at > 65,536
     positions: long silences at large B) makes the gated exact 2^-40 form produce dTab:
-    bit-identical to SRNN_DTAB_PACK=0's output."""
+    bit-identical to SRNN_DTAB_PACK=0's output.  Tl = 9000 is past the exact position-major
+    form's LDS budget (the packed one still fits): the packed form must not be taken there,
+    since nothing would stand behind it."""
     import os
-    B, Tl, D = 128, 1024, 1024
-    g = torch.Generator().manual_seed(11)
+    D = 1024
+    g = torch.Generator().manual_seed(11 + Tl)
     x = torch.randint(0, 256, (B, Tl + 15), generator=g)
     x[torch.rand(x.shape, generator=g) < 0.6] = 128
     assert int(torch.bincount(x.reshape(-1)).max()) > 65536
     x = x.to(DEV)
     da = (torch.randn(B * Tl, D, generator=g) * 1e-4).to(DEV, torch.bfloat16)
-    t_gate, c_gate = _dtab4(hip, da, x, B, Tl)
+    t_gate, c_gate = _dtab4(hip, da, x, B, Tl, want_colsum=False)
     os.environ['SRNN_DTAB_PACK'] = '0'
     try:
-        t_ex, c_ex = _dtab4(hip, da, x, B, Tl)
+        t_ex, c_ex = _dtab4(hip, da, x, B, Tl, want_colsum=False)
     finally:
         del os.environ['SRNN_DTAB_PACK']
-    assert torch.equal(t_gate, t_ex) and torch.equal(c_gate, c_ex)
+    assert torch.equal(t_gate.view(torch.int16), t_ex.view(torch.int16))
+    assert (c_gate is None) == (c_ex is None)
+    if c_gate is not None:
+        assert torch.equal(c_gate, c_ex)
+    if Tl > 8000:
+        # every entry is a real sum (no stale workspace): compare with an fp64 scatter
+        ref = torch.zeros(256, 16, D, dtype=torch.float64)
+        xc, dc = x.cpu(), da.double().cpu()
+        for k in range(16):
+            ref[:, k].index_add_(0, xc[:, k:k + Tl].reshape(-1), dc)
+        err = (t_gate.double() - ref).abs()
+        assert float((err - ref.abs() * 2.0 ** -8).max()) < 1e-6
 
 
 def test_mlp_dtab_nonfinite_poisons(hip):
@@ -1493,3 +1509,52 @@ def test_gemm_csum_request(hip, form):
     hip.lib().call('srnn_gemm_csum_next', hip.ptr(part))
     hip.gemm(a[:64, :64].contiguous(), a[:64, :64].contiguous(), out_dtype=torch.bfloat16)
     assert hip.lib().dll.srnn_gemm_csum_taken() == 0
+
+
+def test_index_add_rows_deterministic(hip):
+    """srnn_index_add_rows (the speaker-embedding gradient): table[q] += the rows of src whose
+    index is q, summed in row order -- the same bits on every run, equal to a sequential fp32
+    sum in that order, within fp32 rounding of the fp64 index_add."""
+    S, n = 6, 512
+    g = torch.Generator().manual_seed(21)
+    idx = torch.randint(0, S, (n,), generator=g)
+    src = torch.randn(n, S, generator=g)
+    base = torch.randn(S, S, generator=g)
+    outs = []
+    for _ in range(2):
+        t = base.clone().to(DEV)
+        hip.lib().call('srnn_index_add_rows', hip.ptr(t), S, S, hip.ptr(idx.to(DEV)), n, S,
+                       hip.ptr(src.to(DEV)), S, hip.stream())
+        torch.cuda.synchronize()
+        outs.append(t.cpu())
+    assert torch.equal(outs[0], outs[1])
+    seq = base.clone()
+    for r in range(n):                     # the kernel's order, in fp32
+        seq[idx[r]] += src[r]
+    assert torch.equal(outs[0], seq)
+    ref = base.double().index_add(0, idx, src.double())
+    torch.testing.assert_close(outs[0].double(), ref, atol=1e-5, rtol=0)
+
+
+@pytest.mark.parametrize('args,kwargs', [((), {}), ((), {'reduction': 'sum'}),
+                                         ((None, None, 7), {}), ((), {'reduction': 'none'}),
+                                         ((), {'weight': 'w'}), ((), {'size_average': False}),
+                                         ((), {'ignore_index': 300})])
+def test_nll_bits_passes_nll_loss_arguments(hip, args, kwargs):
+    """sequence_nll_loss_bits(input, target, *args, **kwargs) = nll_loss(input.view(-1, Q),
+    target.view(-1), *args, **kwargs) * log2(e), as the reference (nn.py:66-70) -- the extra
+    arguments are passed through instead of refused."""
+    import math
+    import nn as snn
+    B, T, Q = 3, 40, 256
+    g = torch.Generator().manual_seed(5)
+    lp = torch.log_softmax(torch.randn(B, T, Q, generator=g), -1)
+    tgt = torch.randint(0, Q, (B, T), generator=g)
+    tgt[0, :5] = 7
+    if kwargs.get('weight') == 'w':
+        kwargs = {'weight': torch.rand(Q, generator=g)}
+    ref = torch.nn.functional.nll_loss(lp.view(-1, Q), tgt.view(-1), *args, **kwargs) * \
+        math.log(math.e, 2)
+    dkw = {k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in kwargs.items()}
+    got = snn.sequence_nll_loss_bits(lp.to(DEV), tgt.to(DEV), *args, **dkw)
+    torch.testing.assert_close(got.cpu().double(), ref.double(), atol=2e-5, rtol=1e-5)

@@ -103,7 +103,12 @@ def test_tbptt_sampled_golden(hip, name):
             fails.append(str(e).strip().splitlines()[0][:200])
     print('losses', losses, 'reference', list(g['losses']), 'perturbation envelope %.3g'
           % float(g['env_max/losses']))
-    check(within_floor, losses, g['losses'], g, 'losses', 1e-4)
+    # chunk 0 (fresh weights: the forward + backward proper, before any Adam step) is held
+    # to the strict 1e-4 alone -- the perturbed reference moves it by ~1e-7; the envelope
+    # (whose 'losses' key is the max over chunks, set by chunk 2) covers the later chunks only
+    check(np.testing.assert_allclose, losses[0], g['losses'][0], atol=1e-4, rtol=0,
+          err_msg='chunk-0 loss')
+    check(within_floor, losses[1:], g['losses'][1:], g, 'losses', 1e-4)
     for s in range(n_steps):
         for t in range(len(cfg['frame_sizes'])):
             key = 'hidden_%d_tier%d' % (s, t)
@@ -148,28 +153,20 @@ def test_bf16_loss_trajectory_50_chunks(hip):
     """configs[1] (B = 128, T = 1024): 50 TBPTT chunks (reset, then 49 carried) with clip +
     Adam from the same weights and data in bf16 (the bench's path) and in fp32 (the path
     pinned to the reference).  Over 50 Adam steps a rounding-level change moves the
-    trajectory by itself (sign-driven first moments of near-zero gradients), so the bound is
-    set against the bf16 path's own sensitivity, measured here: the same bf16 run from weights
-    perturbed by one ulp (random signs, 2 seeds) gives env = the largest per-chunk relative
-    distance to the unperturbed bf16 run.  Bound: every chunk's loss within 5e-3 + 2 env
-    relative of the fp32 trajectory's, the mean relative difference below 1.5e-3.  Measured
-    on MI355X (round 4): max 2.7e-3 .. 5.7e-3 (chunk 35 / 43) depending on the summation order
-    of one bias gradient (a rounding-level change), mean 6.8e-4 .. 9.3e-4; DESIGN §4."""
+    trajectory by itself (sign-driven first moments of near-zero gradients).  Fixed bounds,
+    set from the round-4 measurements on MI355X: max relative loss difference 2.7e-3 .. 5.7e-3
+    (chunk 35 / 43, depending on the summation order of one bias gradient), mean 6.8e-4 ..
+    9.3e-4, and the bf16 run's own one-ulp-perturbation sensitivity up to 5.1e-3
+    (profiles/r04_traj_50chunks.log) -- every chunk within 8e-3 relative of the fp32
+    trajectory, the mean below 1.5e-3, chunk 0 (no Adam step yet) within 1e-3; DESIGN §4."""
     import bench
     import nn as snn
     import optim
     B, T, L, N = 128, 1024, 64, 50
     batches = bench.gpu_batches(bench.synth_batches(B, T, L, N, 0), DEV)
 
-    def traj(dtype, perturb=None):
+    def traj(dtype):
         _, pred = bench.make_model(dtype)
-        if perturb is not None:
-            g = torch.Generator().manual_seed(perturb)
-            with torch.no_grad():
-                for p in pred.parameters():
-                    up = torch.rand(p.shape, generator=g) < 0.5
-                    p.copy_(torch.where(up, torch.nextafter(p, torch.full_like(p, float('inf'))),
-                                        torch.nextafter(p, torch.full_like(p, -float('inf')))))
         pred = pred.to(DEV)
         opt = optim.gradient_clipping(torch.optim.Adam(pred.parameters(), lr=1e-3))
         out = []
@@ -186,13 +183,13 @@ def test_bf16_loss_trajectory_50_chunks(hip):
         return torch.stack(out).double().cpu().numpy()
     b = traj(torch.float32)
     a = traj(torch.bfloat16)
-    env = max(float(np.max(np.abs(traj(torch.bfloat16, s) - a) / np.abs(a))) for s in (1, 2))
     rel = np.abs(a - b) / np.abs(b)
     print('bf16-vs-fp32 loss trajectory over %d chunks: max rel %.3g (chunk %d), mean rel %.3g;'
-          ' fp32 %.4f -> %.4f, bf16 %.4f -> %.4f; bf16 one-ulp sensitivity env %.3g'
-          % (N, rel.max(), int(rel.argmax()), rel.mean(), b[0], b[-1], a[0], a[-1], env))
+          ' fp32 %.4f -> %.4f, bf16 %.4f -> %.4f'
+          % (N, rel.max(), int(rel.argmax()), rel.mean(), b[0], b[-1], a[0], a[-1]))
     assert np.all(np.isfinite(a))
-    assert rel.max() < 5e-3 + 2 * env and rel.mean() < 1.5e-3
+    assert rel[0] < 1e-3
+    assert rel.max() < 8e-3 and rel.mean() < 1.5e-3
 
 
 def test_persistent_fp32_long_teacher_forced(hip):
