@@ -137,6 +137,17 @@ int srnn_gru_xcd_error(const void* work);
  * weights).  The training path checks it once per Trainer iteration (the reference has no
  * equivalent: its cuDNN GRU cannot fail this way).                                        */
 int srnn_persistent_error_take(void);
+/* Co-residency of the persistent kernels (csrc/handoff.hpp, persist.hip): n processes run
+   persistent grids on this device at once (a multi-rank rehearsal on one GPU; default 1).
+   Support predicates (srnn_gru_xcd_work_bytes, srnn_gru_seq_supported, the generation plan)
+   then only accept grids that fit the device n times over; every persistent launch checks
+   occupancy x CUs >= workgroups x n and refuses (error) otherwise.  The reference has no
+   counterpart (its GRU is torch.nn.GRU, model.py:148-165).                                 */
+int srnn_set_device_share(int n);
+int srnn_device_share(void);
+/* Diagnostics: occupy `blocks` CUs (160 KiB LDS each) for `usec` us; *done += 1 per
+   workgroup at the end (optional) -- the co-residency tests' stand-in for other work.      */
+int srnn_hold_cus(int blocks, int usec, int* done, void* stream);
 /* Stream-ordered access to that flag for data parallelism: dst = flag ? 1.f : 0.f, and
  * flag |= (src > 0).  The flag rides in a gradient bucket so every rank agrees.           */
 int srnn_persistent_flag_to_f32(float* dst, void* stream);

@@ -291,7 +291,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         }
         // placement check (wave 0, after its own loads are in flight)
         if (wave == 0) {
-            const int loc = cen && hx_group_local(cen + g * a.P, a.P, a.err) ? 1 : 0;
+            const int loc = cen && hx_group_local(cen + g * a.P, a.P, a.err, !a.nolocal) ? 1 : 0;
             if (tid == 0) {
                 gsh[2] = loc;
                 GM_STAMP();
@@ -738,11 +738,10 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     const int UK = dtype == SRNN_BF16 ? 32 : 16;
     const int NU = (D + UK - 1) / UK;
     const int upw = (NU + gm::NW - 1) / gm::NW;
-    const int ncu = device_cus();
-    if (ncu <= 0) return 0;
     int R = 0;
     for (int r : {8})          // one a1 element per thread: R * CW <= 512
-        if ((int64_t)cdiv(B, r) * P <= ncu) { R = r; break; }
+        // every workgroup co-resident, for each process sharing the device (persist.hip)
+        if (srnn_persist_fits_cus((int64_t)cdiv(B, r) * P)) { R = r; break; }
     if (!R) return 0;
     const GmKernel k = dtype == SRNN_BF16 ? pick<bf16>(upw, NZ / 16, FS0, D, R)
                                           : pick<float>(upw, NZ / 16, FS0, D, R);
@@ -858,7 +857,10 @@ int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
     a.P = pl->P;
     a.CW = pl->CW;
     a.NZ = pl->NZ;
-    if (!pl->local || pl->G * pl->P > HX_KEYED_WORDS) a.census = nullptr;
+    // the census is the arrival gate (handoff.hpp) as well as the placement check: always on;
+    // SRNN_GEN_LOCAL=0 only forces the global-mode hand-offs
+    SRNN_REQUIRE(a.census && pl->G * pl->P <= HX_KEYED_WORDS, "gen_mlp: no census array");
+    a.nolocal = pl->local ? 0 : 1;
     {
         // SRNN_GEN_DIAG=1: phase timestamps of the first launch into a device buffer that
         // srnn_gen_diag_dump prints (timing diagnostics only)
@@ -885,6 +887,8 @@ int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         if (slot < 16) { done[slot] = (const void*)k; done_lds[slot] = 160 * 1024; }
     }
+    if (srnn_persist_check((const void*)k, gm::NTHR, pl->lds, (int64_t)pl->G * pl->P, "gen_mlp"))
+        return 1;
     hipLaunchKernelGGL(k, dim3(pl->G * pl->P), dim3(gm::NTHR), pl->lds, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;

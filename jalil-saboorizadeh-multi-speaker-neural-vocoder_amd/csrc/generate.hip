@@ -954,7 +954,9 @@ extern "C" int srnn_generate2(const SrnnModel* m, int n_seqs, int n_cond, const 
     if (!rc && c.pl) {
         int e = 0;
         if (hipMemcpy(&e, c.b.gerr, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess || e) {
-            srnn_set_error("generate: persistent sample loop lost a hand-off (spin limit)");
+            srnn_set_error(e == 2 ? "generate: persistent sample loop's workgroups were not all "
+                                    "resident within 30 s (another process holds the CUs?)"
+                                  : "generate: persistent sample loop lost a hand-off (spin limit)");
             rc = 2;
         }
     }

@@ -364,19 +364,13 @@ __global__ __launch_bounds__(256, 1) void gru_seq_bwd_kernel(GruSeqBwdArgs a) {
     }
 }
 
-static int g_ncu = 0;
 
 // 1 if the persistent path can run this shape on this device, else 0
 extern "C" int srnn_gru_seq_supported(int dtype, int B, int D) {
     if (dtype != SRNN_BF16 || D % 128 != 0 || D > gseq::MAXK || B <= 0) return 0;
-    if (!g_ncu) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess) return 0;
-        if (hipDeviceGetAttribute(&g_ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 0;
-    }
-    // every workgroup must be co-resident (one per CU: 160 KiB LDS each); <= 64 unit tiles
-    return D / 16 <= 64 && (int64_t)(D / 16) * cdiv(B, gseq::BM) <= g_ncu ? 1 : 0;
+    // every workgroup must be co-resident (one per CU: 160 KiB LDS each, for every process
+    // sharing the device, persist.hip); <= 64 unit tiles
+    return D / 16 <= 64 && srnn_persist_fits_cus((int64_t)(D / 16) * cdiv(B, gseq::BM)) ? 1 : 0;
 }
 
 extern "C" int srnn_gru_seq_bwd(int dtype, int B, int D, int Fr, const float* dy, int64_t lddy,
@@ -413,6 +407,9 @@ extern "C" int srnn_gru_seq_bwd(int dtype, int B, int D, int Fr, const float* dy
     a.spin_limit = srnn_persist_spin_limit((int)gseq::SPIN_LIMIT);
     a.withhold = env_flag("SRNN_PERSIST_FORCE_FAIL", 0);
     a.B = B; a.D = D; a.Fr = Fr;
+    if (srnn_persist_check((const void*)gru_seq_bwd_kernel, 256, gseqb::LDS,
+                           (int64_t)(D / 16) * nm, "gru_seq_bwd"))
+        return 1;
     hipLaunchKernelGGL(gru_seq_bwd_kernel, dim3(D / 16, nm), dim3(256), gseqb::LDS, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;
@@ -453,6 +450,9 @@ extern "C" int srnn_gru_seq_fwd(int dtype, int B, int D, int Fr, const float* gi
         const char* e = getenv("SRNN_GSEQ_DIAG");
         a.diag = e ? atoi(e) : 0;
     }
+    if (srnn_persist_check((const void*)gru_seq_fwd_kernel, 256, gseq::LDS,
+                           (int64_t)(D / 16) * nm, "gru_seq_fwd"))
+        return 1;
     hipLaunchKernelGGL(gru_seq_fwd_kernel, dim3(D / 16, nm), dim3(256), gseq::LDS, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;

@@ -40,8 +40,10 @@ constexpr int HDR = 2048;
 // fused Adam skips its update while that flag is up and the host reads it at its own sync
 // points (srnn_persistent_error_take).
 __device__ __forceinline__ void gx_note_failure(const int* err, int* sticky) {
-    if (threadIdx.x == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        __hip_atomic_store(sticky, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+        const int e = __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (e) __hip_atomic_fetch_max(sticky, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 // Row layout of a sweep (host-chosen, gx_layout): G groups x MT tiles of RV <= 16 valid rows;
@@ -58,7 +60,8 @@ struct GruXArgs {
     bf16* hp_lp;                                    // optional: h_{t-1} (bf16), same layout as out
     float* gates; int64_t ldg; int64_t sg;          // r | z | n | gh_n per row and step
     u64* xh;                                        // 2 x G x MT x RG x D/2 granules
-    int* census;                                    // [G][P] zeroed slots, or null (global mode)
+    int* census;                                    // [G][P] zeroed slots (arrival + placement)
+    int nolocal;                                    // 1: global-mode hand-offs (SRNN_GEN_LOCAL=0)
     int* err;
     int* sticky;                                    // persist.hip flag
     int spin_limit;
@@ -85,7 +88,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     // static map (handoff.hpp): group g = block % G, member p = block / G; the placement
     // check runs while the weights load
     const int g = blockIdx.x % a.G, p = blockIdx.x / a.G;
-    if (a.census && tid == 0) hx_group_arrive(a.census + g * a.P + p);
+    if (tid == 0) hx_group_arrive(a.census + g * a.P + p);
     const int u0 = p * CU;
     const int DG = D / 2;
     unsigned long long* dg = (a.diag && blockIdx.x == 0 && tid == 0) ? a.diag : nullptr;
@@ -116,7 +119,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
         }
     }
     if (wave == 0) {
-        const int loc = a.census && hx_group_local(a.census + g * a.P, a.P, a.err) ? 1 : 0;
+        const int loc = hx_group_local(a.census + g * a.P, a.P, a.err, !a.nolocal) ? 1 : 0;
         if (tid == 0) gsh[2] = loc;
     }
     __syncthreads();
@@ -316,6 +319,7 @@ struct GruXBwdArgs {
     float* ddir0;                                   // (B, D)
     u64* xg;                                        // 2 x G x MT x RG x 3D/2 granules
     int* census;
+    int nolocal;
     int* err;
     int* sticky;
     int spin_limit;
@@ -338,7 +342,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
     // static map (handoff.hpp): group g = block % G, member p = block / G; the placement
     // check runs while the weights load
     const int g = blockIdx.x % a.G, p = blockIdx.x / a.G;
-    if (a.census && tid == 0) hx_group_arrive(a.census + g * a.P + p);
+    if (tid == 0) hx_group_arrive(a.census + g * a.P + p);
     const int u0 = p * CU;
     const int KG = K3 / 2;                                      // granules per row
     bf16x8 wf[UPW][NTB];
@@ -365,7 +369,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_kernel(GruXBwdArgs a)
         }
     }
     if (wave == 0) {
-        const int loc = a.census && hx_group_local(a.census + g * a.P, a.P, a.err) ? 1 : 0;
+        const int loc = hx_group_local(a.census + g * a.P, a.P, a.err, !a.nolocal) ? 1 : 0;
         if (tid == 0) gsh[2] = loc;
     }
     __syncthreads();
@@ -570,7 +574,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
     const size_t red_bytes = (size_t)2 * KW * NTB * 4 * PS * sizeof(float);
     int* gsh = (int*)(smem + red_bytes);
     const int g = blockIdx.x % a.G, p = blockIdx.x / a.G;
-    if (a.census && tid == 0) hx_group_arrive(a.census + g * a.P + p);
+    if (tid == 0) hx_group_arrive(a.census + g * a.P + p);
     const int u0 = p * CU;
     bf16x8 wf[UPW][NTB];
     {
@@ -600,7 +604,7 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
             }
     }
     if (wave == 0) {
-        const int loc = a.census && hx_group_local(a.census + g * a.P, a.P, a.err) ? 1 : 0;
+        const int loc = hx_group_local(a.census + g * a.P, a.P, a.err, !a.nolocal) ? 1 : 0;
         if (tid == 0) gsh[2] = loc;
     }
     __syncthreads();
@@ -755,7 +759,6 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
 }
 
 // ------------------------------------------------------------------ host side
-static int g_gx_ncu = 0;
 
 static unsigned long long*& gx_diag_buf() {
     static unsigned long long* p = nullptr;
@@ -774,15 +777,11 @@ extern "C" int srnn_gru_diag_dump(void) {
     return 0;
 }
 
+// CUs one process's sweep may count on: the device's, divided among the processes that run
+// persistent kernels on it at once (persist.hip, srnn_set_device_share) -- every launch's
+// G x P workgroups then fit beside theirs (handoff.hpp co-residency)
 static int gx_cus() {
-    if (!g_gx_ncu) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&g_gx_ncu, hipDeviceAttributeMultiprocessorCount, dev) !=
-                hipSuccess)
-            g_gx_ncu = 0;
-    }
-    return g_gx_ncu;
+    return srnn_device_cus() / srnn_device_share();
 }
 
 // Row layout of one launch for B rows at width D (GruXArgs): false if the device or shape
@@ -861,7 +860,8 @@ extern "C" int srnn_gru_xcd_fwd2(int dtype, int B, int D, int Fr, const float* g
     SRNN_REQUIRE(a.sticky, "gru_xcd: sticky flag allocation failed");
     a.spin_limit = srnn_persist_spin_limit(hx::SPIN_LIMIT);
     a.withhold = env_flag("SRNN_PERSIST_FORCE_FAIL", 0);
-    a.census = env_flag("SRNN_GEN_LOCAL", 1) ? (int*)work + 16 : nullptr;
+    a.census = (int*)work + 16;
+    a.nolocal = !env_flag("SRNN_GEN_LOCAL", 1);
     a.xh = (u64*)((char*)work + gx::HDR);
     a.B = B; a.D = D; a.Fr = Fr;
     a.diag = nullptr;
@@ -903,6 +903,8 @@ extern "C" int srnn_gru_xcd_fwd2(int dtype, int B, int D, int Fr, const float* g
                                            160 * 1024));
         attr[ai][mi] = true;
     }
+    if (srnn_persist_check((const void*)k, gx::NTHR, lds, (int64_t)a.G * a.P, "gru_xcd_fwd"))
+        return 1;
     hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;
@@ -977,7 +979,8 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
     SRNN_REQUIRE(a.sticky, "gru_xcd_bwd: sticky flag allocation failed");
     a.spin_limit = srnn_persist_spin_limit(hx::SPIN_LIMIT);
     a.withhold = env_flag("SRNN_PERSIST_FORCE_FAIL", 0);
-    a.census = env_flag("SRNN_GEN_LOCAL", 1) ? (int*)work + 16 : nullptr;
+    a.census = (int*)work + 16;
+    a.nolocal = !env_flag("SRNN_GEN_LOCAL", 1);
     a.xg = (u64*)((char*)work + gx::HDR);
     a.B = B; a.D = D; a.Fr = Fr;
     a.exp = env_flag("SRNN_GX_EXP", 0);
@@ -999,6 +1002,8 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
              gru_xcd_bwd_pk_kernel<16, 4>}};
         const int mi = L.mt == 1 ? 0 : L.mt == 2 ? 1 : 2;
         const PkK k = kp[D / 256 - 1][mi];
+        if (srnn_persist_check((const void*)k, gx::NTHR, lds, (int64_t)a.G * a.P, "gru_xcd_bwd"))
+            return 1;
         hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
         SRNN_LAUNCH_CHECK();
         return 0;
@@ -1022,6 +1027,8 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
           gru_xcd_bwd_kernel<12, true, 4>}}};
     const BwdK k = ks[full ? 1 : 0][ui][mi];
     SRNN_REQUIRE(k, "gru_xcd_bwd: no kernel for D=%d", D);
+    if (srnn_persist_check((const void*)k, gx::NTHR, lds, (int64_t)a.G * a.P, "gru_xcd_bwd"))
+        return 1;
     hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;

@@ -33,6 +33,14 @@ static inline int env_flag(const char* name, int dflt) {
 // SRNN_PERSIST_FORCE_FAIL test switch is set)
 int* srnn_sticky_flag();
 int srnn_persist_spin_limit(int dflt);
+// persist.hip: co-residency of persistent grids (handoff.hpp) -- CUs of the current device,
+// whether `blocks` one-per-CU workgroups fit it for every process sharing it, and the
+// launch-time check with the kernel's occupancy (0 = fits, else reported error)
+int srnn_device_cus();
+extern "C" int srnn_device_share(void);
+int srnn_persist_fits_cus(int64_t blocks);
+int srnn_persist_check(const void* kernel, int threads, size_t lds, int64_t blocks,
+                       const char* what);
 
 // gemm3.hip: grow-only device scratch buffers, one per slot, never freed (a captured HIP graph
 // keeps the pointer current at its capture); null on a HIP error.  Allocated on first use,

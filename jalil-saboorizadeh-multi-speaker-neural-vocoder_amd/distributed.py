@@ -61,6 +61,28 @@ def init(backend=None):
         dist.init_process_group(backend, device_id=torch.device('cuda', device_index()))
     else:
         dist.init_process_group(backend)
+    _declare_device_share()
+
+
+def _declare_device_share():
+    """Ranks of this node that map onto one GPU (a rehearsal: more local ranks than visible
+    devices) each run persistent sweeps on it at once.  Their grids are only co-resident if
+    they fit the device together, so the HIP library is told how many processes share it
+    (samplernn_hip.set_device_share): launches are then sized to 1/share of the CUs or take
+    the per-step kernels -- declared up front instead of a sweep waiting on CUs that another
+    process's sweep holds."""
+    n = torch.cuda.device_count()
+    if n <= 0:
+        return 1
+    lws = int(os.environ.get('LOCAL_WORLD_SIZE', str(world())))
+    share = (lws + n - 1) // n
+    if share > 1:
+        import warnings
+        import samplernn_hip as H
+        warnings.warn('%d ranks share each GPU: persistent kernels are sized to 1/%d of its CUs'
+                      % (share, share))
+        H.set_device_share(share)
+    return share
 
 
 def shard_rows(total_rows, r=None, n=None):

@@ -69,6 +69,8 @@ _SIGS = {
     'srnn_gather_rows': [_P, _L, _P, _L, _I, _P, _I, _L, _P],
     'srnn_scatter_add_rows': [_P, _L, _P, _L, _I, _P, _L, _P],
     'srnn_index_add_rows': [_P, _L, _I, _P, _L, _I, _P, _L, _P],
+    'srnn_set_device_share': [_I],
+    'srnn_hold_cus': [_I, _I, _P, _P],
     'srnn_axpby': [_P, _P, _P, _F, _F, _L, _P],
     'srnn_add_bcast_rows': [_P, _P, _I, _I, _I, _L, _P],
     'srnn_segsum': [_P, _L, _I, _I, _I, _P, _P],
@@ -184,7 +186,7 @@ def exported_symbols():
                             'srnn_gen_persistent_rows', 'srnn_gru_xcd_work_bytes',
                             'srnn_gru_xcd_bwd_work_bytes', 'srnn_gru_xcd_error',
                             'srnn_persistent_error_take', 'srnn_gemm_amax_taken',
-                            'srnn_gemm_csum_taken', 'srnn_blaslt_calls']
+                            'srnn_gemm_csum_taken', 'srnn_blaslt_calls', 'srnn_device_share']
 
 
 # Callbacks run just before a persistent sweep (gru_xcd / gru_seq) is enqueued.  Such a sweep
@@ -257,10 +259,25 @@ def check_persistent_errors():
     fn.restype = ctypes.c_int
     fn.argtypes = []
     v = fn()
+    if v == 2:
+        raise RuntimeError('persistent GRU sweep: its workgroups were not all resident within '
+                           '30 s (another process holds the CUs; see set_device_share) -- results '
+                           'of this step are invalid')
     if v:
         raise RuntimeError('persistent GRU sweep gave up a hand-off (bounded spin) -- results of '
                            'this step are invalid' if v > 0 else
                            'srnn_persistent_error_take: HIP error')
+
+
+def set_device_share(n):
+    """Declare that n processes run persistent kernels on this process's GPU at once (a
+    multi-rank rehearsal on one GPU; 1 normally).  Persistent sweeps and the generation loop
+    then only take launch shapes whose grids fit the device n times over (their co-residency
+    guarantee, csrc/handoff.hpp), chaining smaller launches or taking the per-step kernels
+    otherwise.  Call before the first model step (the support predicates are cached)."""
+    lib().call('srnn_set_device_share', int(n))
+    _GRU_XCD.clear()
+    _GRU_SEQ.clear()
 
 
 class PersistentErrorWatch:
