@@ -6,8 +6,9 @@
 //    speaker projections (dW = dX^T . input, N = frame samples, cond_dim, spk_dim) with K =
 //    all frames of the batch, and the speaker-embedding gradient.  A thread owns one output
 //    row m and all N columns in registers; the workgroup's K chunk of B is staged in LDS
-//    and read as broadcasts; K is split over workgroups and the partial rows meet with
-//    fp32 atomics (C zeroed first), so the grid fills the chip whatever M is.
+//    and read as broadcasts; K is split over workgroups, whose partial rows go to a scratch
+//    and are summed in split order by a second kernel (deterministic: no atomics), so the
+//    grid fills the chip whatever M is.
 //  * small K (K <= 64, NT): the input projections of the tiers (frame samples -> dim,
 //    cond_dim -> dim) with the upper-tier conditioning added (beta * Cin) and the bias:
 //    a thread computes 4 adjacent columns of one row from LDS-staged rows of A and B, so
@@ -29,7 +30,7 @@ __global__ __launch_bounds__(256) void gemm_small_n_kernel(const T* __restrict__
                                                            const T* __restrict__ B, int64_t ldb,
                                                            float* __restrict__ C, int64_t ldc,
                                                            int M, int N, int K, int kchunk,
-                                                           float alpha, int atomic) {
+                                                           float alpha, float* __restrict__ P) {
     constexpr int KC = 32;
     __shared__ float bs[KC][NMAX];
     const int m = blockIdx.x * 256 + threadIdx.x;
@@ -61,15 +62,23 @@ __global__ __launch_bounds__(256) void gemm_small_n_kernel(const T* __restrict__
             for (int n = 0; n < NMAX; ++n) acc[n] += a[kk] * bs[kk][n];
     }
     if (m >= M) return;
+    if (P) {            // split K: this split's partial row, P[z][n][m] (summed in z order)
+        float* pp = P + (int64_t)blockIdx.z * N * M + m;
+#pragma unroll
+        for (int n = 0; n < NMAX; ++n)
+            if (n0 + n < N) pp[(int64_t)(n0 + n) * M] = acc[n];
+        return;
+    }
     float* c = C + (int64_t)m * ldc + n0;
 #pragma unroll
-    for (int n = 0; n < NMAX; ++n) {
-        if (n0 + n < N) {
-            if (atomic) atomicAdd(c + n, alpha * acc[n]);
-            else c[n] = alpha * acc[n];
-        }
-    }
+    for (int n = 0; n < NMAX; ++n)
+        if (n0 + n < N) c[n] = alpha * acc[n];
 }
+
+__global__ __launch_bounds__(256) void gemm_small_nt_sum_kernel(const float* __restrict__ P,
+                                                                float* __restrict__ C,
+                                                                int64_t ldc, int M, int N,
+                                                                int nks, float alpha);
 
 template <typename T, bool TA>
 static int launch_small_n(const void* A, int64_t lda, const void* B, int64_t ldb, float* C,
@@ -81,21 +90,25 @@ static int launch_small_n(const void* A, int64_t lda, const void* B, int64_t ldb
     int nks = std::max(1, std::min(cdiv(K, 64), 1024 / (mblk * ngrp)));
     const int kchunk = ((cdiv(K, nks) + 31) / 32) * 32;
     nks = cdiv(K, kchunk);
+    float* P = nullptr;
     if (nks > 1) {
-        if (ldc == N) {
-            SRNN_CHECK_HIP(hipMemsetAsync(C, 0, (size_t)M * N * 4, s));
-        } else {
-            SRNN_CHECK_HIP(hipMemset2DAsync(C, ldc * 4, 0, (size_t)N * 4, M, s));
-        }
+        P = (float*)srnn_scratch(SRNN_SCRATCH_NT, (size_t)nks * N * M * sizeof(float));
+        SRNN_REQUIRE(P, "gemm_small: split-K scratch allocation failed");
     }
     dim3 grid(mblk, ngrp, nks);
     if (NM == 8)
         hipLaunchKernelGGL((gemm_small_n_kernel<T, TA, 8>), grid, dim3(256), 0, s, (const T*)A,
-                           lda, (const T*)B, ldb, C, ldc, M, N, K, kchunk, alpha, nks > 1 ? 1 : 0);
+                           lda, (const T*)B, ldb, C, ldc, M, N, K, kchunk, alpha, P);
     else
         hipLaunchKernelGGL((gemm_small_n_kernel<T, TA, 16>), grid, dim3(256), 0, s, (const T*)A,
-                           lda, (const T*)B, ldb, C, ldc, M, N, K, kchunk, alpha, nks > 1 ? 1 : 0);
+                           lda, (const T*)B, ldb, C, ldc, M, N, K, kchunk, alpha, P);
     SRNN_LAUNCH_CHECK();
+    if (P) {
+        const int64_t tot = (int64_t)M * N;
+        hipLaunchKernelGGL(gemm_small_nt_sum_kernel, dim3((unsigned)cdiv(tot, (int64_t)256)),
+                           dim3(256), 0, s, P, C, ldc, M, N, nks, alpha);
+        SRNN_LAUNCH_CHECK();
+    }
     return 0;
 }
 
