@@ -676,6 +676,11 @@ def main():
         generation_goldens('a', n_seqs=2, num_cond=32, seed=37, gen_seed=13)
         # configs[2]'s model: 2 rows x 75 top-tier frames = 4,800 samples
         generation_long_goldens('big', n_seqs=2, num_cond=75, seed=38, gen_seed=14, tag='big')
+    if want('e4'):
+        # round 5: configs[4]'s model (4-tier, dim 1024, FS [16, 4, 4], look-ahead cond 86):
+        # generation 2 rows x 2 top-tier frames = 512 samples, and a forward chunk
+        generation_goldens('e', n_seqs=2, num_cond=2, seed=39, gen_seed=15)
+        forward_goldens('e', B=1, T=1024, n_chunks=1, seed=40, keep_rows=list(range(0, 1024, 16)))
     print('done in %.1fs' % (time.time() - t0))
 
 

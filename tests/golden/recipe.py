@@ -161,6 +161,10 @@ CONFIGS = {
                     cond_dim=43, spk_dim=6, learn_h0=False),
     'big': dict(frame_sizes=[16, 4], n_rnn=1, dim=1024, q_levels=256, weight_norm=False,
                 cond_dim=43, spk_dim=6, learn_h0=True),
+    # configs[4]: 4-tier, dim 1024, FS [16, 4, 4], look-ahead conditioning (train.py:213:
+    # cond_dim x (1 + look_ahead) = 86), 6 speakers
+    'e': dict(frame_sizes=[16, 4, 4], n_rnn=1, dim=1024, q_levels=256, weight_norm=False,
+              cond_dim=86, spk_dim=6, learn_h0=True),
     # configs[0]: 2-tier, dim 256, one speaker (train.py:201 counts speaker directories, so a
     # single-speaker dataset gives spk_dim = 1), the train.py defaults otherwise
     'a': dict(frame_sizes=[16], n_rnn=1, dim=256, q_levels=256, weight_norm=False,

@@ -26,7 +26,7 @@ def build(cfg, weights, dtype=torch.float32):
     return m.to(DEV), pred.to(DEV)
 
 
-@pytest.mark.parametrize('name', ['t2', 't3', 't3r2wn', 't4la', 't3_20_4', 'big', 'a'])
+@pytest.mark.parametrize('name', ['t2', 't3', 't3r2wn', 't4la', 't3_20_4', 'big', 'a', 'e'])
 def test_forward_golden(hip, name):
     g = golden('fwd_' + name)
     cfg = recipe.CONFIGS[name]
@@ -48,12 +48,13 @@ def test_forward_golden(hip, name):
                                            g['hidden_%d_tier%d' % (n, t)], atol=2e-5, rtol=0)
 
 
-@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn', 'big', 'a'])
+@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn', 'big', 'a', 'e'])
 @pytest.mark.parametrize('graph,persistent', [(True, True), (False, True), (True, False),
                                               (False, False)])
 def test_generation_golden(hip, name, graph, persistent):
     """fp32 generation with the reference's replayed multinomial noise: index streams bit
-    for bit, log-probs 1e-4 ('big' = configs[2]'s dim-1024 model, 128 samples)."""
+    for bit, log-probs 1e-4 ('big' = configs[2]'s dim-1024 model, 128 samples; 'e' =
+    configs[4]'s 4-tier dim-1024 look-ahead model, FS [16, 4, 4], 512 samples)."""
     import model as M
     g = golden('gen_' + name)
     cfg = recipe.CONFIGS[name]

@@ -56,7 +56,7 @@ def test_samples_wav_on_lut_grid():
     assert len(f32) == 17 and all(l % 80 == 0 for l in f32)
 
 
-@pytest.mark.parametrize('name', ['t2', 't3', 't3r2wn', 't4la', 't3_20_4', 'big'])
+@pytest.mark.parametrize('name', ['t2', 't3', 't3r2wn', 't4la', 't3_20_4', 'big', 'e'])
 def test_oracle_forward(name):
     g = golden('fwd_' + name)
     cfg = recipe.CONFIGS[name]
@@ -75,7 +75,7 @@ def test_oracle_forward(name):
                                            atol=2e-6, rtol=0)
 
 
-@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn', 'big'])
+@pytest.mark.parametrize('name', ['t2', 't3', 't4la', 't3_20_4', 't3r2wn', 'big', 'e'])
 def test_oracle_generation(name):
     g = golden('gen_' + name)
     cfg = recipe.CONFIGS[name]
