@@ -164,10 +164,77 @@ template <> __device__ __forceinline__ float gm_tap_load<float>(__amdgpu_buffer_
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
 }
 
+// ---- in-launch tick GEMM (TG kernels) --------------------------------------------------
+// up0 = A W^T + bias for all B (<= 128) rows; workgroup w takes 16-column tiles
+// [w ntl / nblk, (w + 1) ntl / nblk) (<= 5 of them).  Both operands stream through a 2-slot
+// LDS ring of 64-deep k chunks by global_load_lds (128-B rows, 16-B slots XOR-swizzled by
+// (row >> 1) & 7: conflict-free fragment reads), one chunk ahead; wave w owns output rows
+// [16 w, 16 w + 16).  The MFMA runs with the operands swapped, so a lane holds 4 consecutive
+// columns of one row: the epilogue is one 16-B write-through (sc1) store per tile.  The
+// fragment reads are inline asm and every wait is counted by hand: the resident-fragment
+// loads of the prologue are issued between the chunks and must stay in flight across them.
+namespace gmt {
+constexpr int KC = 64;                  // k per chunk
+constexpr int ROWB = KC * 2;            // 128 B per staged row (8 x 16-B slots)
+constexpr int AROWS = 128;              // A rows staged (B <= 128; clamped)
+constexpr int WROWS = 128;              // weight rows staged (<= 5 real tiles, clamped)
+constexpr int ASLOT = AROWS * ROWB, WSLOT = WROWS * ROWB;   // 16 KiB each
+constexpr int SLOT = ASLOT + WSLOT;
+constexpr int LDS = 2 * SLOT;
+constexpr int PA = ASLOT / 1024 / gm::NW;      // DMA pieces per wave per chunk per operand (2)
+constexpr int PW = WSLOT / 1024 / gm::NW;
+constexpr int WORDS = 1280;             // grid-barrier words start at gerr + WORDS
+}  // namespace gmt
+
+#define GMT_LDS(p) ((__attribute__((address_space(3))) void*)(p))
+#define GMT_GLB(p) ((const __attribute__((address_space(1))) void*)(p))
+
+template <int N>
+__device__ __forceinline__ void gmt_wait_vm() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// Grid barrier of the TG kernels (MI355X guide, valid form R1): every storing thread drains
+// its write-through stores, the workgroup joins, one lane publishes `epoch` (monotonic within
+// a generate call) in its word, and wave 0 polls every word with sc1 loads; the other waves
+// wait at the closing workgroup barrier.  Bounded by the co-residency wall-time guard
+// (handoff.hpp): on a timeout (or another workgroup's error) the error word is raised and the
+// launch runs out through the hand-off spins' checks.
+__device__ __forceinline__ void gmt_grid_barrier(int* bar, int nblk, int epoch, int* err) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(bar + blockIdx.x, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        int polls = 0;
+        for (;;) {
+            bool done = true;
+            for (int q = lane; q < nblk; q += 64)
+                done &= __hip_atomic_load(bar + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= epoch;
+            if (__all(done)) break;
+            __builtin_amdgcn_s_sleep(2);
+            if ((++polls & 63) == 0) {
+                if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+                if (__builtin_amdgcn_s_memrealtime() - t0 > hx::ARRIVAL_TICKS) {
+                    if (lane == 0)
+                        __hip_atomic_fetch_max(err, hx::ERR_RESIDENCY, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+            }
+        }
+    }
+    __syncthreads();
+}
+
 // FS0C: FS0 as a compile-time constant (0: runtime a.FS0).  DC: the whole launch shape as
 // constants -- D = DC, R = 8, CW = 64, NZ = Q / (D / 64) (0: runtime); the per-unit validity
 // masks of the runtime shape would otherwise be scalar-register spills in the loop.
-template <typename T, int UPW, int NT, int NZT, int MAXT, int FS0C, int DC>
+// TG: the bottom tick's GEMM runs in this launch before the sample loop (GenMlpArgs::tg;
+// bf16 only), with the prologue's resident-fragment loads in flight beside it.
+template <typename T, int UPW, int NT, int NZT, int MAXT, int FS0C, int DC, bool TG = false>
 __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
     using F = typename GmT<T>::frag;
     constexpr int GV = GmT<T>::GV, UK = GmT<T>::UK, EPL = UK / 4;
@@ -247,25 +314,172 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         const uint4* fh = reinterpret_cast<const uint4*>(a.wfr_hid);
         const uint4* fo = reinterpret_cast<const uint4*>(a.wfr_out);
         const int nzt1 = nzt > 0 ? nzt : 1;
-#pragma unroll
-        for (int j = 0; j < UPW; ++j) {
+        auto ld_w = [&](int j, int t) {
             const int u = wave + gm::NW * j;
             const int uc = min(u, NU - 1);
             const int ke = min(u * UK + (lane >> 4) * EPL, D - EPL);
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                const int n = min(c0 + t * 16 + (lane & 15), D - 1);
-                lw[j][t] = fh ? fh[(((size_t)p * NU + uc) * nt + min(t, nt - 1)) * 64 + lane]
-                              : *reinterpret_cast<const uint4*>((const T*)a.w_hid + (int64_t)n * D + ke);
-            }
+            const int n = min(c0 + t * 16 + (lane & 15), D - 1);
+            // (TG: the images are required -- a load without a branch around it, which would
+            //  make the wait analysis drain every load in flight at the join)
+            if (TG || fh)
+                lw[j][t] = fh[(((size_t)p * NU + uc) * nt + min(t, nt - 1)) * 64 + lane];
+            else
+                lw[j][t] = *reinterpret_cast<const uint4*>((const T*)a.w_hid + (int64_t)n * D + ke);
+        };
+        auto ld_z = [&](int j, int t) {
             if constexpr (!WOL) {
+                const int u = wave + gm::NW * j;
+                const int uc = min(u, NU - 1);
+                const int ke = min(u * UK + (lane >> 4) * EPL, D - EPL);
+                const int n = min(z0 + t * 16 + (lane & 15), Q - 1);
+                if (TG || fo)
+                    lz[j][t] = fo[(((size_t)p * NU + uc) * nzt1 + min(t, nzt1 - 1)) * 64 + lane];
+                else
+                    lz[j][t] = *reinterpret_cast<const uint4*>((const T*)a.w_out + (int64_t)n * D + ke);
+            }
+        };
+        constexpr int PER = 16 / sizeof(T);
+        const int cpr = CW / PER;                       // pieces per table row
+        const int npc = Q * cpr;
+        constexpr int MAXIT = gm::Q * 64 * (int)sizeof(T) / 16 / gm::NTHR;   // CW = 64: 4 / 8
+        uint4 buf[MAXIT];
+        auto ld_tab = [&](int it) {
+            const int e = min(tid + it * gm::NTHR, npc - 1);
+            const int q = e / cpr, c = (e % cpr) * PER;
+            const T* src = tab + ((int64_t)(FS0 - 1) * Q + q) * D + c0 + c;
+            if constexpr (TG) {
+                // straight into the LDS slice (piece e at e * 16 B: this wave's 64 pieces of
+                // round it are one contiguous KiB; npc is a multiple of the 512 threads here)
+                __builtin_amdgcn_global_load_lds(
+                    GMT_GLB(src), GMT_LDS(reinterpret_cast<char*>(tab15) +
+                                          (size_t)(it * gm::NTHR + wave * 64) * 16),
+                    16, 0, 0);
+            } else {
+                buf[it] = *reinterpret_cast<const uint4*>(src);
+            }
+        };
+        // every resident-fragment / table load, in issue order
+        constexpr int NLW = UPW * NT, NLZ = WOL ? 0 : UPW * NZT, NLD = NLW + NLZ + MAXIT;
+        auto ld = [&](int i) {
+            if (i < NLW) ld_w(i / NT, i % NT);
+            else if (i < NLW + NLZ) ld_z((i - NLW) / NZT, (i - NLW) % NZT);
+            else ld_tab(i - NLW - NLZ);
+        };
+        if constexpr (TG) {
+            // ---- the bottom tick's GEMM (GenMlpArgs::tg), the fragment loads interleaved:
+            // group c (4 loads, chunks 0 .. 6) is issued after chunk c + 1's DMA, so it is
+            // younger than the chunk waited for next and lands while the GEMM runs (vmcnt is
+            // in order)
+            using namespace gmt;
+            static_assert(DC == 1024 && NLD == 28, "TG: 7 groups of 4 loads over 16 chunks");
+            constexpr int NCH = DC / KC;
+            const int nblk = a.G * a.P;
+            const int ntl = a.tg.N / 16;
+            const int tb0 = (int)((int64_t)blockIdx.x * ntl / nblk);
+            const int tb1 = (int)((int64_t)(blockIdx.x + 1) * ntl / nblk);
+            char* stg = reinterpret_cast<char*>(gsh) + 16;
+            const bf16* asrc[PA];
+            const bf16* wsrc[PW];
 #pragma unroll
-                for (int t = 0; t < NZT; ++t) {
-                    const int n = min(z0 + t * 16 + (lane & 15), Q - 1);
-                    lz[j][t] = fo ? fo[(((size_t)p * NU + uc) * nzt1 + min(t, nzt1 - 1)) * 64 + lane]
-                                  : *reinterpret_cast<const uint4*>((const T*)a.w_out + (int64_t)n * D + ke);
+            for (int i = 0; i < PA; ++i) {
+                const int r = 8 * (wave * PA + i) + (lane >> 3);           // A row 0..127
+                const int sl = (lane & 7) ^ ((r >> 1) & 7);
+                asrc[i] = reinterpret_cast<const bf16*>(a.tg.A) + (int64_t)min(r, a.B - 1) * DC +
+                          sl * 8;
+            }
+#pragma unroll
+            for (int i = 0; i < PW; ++i) {
+                const int r = 8 * (wave * PW + i) + (lane >> 3);           // weight row 0..127
+                const int tile = min(tb0 + r / 16, tb1 - 1);
+                const int sl = (lane & 7) ^ ((r >> 1) & 7);
+                wsrc[i] = reinterpret_cast<const bf16*>(a.tg.W) +
+                          (int64_t)(tile * 16 + (r & 15)) * DC + sl * 8;
+            }
+            auto dma = [&](int ch) {
+                char* slot = stg + (ch & 1) * SLOT;
+#pragma unroll
+                for (int i = 0; i < PA; ++i)
+                    __builtin_amdgcn_global_load_lds(GMT_GLB(asrc[i] + ch * KC),
+                                                     GMT_LDS(slot + (wave * PA + i) * 1024), 16, 0, 0);
+#pragma unroll
+                for (int i = 0; i < PW; ++i)
+                    __builtin_amdgcn_global_load_lds(
+                        GMT_GLB(wsrc[i] + ch * KC), GMT_LDS(slot + ASLOT + (wave * PW + i) * 1024),
+                        16, 0, 0);
+            };
+            floatx4 acc[5];
+#pragma unroll
+            for (int t = 0; t < 5; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            const unsigned lbase = (unsigned)(uintptr_t)GMT_LDS(stg);
+            dma(0);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int ch = 0; ch < NCH; ++ch) {
+                if (ch + 1 < NCH) dma(ch + 1);
+                if (ch < 7) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) ld(ch * 4 + i);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                // chunk ch landed: younger ops are fragment groups ch - 1 and ch (4 each, chunks
+                // 0 .. 6) and chunk ch + 1's 4 DMA pieces
+                if (ch == 0) gmt_wait_vm<4 + 4>();
+                else if (ch < 7) gmt_wait_vm<4 + 4 + 4>();
+                else if (ch == 7) gmt_wait_vm<4 + 4>();
+                else if (ch + 1 < NCH) gmt_wait_vm<4>();
+                else gmt_wait_vm<0>();
+                // (raw barrier: __syncthreads would also drain vmcnt -- the fragment loads)
+                __builtin_amdgcn_s_barrier();
+                const unsigned sa = lbase + (unsigned)((ch & 1) * SLOT);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int j = u * 4 + (lane >> 4);
+                    bf16x8 af, bfr[5];
+                    {
+                        const int r = 16 * wave + (lane & 15);
+                        const unsigned ad = sa + (unsigned)(r * ROWB + ((j ^ ((r >> 1) & 7)) * 16));
+                        asm volatile("ds_read_b128 %0, %1" : "=v"(af) : "v"(ad) : "memory");
+                    }
+#pragma unroll
+                    for (int t = 0; t < 5; ++t) {
+                        const int r = t * 16 + (lane & 15);
+                        const unsigned ad =
+                            sa + (unsigned)(ASLOT + r * ROWB + ((j ^ ((r >> 1) & 7)) * 16));
+                        asm volatile("ds_read_b128 %0, %1" : "=v"(bfr[t]) : "v"(ad) : "memory");
+                    }
+                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                    for (int t = 0; t < 5; ++t)
+                        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[t], af, acc[t], 0, 0, 0);
+                }
+                __builtin_amdgcn_s_barrier();      // slot (ch & 1) is chunk ch + 2's
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // epilogue: lane holds C[m][n .. n + 3] of each tile; 16-B write-through stores
+            const int m = 16 * wave + (lane & 15);
+            const __amdgpu_buffer_rsrc_t rcw =
+                __builtin_amdgcn_make_buffer_rsrc(a.tg.C, (short)0, 0x7fffffff, 0x00020000);
+            typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
+            floatx4 bq[5];
+#pragma unroll
+            for (int t = 0; t < 5; ++t)
+                bq[t] = *reinterpret_cast<const floatx4*>(
+                    a.tg.bias + min(tb0 + t, tb1 - 1) * 16 + (lane >> 4) * 4);
+#pragma unroll
+            for (int t = 0; t < 5; ++t) {
+                if (t < tb1 - tb0 && m < a.B) {
+                    const int n = (tb0 + t) * 16 + (lane >> 4) * 4;
+                    __builtin_amdgcn_raw_buffer_store_b128(
+                        __builtin_bit_cast(u32x4_, acc[t] + bq[t]), rcw,
+                        (int)(((int64_t)m * a.tg.ldc + n) * 4), 0, 16 /* sc1 */);
                 }
             }
+            // every workgroup's part of up0 is out before any sample loop reads it
+            const int epoch = (*a.base + a.off - a.L) / FS0 + 1;
+            gmt_grid_barrier(a.tg.bar, nblk, epoch, a.err);
+        } else {
+#pragma unroll
+            for (int i = 0; i < NLD; ++i) ld(i);
         }
         if constexpr (WOL) {
             // rows z0 .. z0 + 15 of W_out into LDS (16-B pieces; NZ = 16 at D = 1024)
@@ -276,18 +490,6 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                     *reinterpret_cast<const uint4*>((const T*)a.w_out +
                                                     (int64_t)min(z0 + n, Q - 1) * D + k);
             }
-        }
-        constexpr int PER = 16 / sizeof(T);
-        const int cpr = CW / PER;                       // pieces per table row
-        const int npc = Q * cpr;
-        constexpr int MAXIT = gm::Q * 64 * 4 / 16 / gm::NTHR;   // fp32, CW = 64: 8
-        uint4 buf[MAXIT];
-#pragma unroll
-        for (int it = 0; it < MAXIT; ++it) {
-            const int e = min(tid + it * gm::NTHR, npc - 1);
-            const int q = e / cpr, c = (e % cpr) * PER;
-            buf[it] = *reinterpret_cast<const uint4*>(
-                tab + ((int64_t)(FS0 - 1) * Q + q) * D + c0 + c);
         }
         // placement check (wave 0, after its own loads are in flight)
         if (wave == 0) {
@@ -322,10 +524,12 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         }
         // newest-tap table slice (Q x CW, loaded in 16-B pieces above, before the census wait)
         // (clamped pieces store the same bytes to the same slot: no branch)
+        if constexpr (!TG) {     // (TG: loaded straight into LDS, landed at the grid barrier)
 #pragma unroll
-        for (int it = 0; it < MAXIT; ++it) {
-            const int e = min(tid + it * gm::NTHR, npc - 1);
-            *reinterpret_cast<uint4*>(tab15 + (size_t)e * PER) = buf[it];
+            for (int it = 0; it < MAXIT; ++it) {
+                const int e = min(tid + it * gm::NTHR, npc - 1);
+                *reinterpret_cast<uint4*>(tab15 + (size_t)e * PER) = buf[it];
+            }
         }
         GM_STAMP();
     }
@@ -361,7 +565,14 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         const float* gr = a.tk->G + (int64_t)tb * a.tk->ldg;
         const float* hr = a.tk->gh + (int64_t)tb * a.tk->ldgh;
         tg[0] = gr[tu]; tg[1] = gr[D + tu]; tg[2] = gr[2 * D + tu];
-        tg[3] = hr[tu]; tg[4] = hr[D + tu]; tg[5] = hr[2 * D + tu];
+        if constexpr (TG) {     // gh: this launch's GEMM output (sc1 loads, as up0)
+            float* hw = const_cast<float*>(hr);
+            tg[3] = __hip_atomic_load(hw + tu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tg[4] = __hip_atomic_load(hw + D + tu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            tg[5] = __hip_atomic_load(hw + 2 * D + tu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            tg[3] = hr[tu]; tg[4] = hr[D + tu]; tg[5] = hr[2 * D + tu];
+        }
         tg[6] = a.tk->hp[(int64_t)tb * D + tu];
     }
     __syncthreads();
@@ -388,7 +599,14 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             const uint32_t row = (uint32_t)xs[k] + (uint32_t)((k < FS0 - 1 ? k : 0) * Q);
             tv[k] = gm_tap_load<T>(rtab, row * (uint32_t)D * (uint32_t)sizeof(T) + colb);
         }
-        upv = a.up0[(int64_t)eb * a.ldup + (int64_t)(i % FS0) * D + c0 + ec];
+        {
+            // (TG: up0 was written in this launch by other workgroups, write-through: every
+            //  load of it an sc1 load -- MI355X guide, valid forms)
+            const float* up = a.up0 + (int64_t)eb * a.ldup + (int64_t)(i % FS0) * D + c0 + ec;
+            upv = TG ? __hip_atomic_load(const_cast<float*>(up), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT)
+                     : *up;
+        }
     };
     auto finish_part = [&]() {
         float v = upv;
@@ -746,6 +964,13 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     const GmKernel k = dtype == SRNN_BF16 ? pick<bf16>(upw, NZ / 16, FS0, D, R)
                                           : pick<float>(upw, NZ / 16, FS0, D, R);
     if (!k) return 0;
+    // the in-launch tick GEMM variant (bf16, the compiled D = 1024 / FS0 = 16 shape);
+    // SRNN_GEN_TICK_GEMM=0 keeps the bottom tick's GEMM a launch of its own
+    pl->kernel_tg = nullptr;
+    pl->lds_tg = 0;
+    if (dtype == SRNN_BF16 && FS0 == 16 && D == 1024 && R == 8 && Q == gm::Q &&
+        env_flag("SRNN_GEN_TICK_GEMM", 1))
+        pl->kernel_tg = (const void*)gen_mlp_kernel<bf16, 4, 4, 2, 15, 16, 1024, true>;
     const int es = dtype == SRNN_BF16 ? 2 : 4;
     const int KW = NU < gm::NW ? NU : gm::NW;
     const int ntm = (CW / 16) > (NZ / 16) ? CW / 16 : NZ / 16;
@@ -756,6 +981,10 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     if (dtype == SRNN_F32 && upw > 4)                 // W_out slice in LDS (gen_mlp_kernel WOL)
         lds += (size_t)NZ * (D + 8) * 4;
     if (lds > 160 * 1024) return 0;
+    if (pl->kernel_tg) {
+        pl->lds_tg = lds + gmt::LDS;
+        if (pl->lds_tg > 160 * 1024) pl->kernel_tg = nullptr;
+    }
     pl->ok = 1;
     pl->local = env_flag("SRNN_GEN_LOCAL", 1);
     pl->dtype = dtype;
@@ -776,6 +1005,7 @@ int gen_mlp_plan(int dtype, int B, int D, int FS0, int Q, GenMlpPlan* pl) {
     pl->wfr_hid_bytes = (size_t)P * NU * nt * 64 * 16;
     pl->wfr_out_bytes = (dtype == SRNN_F32 && upw > 4) ? 0 : (size_t)P * NU * nzt * 64 * 16;
     if (!env_flag("SRNN_GEN_WFRAG", 1)) pl->wfr_hid_bytes = pl->wfr_out_bytes = 0;
+    if (!pl->wfr_hid_bytes || !pl->wfr_out_bytes) pl->kernel_tg = nullptr;   // (TG reads them)
     return 1;
 }
 
@@ -876,20 +1106,33 @@ int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
             gm_diag_buf() = diag;
         }
     }
-    const GmKernel k = (GmKernel)pl->kernel;
+    const bool tg = a.tg.N > 0;
+    if (tg) {
+        const int nblk = pl->G * pl->P;
+        SRNN_REQUIRE(pl->kernel_tg && a.wfr_hid && a.wfr_out,
+                     "gen_mlp: no in-launch tick GEMM for this shape");
+        SRNN_REQUIRE(a.tg.K == 1024 && a.tg.N % 16 == 0 && cdiv(a.tg.N / 16, nblk) <= 5 &&
+                         a.B <= 128 && a.tg.ldc % 4 == 0 && a.tg.A && a.tg.W && a.tg.bias &&
+                         a.tg.C && nblk <= 2048 - gmt::WORDS,
+                     "gen_mlp: tick GEMM shape (N %d, K %d, B %d) not supported", a.tg.N, a.tg.K,
+                     a.B);
+        a.tg.bar = a.err + gmt::WORDS;
+    }
+    const GmKernel k = (GmKernel)(tg ? pl->kernel_tg : pl->kernel);
+    const size_t lds = tg ? pl->lds_tg : pl->lds;
     // raise the dynamic-LDS limit once per kernel (not inside a graph capture's launches)
     static const void* done[16];
     static size_t done_lds[16];
     int slot = 0;
     while (slot < 16 && done[slot] && done[slot] != (const void*)k) ++slot;
-    if (slot == 16 || !done[slot] || done_lds[slot] < pl->lds) {
+    if (slot == 16 || !done[slot] || done_lds[slot] < lds) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
         if (slot < 16) { done[slot] = (const void*)k; done_lds[slot] = 160 * 1024; }
     }
-    if (srnn_persist_check((const void*)k, gm::NTHR, pl->lds, (int64_t)pl->G * pl->P, "gen_mlp"))
+    if (srnn_persist_check((const void*)k, gm::NTHR, lds, (int64_t)pl->G * pl->P, "gen_mlp"))
         return 1;
-    hipLaunchKernelGGL(k, dim3(pl->G * pl->P), dim3(gm::NTHR), pl->lds, s, a);
+    hipLaunchKernelGGL(k, dim3(pl->G * pl->P), dim3(gm::NTHR), lds, s, a);
     SRNN_LAUNCH_CHECK();
     return 0;
 }

@@ -470,6 +470,10 @@ struct Ctx {
     // upper tier's tick (its whole period)
     int noise_beg = 0, noise_end = -1;
     bool gate_done = false;   // the last persistent launch did the next bottom tick's gates
+    // the folded bottom tick's GEMM runs inside the persistent launch that follows it
+    // (GenMlpArgs::tg): set by tier_tick, consumed by that launch
+    bool tick_gemm = false;
+    GenMlpArgs::TickGemm pending{};
 };
 
 #define RET(x) do { int _r = (x); if (_r) return _r; } while (0)
@@ -491,11 +495,27 @@ int tier_tick(Ctx& c, int k, int off, int par) {
         const dim3 g2(cdiv(D, 256), cdiv(B, FG_RB));
         const int planes = 1;
         const int64_t fs0d = (int64_t)t.frame_size * D;
+        // [up | gh'] = h [W_up; W_hh]^T + [b_up; b_hh]: its own launch, or inside the
+        // persistent launch that follows (c.tick_gemm)
+        auto tick_gemm = [&]() -> int {
+            if (c.tick_gemm) {
+                SRNN_REQUIRE(c.pending.N == 0, "generate: tick GEMM left unconsumed");
+                c.pending.A = c.b.hlp[0][0][nxt];
+                c.pending.W = c.b.wcat;
+                c.pending.bias = c.b.bcat;
+                c.pending.C = c.b.up[0];
+                c.pending.ldc = c.b.ldup0;
+                c.pending.N = (int)(fs0d + 3 * D);
+                c.pending.K = D;
+                return 0;
+            }
+            return linear_fwd(dt, SRNN_F32, B, (int)(fs0d + 3 * D), D, c.b.hlp[0][0][nxt], D,
+                              c.b.wcat, D, c.b.bcat, c.b.up[0], c.b.ldup0, 0, c.s);
+        };
         if (c.gate_done) {
             // the gate update ran at the end of the last persistent launch (GenMlpArgs::tk)
             c.gate_done = false;
-            return linear_fwd(dt, SRNN_F32, B, (int)(fs0d + 3 * D), D, c.b.hlp[0][0][nxt], D,
-                              c.b.wcat, D, c.b.bcat, c.b.up[0], c.b.ldup0, 0, c.s);
+            return tick_gemm();
         }
         if (dt == SRNN_F32)
             hipLaunchKernelGGL((fold_gru_kernel<float>), dim3(g2.x, g2.y, planes), dim3(256), 0,
@@ -510,8 +530,7 @@ int tier_tick(Ctx& c, int k, int off, int par) {
                                c.b.up[0] + fs0d, c.b.ldup0, c.b.h[0][0][cur], c.b.h[0][0][nxt],
                                (bf16*)c.b.hlp[0][0][nxt], B, D, nz);
         SRNN_LAUNCH_CHECK();
-        return linear_fwd(dt, SRNN_F32, B, (int)(fs0d + 3 * D), D, c.b.hlp[0][0][nxt], D,
-                          c.b.wcat, D, c.b.bcat, c.b.up[0], c.b.ldup0, 0, c.s);
+        return tick_gemm();
     }
     if (k == 1 && c.b.fold_top) {
         // folded top tick: a (+ the period's noise) -> gi = a Min1^T + P1, gh1 carried ->
@@ -691,6 +710,10 @@ int run_block(Ctx& c, int periods) {
                 a.tk = c.b.ticks + 2 * fi + (ticks[0] & 1);    // that tick's G row, cur / nxt
                 c.gate_done = true;
             }
+            if (c.pending.N) {        // this bottom tick's GEMM, in the launch
+                a.tg = c.pending;
+                c.pending = GenMlpArgs::TickGemm{};
+            }
             RET(gen_mlp_launch(c.pl, a, c.s));
         }
     }
@@ -766,6 +789,7 @@ extern "C" int srnn_generate2(const SrnnModel* m, int n_seqs, int n_cond, const 
     c.ldseq = (int64_t)c.L * (n_cond + 1);
     c.logp = logp;
     c.pl = pl.ok ? &pl : nullptr;
+    c.tick_gemm = c.pl && pl.kernel_tg && c.b.fold;
     hipStream_t user = (hipStream_t)stream;
     const int D = m->dim, B = n_seqs;
     // private stream so a hipGraph can be captured regardless of the caller's stream

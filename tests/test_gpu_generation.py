@@ -245,3 +245,40 @@ def test_noise_ahead_matches_in_loop_draws(hip, monkeypatch, sampler):
         s0, l0 = generate(m, B, cond, spk, True, **kw)
         assert torch.equal(s1, s0)
         assert torch.equal(l1, l0)
+
+
+@pytest.mark.parametrize('B,n_cond', [(128, 6), (120, 2), (9, 4)])
+def test_tick_gemm_in_launch_bf16(hip, monkeypatch, B, n_cond):
+    """The bottom tick's [W_up; W_hh] GEMM inside the persistent launch (GenMlpArgs::tg: a
+    GEMM phase, write-through stores, one grid barrier, then the sample loop) against its own
+    launch (SRNN_GEN_TICK_GEMM=0): the same products in another fp32 summation order, so on
+    every step whose row prefix is still identical the log-probs agree within bf16 rounding
+    of the conditioning; n_cond = 6 replays the captured block twice (grid-barrier epochs
+    across replays); the sampler identity and the teacher-forced fp32 bound hold."""
+    cfg = recipe.CONFIGS['big']
+    m, pred = build(cfg, 19, torch.bfloat16)
+    L = m.lookback
+    cond = recipe.synth_cond((B, n_cond, cfg['cond_dim']), 21)
+    spk = np.arange(B) % cfg['spk_dim']
+    noise = torch.from_numpy(recipe.synth_noise((n_cond * L, B, 256), 22))
+    monkeypatch.setenv('SRNN_GEN_TICK_GEMM', '1')
+    s1, l1 = generate(m, B, cond, spk, True, noise=noise)
+    monkeypatch.setenv('SRNN_GEN_TICK_GEMM', '0')
+    s0, l0 = generate(m, B, cond, spk, True, noise=noise)
+    drawn = torch.argmax(torch.exp(l1) / noise.permute(1, 0, 2), dim=-1)
+    assert torch.equal(drawn, s1[:, L:])
+    same = torch.cumprod((s1[:, L:] == s0[:, L:]).int(), dim=1)
+    ok = torch.cat([torch.ones(B, 1, dtype=torch.int32), same[:, :-1]], dim=1).bool()
+    err = (l1 - l0).abs()[ok]
+    print('tick GEMM in launch vs own launch: %.3f of steps on identical prefixes, max %.4g '
+          'mean %.3g' % (ok.float().mean().item(), err.max().item(), err.mean().item()))
+    assert ok.float().mean().item() > 0.5
+    assert err.max().item() < 0.1, err.max().item()
+    assert err.mean().item() < 2e-3, err.mean().item()
+    m.compute_dtype = torch.float32
+    with torch.no_grad():
+        tf = pred(s1[:, :-1], True, torch.from_numpy(cond),
+                  torch.from_numpy(spk).reshape(-1, 1)).cpu()
+    err = (tf - l1).abs()
+    assert err.max().item() < 0.25, err.max().item()
+    assert err.mean().item() < 0.02, err.mean().item()
