@@ -375,11 +375,12 @@ def run_gen(dev, n_seqs, n_cond, dtype, frame_sizes=(16, 4), cond_dim=43, row0=0
     return time.perf_counter() - t0, w_step
 
 
-def gen_traffic():
-    """HBM bytes per generation step of the bf16 loop (B = 128, D = 1024, FS = [16, 4]) from the
-    committed rocprofv3 PMC passes (tools/pmc_gen.py: FETCH_SIZE kB x 2 + WRITE_SIZE kB over
-    every dispatch of the loop's kernels / samples generated), attributed to HEAD's kernels."""
-    return _pmc_file('r*_pmc_gen.txt')
+def gen_traffic(kind='gen'):
+    """HBM bytes per generation step of a generation line (kind gen / gen_fp32 / gen_e /
+    gen_e_fp32: B = 128, D = 1024) from the committed rocprofv3 PMC passes (tools/pmc_gen.sh:
+    FETCH_SIZE kB x 2 + WRITE_SIZE kB over every dispatch of the loop's kernels / samples
+    generated), attributed to HEAD's kernels."""
+    return _pmc_file('r*_pmc_%s.txt' % kind)
 
 
 def cpu_baseline(seconds_budget=30.0):
@@ -560,8 +561,10 @@ def main():
                              'frac': round(bytes_step * steps_per_s / 1e9 /
                                            (MI355X_HBM_TBS * 1000), 4),
                              'traffic': None, 'traffic_source': 'no PMC pass for this line'}}
-        if dname == 'bf16' and tuple(frame_sizes) == (16, 4) and args.gen_seqs == 128:
-            line['roofline']['traffic'], line['roofline']['traffic_source'] = gen_traffic()
+        if args.gen_seqs == 128:
+            kind = ('gen' if tuple(frame_sizes) == (16, 4) else 'gen_e') + \
+                ('' if dname == 'bf16' else '_fp32')
+            line['roofline']['traffic'], line['roofline']['traffic_source'] = gen_traffic(kind)
         return line
 
     gen = gen_fp32 = gen_e = gen_e_fp32 = None

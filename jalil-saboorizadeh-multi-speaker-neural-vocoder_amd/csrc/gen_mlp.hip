@@ -166,7 +166,7 @@ template <> __device__ __forceinline__ float gm_tap_load<float>(__amdgpu_buffer_
 
 // ---- in-launch tick GEMM (TG kernels) --------------------------------------------------
 // up0 = A W^T + bias for all B (<= 128) rows; workgroup w takes 16-column tiles
-// [w ntl / nblk, (w + 1) ntl / nblk) (<= 5 of them).  Both operands stream through a 2-slot
+// [w ntl / nblk, (w + 1) ntl / nblk) (<= TMAX of them).  Both operands stream through a 2-slot
 // LDS ring of 64-deep k chunks by global_load_lds (128-B rows, 16-B slots XOR-swizzled by
 // (row >> 1) & 7: conflict-free fragment reads), one chunk ahead; wave w owns output rows
 // [16 w, 16 w + 16).  The MFMA runs with the operands swapped, so a lane holds 4 consecutive
@@ -184,6 +184,7 @@ constexpr int LDS = 2 * SLOT;
 constexpr int PA = ASLOT / 1024 / gm::NW;      // DMA pieces per wave per chunk per operand (2)
 constexpr int PW = WSLOT / 1024 / gm::NW;
 constexpr int WORDS = 1280;             // grid-barrier words start at gerr + WORDS
+constexpr int TMAX = 6;                 // 16-column tiles per workgroup at most
 }  // namespace gmt
 
 #define GMT_LDS(p) ((__attribute__((address_space(3))) void*)(p))
@@ -390,7 +391,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
 #pragma unroll
             for (int i = 0; i < PW; ++i) {
                 const int r = 8 * (wave * PW + i) + (lane >> 3);           // weight row 0..127
-                const int tile = min(tb0 + r / 16, tb1 - 1);
+                const int tile = max(min(tb0 + r / 16, tb1 - 1), 0);
                 const int sl = (lane & 7) ^ ((r >> 1) & 7);
                 wsrc[i] = reinterpret_cast<const bf16*>(a.tg.W) +
                           (int64_t)(tile * 16 + (r & 15)) * DC + sl * 8;
@@ -407,9 +408,9 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                         GMT_GLB(wsrc[i] + ch * KC), GMT_LDS(slot + ASLOT + (wave * PW + i) * 1024),
                         16, 0, 0);
             };
-            floatx4 acc[5];
+            floatx4 acc[TMAX];
 #pragma unroll
-            for (int t = 0; t < 5; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
+            for (int t = 0; t < TMAX; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
             const unsigned lbase = (unsigned)(uintptr_t)GMT_LDS(stg);
             dma(0);
             __builtin_amdgcn_sched_barrier(0);
@@ -423,6 +424,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 __builtin_amdgcn_sched_barrier(0);
                 // chunk ch landed: younger ops are fragment groups ch - 1 and ch (4 each, chunks
                 // 0 .. 6) and chunk ch + 1's 4 DMA pieces
+                if (a.tg.dbg & 1) gmt_wait_vm<0>();
                 if (ch == 0) gmt_wait_vm<4 + 4>();
                 else if (ch < 7) gmt_wait_vm<4 + 4 + 4>();
                 else if (ch == 7) gmt_wait_vm<4 + 4>();
@@ -434,22 +436,30 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const int j = u * 4 + (lane >> 4);
-                    bf16x8 af, bfr[5];
+                    bf16x8 af, bfr[TMAX];
                     {
                         const int r = 16 * wave + (lane & 15);
                         const unsigned ad = sa + (unsigned)(r * ROWB + ((j ^ ((r >> 1) & 7)) * 16));
                         asm volatile("ds_read_b128 %0, %1" : "=v"(af) : "v"(ad) : "memory");
                     }
 #pragma unroll
-                    for (int t = 0; t < 5; ++t) {
+                    for (int t = 0; t < TMAX; ++t) {
                         const int r = t * 16 + (lane & 15);
                         const unsigned ad =
                             sa + (unsigned)(ASLOT + r * ROWB + ((j ^ ((r >> 1) & 7)) * 16));
                         asm volatile("ds_read_b128 %0, %1" : "=v"(bfr[t]) : "v"(ad) : "memory");
                     }
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                    // the wait names the fragments as operands: the MFMAs that read them cannot
+                    // be scheduled above it (the compiler does not know an asm LDS read is
+                    // asynchronous)
+                    static_assert(TMAX == 6, "TG: the wait below lists TMAX fragments");
+                    asm volatile("s_waitcnt lgkmcnt(0)"
+                                 : "+v"(af), "+v"(bfr[0]), "+v"(bfr[1]), "+v"(bfr[2]), "+v"(bfr[3]),
+                                   "+v"(bfr[4]), "+v"(bfr[5])
+                                 :
+                                 : "memory");
 #pragma unroll
-                    for (int t = 0; t < 5; ++t)
+                    for (int t = 0; t < TMAX; ++t)
                         acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[t], af, acc[t], 0, 0, 0);
                 }
                 __builtin_amdgcn_s_barrier();      // slot (ch & 1) is chunk ch + 2's
@@ -460,13 +470,13 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             const __amdgpu_buffer_rsrc_t rcw =
                 __builtin_amdgcn_make_buffer_rsrc(a.tg.C, (short)0, 0x7fffffff, 0x00020000);
             typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
-            floatx4 bq[5];
+            floatx4 bq[TMAX];
 #pragma unroll
-            for (int t = 0; t < 5; ++t)
+            for (int t = 0; t < TMAX; ++t)
                 bq[t] = *reinterpret_cast<const floatx4*>(
-                    a.tg.bias + min(tb0 + t, tb1 - 1) * 16 + (lane >> 4) * 4);
+                    a.tg.bias + max(min(tb0 + t, tb1 - 1), 0) * 16 + (lane >> 4) * 4);
 #pragma unroll
-            for (int t = 0; t < 5; ++t) {
+            for (int t = 0; t < TMAX; ++t) {
                 if (t < tb1 - tb0 && m < a.B) {
                     const int n = (tb0 + t) * 16 + (lane >> 4) * 4;
                     __builtin_amdgcn_raw_buffer_store_b128(
@@ -477,6 +487,11 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             // every workgroup's part of up0 is out before any sample loop reads it
             const int epoch = (*a.base + a.off - a.L) / FS0 + 1;
             gmt_grid_barrier(a.tg.bar, nblk, epoch, a.err);
+            if (a.tg.dbg & 2) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
         } else {
 #pragma unroll
             for (int i = 0; i < NLD; ++i) ld(i);
@@ -565,8 +580,10 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         const float* gr = a.tk->G + (int64_t)tb * a.tk->ldg;
         const float* hr = a.tk->gh + (int64_t)tb * a.tk->ldgh;
         tg[0] = gr[tu]; tg[1] = gr[D + tu]; tg[2] = gr[2 * D + tu];
-        if constexpr (TG) {     // gh: this launch's GEMM output (sc1 loads, as up0)
-            float* hw = const_cast<float*>(hr);
+        if constexpr (TG) {     // gh: this launch's GEMM output (global sc1 loads, as up0;
+                                // the pointer comes from memory, so force the global form)
+            typedef __attribute__((address_space(1))) float gf;
+            gf* hw = (gf*)const_cast<float*>(hr);
             tg[3] = __hip_atomic_load(hw + tu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             tg[4] = __hip_atomic_load(hw + D + tu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             tg[5] = __hip_atomic_load(hw + 2 * D + tu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1080,6 +1097,12 @@ extern "C" int srnn_gen_diag_dump(void) {
     return 0;
 }
 
+int gen_mlp_tick_gemm_ok(const GenMlpPlan* pl, int N, int K, int B) {
+    const int nblk = pl->G * pl->P;
+    return pl->ok && pl->kernel_tg && K == 1024 && N % 16 == 0 && N / 16 >= nblk &&
+           cdiv(N / 16, nblk) <= gmt::TMAX && B <= 128 && nblk <= 2048 - gmt::WORDS;
+}
+
 int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
     SRNN_REQUIRE(pl && pl->ok, "gen_mlp: no plan");
     a.R = pl->R;
@@ -1108,15 +1131,14 @@ int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
     }
     const bool tg = a.tg.N > 0;
     if (tg) {
-        const int nblk = pl->G * pl->P;
         SRNN_REQUIRE(pl->kernel_tg && a.wfr_hid && a.wfr_out,
                      "gen_mlp: no in-launch tick GEMM for this shape");
-        SRNN_REQUIRE(a.tg.K == 1024 && a.tg.N % 16 == 0 && cdiv(a.tg.N / 16, nblk) <= 5 &&
-                         a.B <= 128 && a.tg.ldc % 4 == 0 && a.tg.A && a.tg.W && a.tg.bias &&
-                         a.tg.C && nblk <= 2048 - gmt::WORDS,
+        SRNN_REQUIRE(gen_mlp_tick_gemm_ok(pl, a.tg.N, a.tg.K, a.B) && a.tg.ldc % 4 == 0 &&
+                         a.tg.A && a.tg.W && a.tg.bias && a.tg.C,
                      "gen_mlp: tick GEMM shape (N %d, K %d, B %d) not supported", a.tg.N, a.tg.K,
                      a.B);
         a.tg.bar = a.err + gmt::WORDS;
+        a.tg.dbg = env_flag("SRNN_GEN_TG_DBG", 0);
     }
     const GmKernel k = (GmKernel)(tg ? pl->kernel_tg : pl->kernel);
     const size_t lds = tg ? pl->lds_tg : pl->lds;

@@ -789,7 +789,8 @@ extern "C" int srnn_generate2(const SrnnModel* m, int n_seqs, int n_cond, const 
     c.ldseq = (int64_t)c.L * (n_cond + 1);
     c.logp = logp;
     c.pl = pl.ok ? &pl : nullptr;
-    c.tick_gemm = c.pl && pl.kernel_tg && c.b.fold;
+    c.tick_gemm = c.pl && c.b.fold &&
+                  gen_mlp_tick_gemm_ok(&pl, (m->tier[0].frame_size + 3) * m->dim, m->dim, n_seqs);
     hipStream_t user = (hipStream_t)stream;
     const int D = m->dim, B = n_seqs;
     // private stream so a hipGraph can be captured regardless of the caller's stream

@@ -30,6 +30,24 @@ def build(cfg, seed, dtype):
     return m.to(DEV), pred.to(DEV)
 
 
+def check_draws(lp, noise, seq, L):
+    """The sampler definition, exactly: x_t = argmax(exp(logp_t) / q_t) (first index on ties)
+    of the log-probs the loop reports -- with a diagnostic of any mismatch (its step, row and
+    the log-space margin between the two candidates)."""
+    drawn = torch.argmax(torch.exp(lp) / noise.permute(1, 0, 2), dim=-1)
+    got = seq[:, L:]
+    bad = (drawn != got).nonzero()
+    if bad.numel():
+        sc = lp.double() - torch.log(noise.permute(1, 0, 2).double())
+        info = []
+        for b, t in bad[:8].tolist():
+            info.append('row %d step %d (mod 16: %d): drawn %d score %.7g, loop %d score %.7g'
+                        % (b, t, t % 16, drawn[b, t].item(), sc[b, t, drawn[b, t]].item(),
+                           got[b, t].item(), sc[b, t, got[b, t]].item()))
+        raise AssertionError('%d of %d draws differ: %s' % (bad.shape[0], got.numel(),
+                                                             '; '.join(info)))
+
+
 def generate(m, n_seqs, cond, spk, persistent, **kw):
     import model as M
     gen = M.Generator(m, True)
@@ -53,8 +71,9 @@ def test_persistent_matches_per_sample_fp32(hip, D, B, n_cond, n_rnn):
     torch.testing.assert_close(l1, l0, atol=1e-4, rtol=0)
 
 
-@pytest.mark.parametrize('B', [128, 120, 9])
-def test_persistent_bf16_d1024(hip, B):
+@pytest.mark.parametrize('B,tg', [(128, '1'), (128, '0'), (120, '1'), (9, '1')])
+def test_persistent_bf16_d1024(hip, monkeypatch, B, tg):
+    monkeypatch.setenv('SRNN_GEN_TICK_GEMM', tg)
     cfg = recipe.CONFIGS['big']
     m, pred = build(cfg, 11, torch.bfloat16)
     assert hip.gen_persistent_rows(torch.bfloat16, B, 1024, 16) > 0
@@ -64,9 +83,7 @@ def test_persistent_bf16_d1024(hip, B):
     noise = torch.from_numpy(recipe.synth_noise((n_cond * 64, B, 256), 3))
     seq, lp = generate(m, B, cond, spk, True, noise=noise)
     L = m.lookback
-    # sampler definition, exactly: x_t = argmax(exp(logp_t) / q_t) (first index on ties)
-    drawn = torch.argmax(torch.exp(lp) / noise.permute(1, 0, 2), dim=-1)
-    assert torch.equal(drawn, seq[:, L:])
+    check_draws(lp, noise, seq, L)
     # teacher-forced fp32 Predictor on the generated stream: bf16 tolerance on log-probs
     m.compute_dtype = torch.float32
     with torch.no_grad():
@@ -132,8 +149,7 @@ def test_config_e_bf16_d1024(hip):
     assert L == 256
     noise = torch.from_numpy(recipe.synth_noise((n_cond * L, B, 256), 4))
     seq, lp = generate(m, B, cond, spk, True, noise=noise)
-    drawn = torch.argmax(torch.exp(lp) / noise.permute(1, 0, 2), dim=-1)
-    assert torch.equal(drawn, seq[:, L:])
+    check_draws(lp, noise, seq, L)
     m.compute_dtype = torch.float32
     with torch.no_grad():
         tf = pred(seq[:, :-1], True, torch.from_numpy(cond),
@@ -265,8 +281,7 @@ def test_tick_gemm_in_launch_bf16(hip, monkeypatch, B, n_cond):
     s1, l1 = generate(m, B, cond, spk, True, noise=noise)
     monkeypatch.setenv('SRNN_GEN_TICK_GEMM', '0')
     s0, l0 = generate(m, B, cond, spk, True, noise=noise)
-    drawn = torch.argmax(torch.exp(l1) / noise.permute(1, 0, 2), dim=-1)
-    assert torch.equal(drawn, s1[:, L:])
+    check_draws(l1, noise, s1, L)
     same = torch.cumprod((s1[:, L:] == s0[:, L:]).int(), dim=1)
     ok = torch.cat([torch.ones(B, 1, dtype=torch.int32), same[:, :-1]], dim=1).bool()
     err = (l1 - l0).abs()[ok]

@@ -39,14 +39,14 @@ def per_kernel(db, ctr):
     return agg
 
 
-def main(fdb, wdb):
+def main(fdb, wdb, what='gen: tools/gen_prof.py bf16 20'):
     f = per_kernel(fdb, 'FETCH_SIZE')
     w = per_kernel(wdb, 'WRITE_SIZE')
     launches = sum(n for k, (n, _) in f.items() if 'gen_mlp_kernel' in k)
     steps = 16 * launches
     tot = 0.0
-    print('# HBM traffic of the generation loop (bf16, B = 128, D = 1024, FS = [16, 4]), '
-          'tools/gen_prof.py bf16 20 under rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE')
+    print('# HBM traffic of the generation loop (B = 128, D = 1024), %s under rocprofv3 '
+          '--pmc FETCH_SIZE / WRITE_SIZE' % what)
     print('# kernel  dispatches  FETCH kB x2  WRITE kB  (totals over the run)')
     for k in sorted(set(f) | set(w)):
         nf, sf = f.get(k, (0, 0.0))
@@ -59,4 +59,4 @@ def main(fdb, wdb):
 
 
 if __name__ == '__main__':
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])
