@@ -180,7 +180,8 @@ constexpr int AROWS = 128;              // A rows staged (B <= 128; clamped)
 constexpr int WROWS = 128;              // weight rows staged (<= 5 real tiles, clamped)
 constexpr int ASLOT = AROWS * ROWB, WSLOT = WROWS * ROWB;   // 16 KiB each
 constexpr int SLOT = ASLOT + WSLOT;
-constexpr int LDS = 2 * SLOT;
+constexpr int NSL = 3;                  // ring slots: chunks ch + 1 and ch + 2 in flight
+constexpr int LDS = NSL * SLOT;
 constexpr int PA = ASLOT / 1024 / gm::NW;      // DMA pieces per wave per chunk per operand (2)
 constexpr int PW = WSLOT / 1024 / gm::NW;
 constexpr int WORDS = 1280;             // grid-barrier words start at gerr + WORDS
@@ -193,6 +194,18 @@ constexpr int TMAX = 6;                 // 16-column tiles per workgroup at most
 template <int N>
 __device__ __forceinline__ void gmt_wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+// vmcnt(n) for a count known after unrolling (multiples of 4 up to 24)
+__device__ __forceinline__ void gmt_wait_n(int n) {
+    switch (n) {
+        case 0: gmt_wait_vm<0>(); break;
+        case 4: gmt_wait_vm<4>(); break;
+        case 8: gmt_wait_vm<8>(); break;
+        case 12: gmt_wait_vm<12>(); break;
+        case 16: gmt_wait_vm<16>(); break;
+        case 20: gmt_wait_vm<20>(); break;
+        default: gmt_wait_vm<0>(); break;
+    }
 }
 
 // Grid barrier of the TG kernels (MI355X guide, valid form R1): every storing thread drains
@@ -397,7 +410,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                           (int64_t)(tile * 16 + (r & 15)) * DC + sl * 8;
             }
             auto dma = [&](int ch) {
-                char* slot = stg + (ch & 1) * SLOT;
+                char* slot = stg + (ch % NSL) * SLOT;
 #pragma unroll
                 for (int i = 0; i < PA; ++i)
                     __builtin_amdgcn_global_load_lds(GMT_GLB(asrc[i] + ch * KC),
@@ -412,27 +425,30 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
 #pragma unroll
             for (int t = 0; t < TMAX; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
             const unsigned lbase = (unsigned)(uintptr_t)GMT_LDS(stg);
+            // issue order: DMA(0), DMA(1); iteration ch: DMA(ch + 2), fragment group ch
+            // (4 loads, ch < 7); DMA pieces are 4 per wave per chunk
             dma(0);
+            dma(1);
             __builtin_amdgcn_sched_barrier(0);
+            auto fcnt = [](int k) { return k >= 0 && k < 7 ? 4 : 0; };
+            auto dcnt = [](int k) { return k < NCH ? 4 : 0; };
 #pragma unroll
             for (int ch = 0; ch < NCH; ++ch) {
-                if (ch + 1 < NCH) dma(ch + 1);
+                if (ch + 2 < NCH) dma(ch + 2);
                 if (ch < 7) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) ld(ch * 4 + i);
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                // chunk ch landed: younger ops are fragment groups ch - 1 and ch (4 each, chunks
-                // 0 .. 6) and chunk ch + 1's 4 DMA pieces
-                if (a.tg.dbg & 1) gmt_wait_vm<0>();
-                if (ch == 0) gmt_wait_vm<4 + 4>();
-                else if (ch < 7) gmt_wait_vm<4 + 4 + 4>();
-                else if (ch == 7) gmt_wait_vm<4 + 4>();
-                else if (ch + 1 < NCH) gmt_wait_vm<4>();
-                else gmt_wait_vm<0>();
+                // chunk ch landed: count the ops issued after its DMA
+                const int younger = ch == 0 ? dcnt(1) + dcnt(2) + fcnt(0)
+                                  : ch == 1 ? dcnt(2) + fcnt(0) + dcnt(3) + fcnt(1)
+                                  : fcnt(ch - 2) + dcnt(ch + 1) + fcnt(ch - 1) + dcnt(ch + 2) +
+                                        fcnt(ch);
+                gmt_wait_n(younger);
                 // (raw barrier: __syncthreads would also drain vmcnt -- the fragment loads)
                 __builtin_amdgcn_s_barrier();
-                const unsigned sa = lbase + (unsigned)((ch & 1) * SLOT);
+                const unsigned sa = lbase + (unsigned)((ch % NSL) * SLOT);
 #pragma unroll
                 for (int u = 0; u < 2; ++u) {
                     const int j = u * 4 + (lane >> 4);
@@ -462,7 +478,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                     for (int t = 0; t < TMAX; ++t)
                         acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[t], af, acc[t], 0, 0, 0);
                 }
-                __builtin_amdgcn_s_barrier();      // slot (ch & 1) is chunk ch + 2's
+                __builtin_amdgcn_s_barrier();      // slot ch % NSL is chunk ch + 3's
                 __builtin_amdgcn_sched_barrier(0);
             }
             // epilogue: lane holds C[m][n .. n + 3] of each tile; 16-B write-through stores
@@ -487,11 +503,6 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             // every workgroup's part of up0 is out before any sample loop reads it
             const int epoch = (*a.base + a.off - a.L) / FS0 + 1;
             gmt_grid_barrier(a.tg.bar, nblk, epoch, a.err);
-            if (a.tg.dbg & 2) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __syncthreads();
-            }
         } else {
 #pragma unroll
             for (int i = 0; i < NLD; ++i) ld(i);
@@ -1138,7 +1149,6 @@ int gen_mlp_launch(const GenMlpPlan* pl, GenMlpArgs a, hipStream_t s) {
                      "gen_mlp: tick GEMM shape (N %d, K %d, B %d) not supported", a.tg.N, a.tg.K,
                      a.B);
         a.tg.bar = a.err + gmt::WORDS;
-        a.tg.dbg = env_flag("SRNN_GEN_TG_DBG", 0);
     }
     const GmKernel k = (GmKernel)(tg ? pl->kernel_tg : pl->kernel);
     const size_t lds = tg ? pl->lds_tg : pl->lds;
