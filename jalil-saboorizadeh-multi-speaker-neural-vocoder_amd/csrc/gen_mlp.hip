@@ -481,6 +481,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 __builtin_amdgcn_s_barrier();      // slot ch % NSL is chunk ch + 3's
                 __builtin_amdgcn_sched_barrier(0);
             }
+            GM_STAMP();                            // GEMM main loop done
             // epilogue: lane holds C[m][n .. n + 3] of each tile; 16-B write-through stores
             const int m = 16 * wave + (lane & 15);
             const __amdgpu_buffer_rsrc_t rcw =
@@ -502,7 +503,9 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             }
             // every workgroup's part of up0 is out before any sample loop reads it
             const int epoch = (*a.base + a.off - a.L) / FS0 + 1;
+            GM_STAMP();                            // epilogue stores issued
             gmt_grid_barrier(a.tg.bar, nblk, epoch, a.err);
+            GM_STAMP();                            // grid barrier passed
         } else {
 #pragma unroll
             for (int i = 0; i < NLD; ++i) ld(i);
