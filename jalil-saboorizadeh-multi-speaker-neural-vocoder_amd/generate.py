@@ -184,7 +184,7 @@ def main(frame_sizes, **params):
             prow = np.concatenate([rows, np.zeros((pad,) + rows.shape[1:], rows.dtype)])
             pspk = np.concatenate([spks, np.zeros(pad, spks.dtype)])
             out = shard_generate(gen, len(prow), prow, pspk, params['seed'],
-                                 sampler=params['sampler'],
+                                 sampler=params['sampler'], noise_rows=len(rows),
                                  seq_len=params['sample_length']).numpy()[:len(rows)]
         else:
             out = gen(len(rows), params['sample_length'], rows, spks, sampler=params['sampler'],

@@ -1012,7 +1012,7 @@ class Generator(Runner):
 
 
 def shard_generate(generator, n_seqs, cond, spk, seed, rank=None, world=None, sampler='philox',
-                   seq_len=0, **kw):
+                   seq_len=0, noise_rows=None, **kw):
     """Rank-sharded generation (the reference runs generate.py:241-253 per file on
     one device): rank r generates the contiguous rows [r n / N, (r + 1) n / N) of an n_seqs batch
     with replicated weights and no collective in the loop; the dequantized rows are gathered to
@@ -1021,7 +1021,10 @@ def shard_generate(generator, n_seqs, cond, spk, seed, rank=None, world=None, sa
       * 'torch' (the reference's multinomial stream, model.py:514-517): every rank draws the
         whole batch's Exp(1) noise from torch's CPU generator exactly as a single process
         would (one (T, n_seqs, Q) draw, so every rank must have been seeded alike) and keeps
-        its rows' slice -- host memory T * n_seqs * Q * 4 bytes per rank.
+        its rows' slice -- host memory T * n_seqs * Q * 4 bytes per rank.  noise_rows: the
+        caller's true row count when n_seqs includes padding rows (to a multiple of the world
+        size): the draw is then (T, noise_rows, Q), as the unpadded single-process run makes
+        it, and the padding rows get unit noise (their output is discarded).
     cond: (num_cond, C) shared or (n_seqs, num_cond, C) per row; spk: int or (n_seqs,).
     seq_len is accepted like Generator's (the reference ignores it, model.py:455).
     Returns the host float32 (n_seqs, num_cond * lookback) batch."""
@@ -1040,7 +1043,13 @@ def shard_generate(generator, n_seqs, cond, spk, seed, rank=None, world=None, sa
         s = s[rows]
     if sampler == 'torch' and kw.get('noise') is None:
         model = generator.model
-        full = torch.empty(num_cond * model.lookback, n_seqs, model.q_levels).exponential_(1)
+        nr = n_seqs if noise_rows is None else int(noise_rows)
+        if not 0 < nr <= n_seqs:
+            raise ValueError('shard_generate: noise_rows %d outside (0, %d]' % (nr, n_seqs))
+        full = torch.empty(num_cond * model.lookback, nr, model.q_levels).exponential_(1)
+        if nr < n_seqs:
+            full = torch.cat([full, full.new_ones((full.shape[0], n_seqs - nr, full.shape[2]))],
+                             1)
         kw['noise'] = full[:, rows].contiguous()
         del full
     out = generator(rows.stop - rows.start, seq_len, c, s, sampler=sampler, seed=seed,

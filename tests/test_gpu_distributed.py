@@ -299,11 +299,12 @@ def test_dp_bf16_buckets_track_reference(hip):
         np.testing.assert_array_equal(got[0][1][k], got[1][1][k], err_msg=k)
 
 
-def _gen_worker(rank, world, port, name, dtype, sampler, q):
+def _gen_worker(rank, world, port, name, dtype, sampler, n, q):
     """Rank-sharded generation (model.shard_generate): each rank generates its contiguous
     rows with the noise of the global rows (Philox, or the reference's torch CPU stream
     drawn for the whole batch on every rank); the gathered batch equals the single-process
-    run's bit for bit."""
+    run's bit for bit.  n not divisible by the world size: the rows are padded as
+    generate.py pads them, and the noise is drawn for the true n (noise_rows)."""
     try:
         sys.path[:0] = [HERE, os.path.join(HERE, 'golden'),
                         os.path.join(os.path.dirname(HERE),
@@ -320,11 +321,15 @@ def _gen_worker(rank, world, port, name, dtype, sampler, q):
         cfg = recipe.CONFIGS[name]
         m, _ = build(cfg, recipe.make_weights(cfg, 51),
                      torch.bfloat16 if dtype == 'bf16' else torch.float32)
-        n, n_cond = 16, 2
+        n_cond = 2
         cond = recipe.synth_cond((n, n_cond, cfg['cond_dim']), 6)
         spk = np.arange(n) % cfg['spk_dim']
+        pad = (-n) % world
+        pcond = np.concatenate([cond, np.zeros((pad,) + cond.shape[1:], cond.dtype)])
+        pspk = np.concatenate([spk, np.zeros(pad, spk.dtype)])
         torch.manual_seed(7)
-        out = M.shard_generate(M.Generator(m, True), n, cond, spk, 99, sampler=sampler)
+        out = M.shard_generate(M.Generator(m, True), n + pad, pcond, pspk, 99, sampler=sampler,
+                               noise_rows=n)[:n]
         full = None
         if rank == 0:
             torch.manual_seed(7)
@@ -340,10 +345,14 @@ def _gen_worker(rank, world, port, name, dtype, sampler, q):
         raise
 
 
-@pytest.mark.parametrize('name,dtype,sampler', [('t3', 'fp32', 'philox'), ('big', 'bf16', 'philox'),
-                                                ('t3', 'fp32', 'torch'), ('big', 'fp32', 'torch')])
-def test_sharded_generation_reproduces_single_process(hip, name, dtype, sampler):
-    got = _spawn(_gen_worker, (name, dtype, sampler))
+@pytest.mark.parametrize('name,dtype,sampler,n', [('t3', 'fp32', 'philox', 16),
+                                                  ('big', 'bf16', 'philox', 16),
+                                                  ('t3', 'fp32', 'torch', 16),
+                                                  ('big', 'fp32', 'torch', 16),
+                                                  ('t3', 'fp32', 'torch', 15),
+                                                  ('t3', 'fp32', 'philox', 15)])
+def test_sharded_generation_reproduces_single_process(hip, name, dtype, sampler, n):
+    got = _spawn(_gen_worker, (name, dtype, sampler, n))
     full = got[0][1]
     for rank in (0, 1):
         assert np.array_equal(got[rank][0], full), rank
