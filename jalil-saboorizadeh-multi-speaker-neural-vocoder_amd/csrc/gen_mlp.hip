@@ -166,26 +166,25 @@ template <> __device__ __forceinline__ float gm_tap_load<float>(__amdgpu_buffer_
 
 // ---- in-launch tick GEMM (TG kernels) --------------------------------------------------
 // up0 = A W^T + bias for all B (<= 128) rows; workgroup w takes 16-column tiles
-// [w ntl / nblk, (w + 1) ntl / nblk) (<= TMAX of them).  Both operands stream through a 2-slot
+// [w ntl / nblk, (w + 1) ntl / nblk) (<= TMAX of them).  Both operands stream through a 4-slot
 // LDS ring of 64-deep k chunks by global_load_lds (128-B rows, 16-B slots XOR-swizzled by
-// (row >> 1) & 7: conflict-free fragment reads), one chunk ahead; wave w owns output rows
-// [16 w, 16 w + 16).  The MFMA runs with the operands swapped, so a lane holds 4 consecutive
+// (row >> 1) & 7: conflict-free fragment reads), three chunks in flight, only the weight rows
+// of the workgroup's own tiles staged; wave w owns output rows [16 w, 16 w + 16).  The MFMA runs with the operands swapped, so a lane holds 4 consecutive
 // columns of one row: the epilogue is one 16-B write-through (sc1) store per tile.  The
 // fragment reads are inline asm and every wait is counted by hand: the resident-fragment
 // loads of the prologue are issued between the chunks and must stay in flight across them.
 namespace gmt {
 constexpr int KC = 64;                  // k per chunk
 constexpr int ROWB = KC * 2;            // 128 B per staged row (8 x 16-B slots)
+constexpr int TMAX = 5;                 // 16-column tiles per workgroup at most
 constexpr int AROWS = 128;              // A rows staged (B <= 128; clamped)
-constexpr int WROWS = 128;              // weight rows staged (<= 5 real tiles, clamped)
-constexpr int ASLOT = AROWS * ROWB, WSLOT = WROWS * ROWB;   // 16 KiB each
+constexpr int WROWS = 16 * TMAX;        // weight rows staged (the workgroup's tiles only)
+constexpr int ASLOT = AROWS * ROWB, WSLOT = WROWS * ROWB;   // 16 / 10 KiB
 constexpr int SLOT = ASLOT + WSLOT;
-constexpr int NSL = 3;                  // ring slots: chunks ch + 1 and ch + 2 in flight
+constexpr int NSL = 4;                  // ring slots: chunks ch + 1 .. ch + 3 in flight
 constexpr int LDS = NSL * SLOT;
-constexpr int PA = ASLOT / 1024 / gm::NW;      // DMA pieces per wave per chunk per operand (2)
-constexpr int PW = WSLOT / 1024 / gm::NW;
+constexpr int PA = ASLOT / 1024 / gm::NW;      // A DMA pieces per wave per chunk (2)
 constexpr int WORDS = 1280;             // grid-barrier words start at gerr + WORDS
-constexpr int TMAX = 6;                 // 16-column tiles per workgroup at most
 }  // namespace gmt
 
 #define GMT_LDS(p) ((__attribute__((address_space(3))) void*)(p))
@@ -195,17 +194,17 @@ template <int N>
 __device__ __forceinline__ void gmt_wait_vm() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
-// vmcnt(n) for a count known after unrolling (multiples of 4 up to 24)
+// vmcnt(n) for a wave-uniform count (0 .. 31; anything else waits for everything)
 __device__ __forceinline__ void gmt_wait_n(int n) {
+#define GMT_W(k) case k: gmt_wait_vm<k>(); break;
     switch (n) {
-        case 0: gmt_wait_vm<0>(); break;
-        case 4: gmt_wait_vm<4>(); break;
-        case 8: gmt_wait_vm<8>(); break;
-        case 12: gmt_wait_vm<12>(); break;
-        case 16: gmt_wait_vm<16>(); break;
-        case 20: gmt_wait_vm<20>(); break;
+        GMT_W(1) GMT_W(2) GMT_W(3) GMT_W(4) GMT_W(5) GMT_W(6) GMT_W(7) GMT_W(8) GMT_W(9)
+        GMT_W(10) GMT_W(11) GMT_W(12) GMT_W(13) GMT_W(14) GMT_W(15) GMT_W(16) GMT_W(17)
+        GMT_W(18) GMT_W(19) GMT_W(20) GMT_W(21) GMT_W(22) GMT_W(23) GMT_W(24) GMT_W(25)
+        GMT_W(26) GMT_W(27) GMT_W(28) GMT_W(29) GMT_W(30) GMT_W(31)
         default: gmt_wait_vm<0>(); break;
     }
+#undef GMT_W
 }
 
 // Grid barrier of the TG kernels (MI355X guide, valid form R1): every storing thread drains
@@ -381,7 +380,7 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
         };
         if constexpr (TG) {
             // ---- the bottom tick's GEMM (GenMlpArgs::tg), the fragment loads interleaved:
-            // group c (4 loads, chunks 0 .. 6) is issued after chunk c + 1's DMA, so it is
+            // group c (4 loads, chunks 0 .. 6) is issued after chunk c + 3's DMA, so it is
             // younger than the chunk waited for next and lands while the GEMM runs (vmcnt is
             // in order)
             using namespace gmt;
@@ -391,9 +390,15 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             const int ntl = a.tg.N / 16;
             const int tb0 = (int)((int64_t)blockIdx.x * ntl / nblk);
             const int tb1 = (int)((int64_t)(blockIdx.x + 1) * ntl / nblk);
+            const int nt = tb1 - tb0;                   // 1 .. TMAX (gen_mlp_tick_gemm_ok)
+            // the tiles' bias, loaded before the ring (older than every chunk: no wait of its own)
+            floatx4 bq[TMAX];
+#pragma unroll
+            for (int t = 0; t < TMAX; ++t)
+                bq[t] = *reinterpret_cast<const floatx4*>(
+                    a.tg.bias + max(min(tb0 + t, tb1 - 1), 0) * 16 + (lane >> 4) * 4);
             char* stg = reinterpret_cast<char*>(gsh) + 16;
             const bf16* asrc[PA];
-            const bf16* wsrc[PW];
 #pragma unroll
             for (int i = 0; i < PA; ++i) {
                 const int r = 8 * (wave * PA + i) + (lane >> 3);           // A row 0..127
@@ -401,9 +406,14 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 asrc[i] = reinterpret_cast<const bf16*>(a.tg.A) + (int64_t)min(r, a.B - 1) * DC +
                           sl * 8;
             }
+            // weight rows 0 .. 16 nt - 1 in 1-KiB pieces of 8 rows: piece wave + 8 i (i = 0, 1)
+            // when it is one of the 2 nt (a wave-uniform count dW of 0 .. 2 per chunk)
+            const int npw = 2 * nt;
+            const int dW = (wave < npw ? 1 : 0) + (wave + gm::NW < npw ? 1 : 0);
+            const bf16* wsrc[2];
 #pragma unroll
-            for (int i = 0; i < PW; ++i) {
-                const int r = 8 * (wave * PW + i) + (lane >> 3);           // weight row 0..127
+            for (int i = 0; i < 2; ++i) {
+                const int r = 8 * (wave + gm::NW * i) + (lane >> 3);     // weight row 0..79
                 const int tile = max(min(tb0 + r / 16, tb1 - 1), 0);
                 const int sl = (lane & 7) ^ ((r >> 1) & 7);
                 wsrc[i] = reinterpret_cast<const bf16*>(a.tg.W) +
@@ -415,37 +425,49 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 for (int i = 0; i < PA; ++i)
                     __builtin_amdgcn_global_load_lds(GMT_GLB(asrc[i] + ch * KC),
                                                      GMT_LDS(slot + (wave * PA + i) * 1024), 16, 0, 0);
-#pragma unroll
-                for (int i = 0; i < PW; ++i)
+                if (wave < npw)
+                    __builtin_amdgcn_global_load_lds(GMT_GLB(wsrc[0] + ch * KC),
+                                                     GMT_LDS(slot + ASLOT + wave * 1024), 16, 0, 0);
+                if (wave + gm::NW < npw)
                     __builtin_amdgcn_global_load_lds(
-                        GMT_GLB(wsrc[i] + ch * KC), GMT_LDS(slot + ASLOT + (wave * PW + i) * 1024),
-                        16, 0, 0);
+                        GMT_GLB(wsrc[1] + ch * KC),
+                        GMT_LDS(slot + ASLOT + (wave + gm::NW) * 1024), 16, 0, 0);
             };
             floatx4 acc[TMAX];
 #pragma unroll
             for (int t = 0; t < TMAX; ++t) acc[t] = floatx4{0.f, 0.f, 0.f, 0.f};
             const unsigned lbase = (unsigned)(uintptr_t)GMT_LDS(stg);
-            // issue order: DMA(0), DMA(1); iteration ch: DMA(ch + 2), fragment group ch
-            // (4 loads, ch < 7); DMA pieces are 4 per wave per chunk
-            dma(0);
-            dma(1);
+            // issue order: DMA(0 .. NSL - 2); iteration ch: DMA(ch + NSL - 1), fragment group
+            // ch (4 loads, ch < 7); a DMA is PA + dW loads of this wave
+            constexpr int AH = NSL - 1;                 // chunks in flight
+#pragma unroll
+            for (int c = 0; c < AH; ++c) dma(c);
             __builtin_amdgcn_sched_barrier(0);
-            auto fcnt = [](int k) { return k >= 0 && k < 7 ? 4 : 0; };
-            auto dcnt = [](int k) { return k < NCH ? 4 : 0; };
 #pragma unroll
             for (int ch = 0; ch < NCH; ++ch) {
-                if (ch + 2 < NCH) dma(ch + 2);
+                if (ch + AH < NCH) dma(ch + AH);
                 if (ch < 7) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) ld(ch * 4 + i);
                 }
                 __builtin_amdgcn_sched_barrier(0);
-                // chunk ch landed: count the ops issued after its DMA
-                const int younger = ch == 0 ? dcnt(1) + dcnt(2) + fcnt(0)
-                                  : ch == 1 ? dcnt(2) + fcnt(0) + dcnt(3) + fcnt(1)
-                                  : fcnt(ch - 2) + dcnt(ch + 1) + fcnt(ch - 1) + dcnt(ch + 2) +
-                                        fcnt(ch);
-                gmt_wait_n(younger);
+                // chunk ch landed: count the loads issued after its DMA (compile-time counts of
+                // DMAs nd and fragment groups nf after it)
+                int nd = 0, nf = 0;
+                if (ch < AH) {
+                    nd = AH - 1 - ch;                   // the prologue's later DMAs
+                    for (int i = 0; i <= ch; ++i) {
+                        nd += i + AH < NCH ? 1 : 0;
+                        nf += i < 7 ? 1 : 0;
+                    }
+                } else {
+                    nf = ch - AH < 7 ? 1 : 0;           // its own iteration's fragment group
+                    for (int i = ch - AH + 1; i <= ch; ++i) {
+                        nd += i + AH < NCH ? 1 : 0;
+                        nf += i < 7 ? 1 : 0;
+                    }
+                }
+                gmt_wait_n(nd * (PA + dW) + nf * 4);
                 // (raw barrier: __syncthreads would also drain vmcnt -- the fragment loads)
                 __builtin_amdgcn_s_barrier();
                 const unsigned sa = lbase + (unsigned)((ch % NSL) * SLOT);
@@ -468,17 +490,17 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                     // the wait names the fragments as operands: the MFMAs that read them cannot
                     // be scheduled above it (the compiler does not know an asm LDS read is
                     // asynchronous)
-                    static_assert(TMAX == 6, "TG: the wait below lists TMAX fragments");
+                    static_assert(TMAX == 5, "TG: the wait below lists TMAX fragments");
                     asm volatile("s_waitcnt lgkmcnt(0)"
                                  : "+v"(af), "+v"(bfr[0]), "+v"(bfr[1]), "+v"(bfr[2]), "+v"(bfr[3]),
-                                   "+v"(bfr[4]), "+v"(bfr[5])
+                                   "+v"(bfr[4])
                                  :
                                  : "memory");
 #pragma unroll
                     for (int t = 0; t < TMAX; ++t)
                         acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[t], af, acc[t], 0, 0, 0);
                 }
-                __builtin_amdgcn_s_barrier();      // slot ch % NSL is chunk ch + 3's
+                __builtin_amdgcn_s_barrier();      // slot ch % NSL is chunk ch + NSL's
                 __builtin_amdgcn_sched_barrier(0);
             }
             GM_STAMP();                            // GEMM main loop done
@@ -487,11 +509,6 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             const __amdgpu_buffer_rsrc_t rcw =
                 __builtin_amdgcn_make_buffer_rsrc(a.tg.C, (short)0, 0x7fffffff, 0x00020000);
             typedef unsigned int u32x4_ __attribute__((ext_vector_type(4)));
-            floatx4 bq[TMAX];
-#pragma unroll
-            for (int t = 0; t < TMAX; ++t)
-                bq[t] = *reinterpret_cast<const floatx4*>(
-                    a.tg.bias + max(min(tb0 + t, tb1 - 1), 0) * 16 + (lane >> 4) * 4);
 #pragma unroll
             for (int t = 0; t < TMAX; ++t) {
                 if (t < tb1 - tb0 && m < a.B) {
