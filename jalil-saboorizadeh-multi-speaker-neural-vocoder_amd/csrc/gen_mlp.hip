@@ -524,8 +524,27 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             gmt_grid_barrier(a.tg.bar, nblk, epoch, a.err);
             GM_STAMP();                            // grid barrier passed
         } else {
+            // (the pre-TG order and form: per unit its W_hid then its W_out fragments)
 #pragma unroll
-            for (int i = 0; i < NLD; ++i) ld(i);
+            for (int j = 0; j < UPW; ++j) {
+                const int u = wave + gm::NW * j;
+                const int uc = min(u, NU - 1);
+                const int ke = min(u * UK + (lane >> 4) * EPL, D - EPL);
+#pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    const int n = min(c0 + t * 16 + (lane & 15), D - 1);
+                    lw[j][t] = fh ? fh[(((size_t)p * NU + uc) * nt + min(t, nt - 1)) * 64 + lane]
+                                  : *reinterpret_cast<const uint4*>((const T*)a.w_hid + (int64_t)n * D + ke);
+                }
+                if constexpr (!WOL) {
+#pragma unroll
+                    for (int t = 0; t < NZT; ++t) {
+                        const int n = min(z0 + t * 16 + (lane & 15), Q - 1);
+                        lz[j][t] = fo ? fo[(((size_t)p * NU + uc) * nzt1 + min(t, nzt1 - 1)) * 64 + lane]
+                                      : *reinterpret_cast<const uint4*>((const T*)a.w_out + (int64_t)n * D + ke);
+                    }
+                }
+            }
         }
         if constexpr (WOL) {
             // rows z0 .. z0 + 15 of W_out into LDS (16-B pieces; NZ = 16 at D = 1024)
@@ -535,6 +554,17 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
                 *reinterpret_cast<uint4*>((T*)wol + (size_t)n * (D + 8) + k) =
                     *reinterpret_cast<const uint4*>((const T*)a.w_out +
                                                     (int64_t)min(z0 + n, Q - 1) * D + k);
+            }
+        }
+        if constexpr (!TG) {
+            // the table slice after the W_out copy (its registers are not live across that
+            // loop), an inline loop as before the TG kernels
+#pragma unroll
+            for (int it = 0; it < MAXIT; ++it) {
+                const int e = min(tid + it * gm::NTHR, npc - 1);
+                const int q = e / cpr, c = (e % cpr) * PER;
+                buf[it] = *reinterpret_cast<const uint4*>(
+                    tab + ((int64_t)(FS0 - 1) * Q + q) * D + c0 + c);
             }
         }
         // placement check (wave 0, after its own loads are in flight)
@@ -647,13 +677,14 @@ __global__ __launch_bounds__(gm::NTHR, 2) void gen_mlp_kernel(GenMlpArgs a) {
             const uint32_t row = (uint32_t)xs[k] + (uint32_t)((k < FS0 - 1 ? k : 0) * Q);
             tv[k] = gm_tap_load<T>(rtab, row * (uint32_t)D * (uint32_t)sizeof(T) + colb);
         }
-        {
+        if constexpr (TG) {
             // (TG: up0 was written in this launch by other workgroups, write-through: every
             //  load of it an sc1 load -- MI355X guide, valid forms)
             const float* up = a.up0 + (int64_t)eb * a.ldup + (int64_t)(i % FS0) * D + c0 + ec;
-            upv = TG ? __hip_atomic_load(const_cast<float*>(up), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT)
-                     : *up;
+            upv = __hip_atomic_load(const_cast<float*>(up), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            upv = a.up0[(int64_t)eb * a.ldup + (int64_t)(i % FS0) * D + c0 + ec];
         }
     };
     auto finish_part = [&]() {
