@@ -324,12 +324,16 @@ __device__ bool dtab_pk_declines(const DtabStat* st, const unsigned* amax_in, in
     return dtab_cmax(st, red) > DTAB_PK_CMAX && amax <= 3.402823466e38f;
 }
 
+// x8 (optional): the windows' sample values as bytes, row pitch wp8 (>= W, zero-padded): the
+// packed scatter's 256 column-slice workgroups each read every window, and 1-byte values
+// are 1/8 of the int64 stream's bytes through the L2 and the load path beside their atomics
 template <typename T>
 __global__ __launch_bounds__(256) void dtab_prep_kernel(const T* __restrict__ da, int64_t ldda,
                                                         int64_t nrows, int D,
                                                         const int64_t* __restrict__ x,
                                                         int64_t ldx, int xoff, int W, int B,
-                                                        int nb_da, DtabStat* __restrict__ st) {
+                                                        int nb_da, DtabStat* __restrict__ st,
+                                                        unsigned char* __restrict__ x8, int wp8) {
     __shared__ int hist[256];
     __shared__ unsigned wmax[4];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -389,7 +393,13 @@ __global__ __launch_bounds__(256) void dtab_prep_kernel(const T* __restrict__ da
     for (int i = tid; i < 256; i += 256) hist[i] = 0;
     __syncthreads();
     const int64_t* xr = x + (int64_t)b * ldx + xoff;
-    for (int p = tid; p < W; p += 256) atomicAdd(&hist[(int)xr[p] & 255], 1);
+    for (int p = tid; p < W; p += 256) {
+        const int q = (int)xr[p] & 255;
+        atomicAdd(&hist[q], 1);
+        if (x8) x8[(int64_t)b * wp8 + p] = (unsigned char)q;
+    }
+    if (x8)
+        for (int p = W + tid; p < wp8; p += 256) x8[(int64_t)b * wp8 + p] = 0;
     __syncthreads();
     if (hist[tid]) atomicAdd(&st->count[tid], hist[tid]);
 }
@@ -407,7 +417,8 @@ template <typename T, int PD = 1, bool BLK = false>
 __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
     const T* __restrict__ da, int64_t ldda, const int64_t* __restrict__ x, int64_t ldx, int xoff,
     int Tlen, int B, const DtabStat* __restrict__ st, const unsigned* __restrict__ amax_in,
-    bf16* __restrict__ out, float* __restrict__ colsum, int D, int Q, const T* __restrict__ blk) {
+    bf16* __restrict__ out, float* __restrict__ colsum, int D, int Q, const T* __restrict__ blk,
+    const unsigned char* __restrict__ x8, int wp8) {
     constexpr int CW = 4, FS = 16;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     unsigned long long* acc = reinterpret_cast<unsigned long long*>(smem);  // [Q][2][FS]
@@ -483,6 +494,26 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
             return (unsigned long long)(long long)lo + ((unsigned long long)(unsigned)hi << 32);
         };
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // strip reads of the last rows
+        if (x8) {
+            // the two rows' byte values (dtab_prep_kernel), four per 4-B load, all in flight
+            const int wq = WPB / 4;
+            unsigned* strip4 = reinterpret_cast<unsigned*>(strip);
+            constexpr int NL = 9;                               // 2 WPB / 4 / 64 at T = 1024
+            for (int d0 = lane; d0 < 2 * wq; d0 += 64 * NL) {
+                unsigned v[NL];
+#pragma unroll
+                for (int k = 0; k < NL; ++k) {
+                    const int d = d0 + 64 * k;
+                    const int r = d >= wq, p4 = d - r * wq, row = b2 + r;
+                    v[k] = (d < 2 * wq && row < B && 4 * p4 < wp8)
+                               ? *reinterpret_cast<const unsigned*>(x8 + (int64_t)row * wp8 + 4 * p4)
+                               : 0u;
+                }
+#pragma unroll
+                for (int k = 0; k < NL; ++k)
+                    if (d0 + 64 * k < 2 * wq) strip4[d0 + 64 * k] = v[k];
+            }
+        } else
         // the two rows' indices into the strip: 12 loads in flight per lane per round (one
         // load per round trip was ~40 serialised HBM latencies per row pair)
         for (int q0 = lane; q0 < 2 * WPB; q0 += 64 * 12) {
@@ -693,8 +724,14 @@ extern "C" int srnn_mlp_dtab4(int dtype, const void* da, int64_t ldda, const int
         // the prep pass only counts the sample values
         const int nb_da = amax_in ? 0 : (int)std::min<int64_t>(1024, std::max<int64_t>(1, nrows / 64));
         const int W = Tlen + 15;
+        // the windows as bytes for the packed scatter (SRNN_DTAB_X8=0: it reads the int64 x)
+        const int wp8 = (W + 15) & ~15;
+        const size_t x8off = (sizeof(DtabStat) + 255) & ~(size_t)255;
+        unsigned char* x8 = nullptr;
+        if (work_bytes >= x8off + (size_t)B * wp8 && !getenv_off("SRNN_DTAB_X8"))
+            x8 = (unsigned char*)work + x8off;
         hipLaunchKernelGGL(dtab_prep_kernel<bf16>, dim3(nb_da + B), dim3(256), 0, s,
-                           (const bf16*)da, ldda, nrows, D, x, ldx, xoff, W, B, nb_da, st);
+                           (const bf16*)da, ldda, nrows, D, x, ldx, xoff, W, B, nb_da, st, x8, wp8);
         SRNN_LAUNCH_CHECK();
         static bool attr = false;
         if (!attr) {
@@ -713,7 +750,8 @@ extern "C" int srnn_mlp_dtab4(int dtype, const void* da, int64_t ldda, const int
                 : (pde && pde[0] == '1') ? dtab_pk_kernel<bf16, 1> : dtab_pk_kernel<bf16, 4>;
         hipLaunchKernelGGL(pk, dim3(cdiv(D, 4)), dim3(DTAB_NT),
                            pk_lds_bytes(Q, Tlen), s, (const bf16*)da, ldda, x, ldx, xoff, Tlen, B,
-                           st, amax_in, (bf16*)dtab_out, colsum, D, Q, (const bf16*)blk);
+                           st, amax_in, (bf16*)dtab_out, colsum, D, Q, (const bf16*)blk, x8,
+                           wp8);
         SRNN_LAUNCH_CHECK();
         // the exact form behind it, gated on the same statistics: all of its workgroups
         // return at once unless the packed form declined (a skewed sample histogram)

@@ -9,6 +9,7 @@ env $VAR=$v timeout -k 10 200 python3 bench.py --steps 20 --warmup 3 --no-gen --
 python3 -c "
 import json
 d=json.loads(open('gpurun_out/${TAG}_b${B}_${v}_$r.json').read().strip().splitlines()[-1])
-print('B=$B $VAR=$v round $r:', d['ms_per_step'])
+ks=d.get('kernels',{})
+print('B=$B $VAR=$v round $r:', d['ms_per_step'], {k: ks[k].get('ms_per_step') for k in (${SITES:-'dtab_scatter',}) if k in ks})
 "
 done; done; done
