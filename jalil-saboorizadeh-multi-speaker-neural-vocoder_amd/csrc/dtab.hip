@@ -440,6 +440,7 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
     int* red = reinterpret_cast<int*>(csum + CW * FS);                 // [4] count maxima
     unsigned char* strip = reinterpret_cast<unsigned char*>(red + 4) + wave * 2 * WPB;
     for (int i = tid; i < nacc + CW * FS; i += DTAB_NT) acc[i] = 0ull;
+    const unsigned acc_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)acc;
     // ---- the scale: every workgroup derives the same e from the same statistics
     const int cmax = dtab_cmax(st, red);
     const float amax = __uint_as_float(amax_in ? *amax_in : st->amax_bits);
@@ -455,6 +456,13 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
         return;
     }
     if (cmax > DTAB_PK_CMAX) return;               // the exact form runs instead (gated)
+    if (acc_base != 0u) {
+        // the bins' addresses below are built without a base (the kernel has no static LDS,
+        // so the dynamic block starts at 0); a nonzero base poisons the slice, never mis-adds
+        for (int i = tid; i < Q * FS * CW; i += DTAB_NT)
+            out[(int64_t)(i / CW) * D + c0 + i % CW] = __float2bfloat16(__builtin_nanf(""));
+        return;
+    }
     int e = 0;
     if (amax > 0.f && cmax > 0) {
         int ex;
@@ -464,32 +472,32 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
     const float S = ldexpf(1.0f, e), invS = ldexpf(1.0f, -e);
     const int h = lane >> 5, p = (lane >> 4) & 1, li = lane & 15;
     const int cA = c0 + 2 * p;                     // this lane's pair (cA, cA + 1); D % 4 == 0
-    const int nbatch = (W + 15) / 16;
-    const unsigned acc_base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)acc;
+    const int nbatch = (Tlen + 15) / 16;           // batches of 16 rows t
     const unsigned strip_base =
         (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)strip;
     unsigned long long colA = 0, colB = 0;
-    unsigned lb[16];
+    unsigned lbo[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) lb[j] = acc_base + ((unsigned)(p * FS + ((j - li) & 15)) << 3);
+    for (int j = 0; j < 16; ++j) lbo[j] = (unsigned)(p * FS + ((j - li) & 15)) << 3;
     const bool want_col = colsum != nullptr;
     for (int b2 = 2 * wave; b2 < B; b2 += 2 * (DTAB_NT / 64)) {
         const int b = b2 + h;
         const bool rv = b < B;
         const T* drow = BLK ? blk + ((int64_t)(c0 >> 2) * B * Tlen + (int64_t)(rv ? b : b2) * Tlen) * 4 + 2 * p
                             : da + (int64_t)(rv ? b : b2) * Tlen * ldda + cA;
-        auto raw = [&](int pbase) -> uint32_t {
-            const int t = pbase + li;
-            if (!(rv && t < Tlen)) return 0u;                 // zero bits: a zero pair
+        // the raw pair of batch bt, loaded unconditionally from a clamped row (no branch around
+        // the load, so a prefetched value is waited for where it is used, not where it lands);
+        // rows past Tlen or past B are zeroed at use by live()
+        auto raw = [&](int bt) -> uint32_t {
+            const int t = min(16 * bt + li, Tlen - 1);
             return *reinterpret_cast<const uint32_t*>(drow + (int64_t)t * (BLK ? 4 : ldda));
         };
+        auto live = [&](int bt) -> bool { return rv && 16 * bt + li < Tlen; };
         auto conv = [&](uint32_t u) -> unsigned long long {
             const float gA = to_f(*reinterpret_cast<const T*>(&u));
             const float gB = to_f(*(reinterpret_cast<const T*>(&u) + 1));
-            if (want_col) {
-                colA += (unsigned long long)fx40(gA);
-                colB += (unsigned long long)fx40(gB);
-            }
+            colA += (unsigned long long)fx40(gA);       // used only when want_col (no branch
+            colB += (unsigned long long)fx40(gB);       // in the batch loop)
             const int lo = __float2int_rn(gA * S), hi = __float2int_rn(gB * S);
             return (unsigned long long)(long long)lo + ((unsigned long long)(unsigned)hi << 32);
         };
@@ -529,62 +537,64 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
             for (int k = 0; k < 12; ++k)
                 if (q0 + 64 * k < 2 * WPB) strip[q0 + 64 * k] = (unsigned char)v[k];
         }
-        unsigned long long cur = 0;
-        unsigned long long nxt = conv(raw(0));
-        uint32_t pre[PD > 1 ? PD - 1 : 1];               // raw values of batches bt + 2 ..
+        // Row-major batches: lane li holds da(t = pbase + li) and adds it to its 16 bins
+        // (x[t + k], k); in atomic j it takes k = (j - li) & 15, so t + k is position pbase + j
+        // (li <= j) or pbase + j + 16 (li > j): the index comes from this batch's 16 strip bytes
+        // or the next batch's, and the data operand is the lane's own value in all 16 atomics.
+        // t + k <= Tlen - 1 + 15 < W, so no position leaves the window; lanes past Tlen (or past
+        // B) add zeros at bin row x = strip padding, which is zero.
+        // raw pairs PD batches ahead in a ring unrolled by PD: slot u of the ring is a fixed
+        // register, so its load is waited for (vmcnt(PD - 1)) in the batch that converts it; a
+        // rotating prefetch queue moved every slot each batch and waited for all loads there
+        uint32_t rw[PD];
 #pragma unroll
-        for (int i = 0; i + 1 < PD; ++i) pre[i] = raw(16 * (i + 1));
+        for (int u = 0; u < PD; ++u) rw[u] = raw(u);
         const unsigned sh = strip_base + (unsigned)(h * WPB);
-        dt_u32x4 qn;
-        asm volatile("s_waitcnt lgkmcnt(0)\n\tds_read_b128 %0, %1\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(qn) : "v"(sh) : "memory");
+        dt_u32x4 qa, qb;                                 // strip bytes [pbase, +16), [+16, +32)
+        asm volatile("s_waitcnt lgkmcnt(0)\n\tds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\t"
+                     "s_waitcnt lgkmcnt(0)"
+                     : "=&v"(qa), "=&v"(qb) : "v"(sh) : "memory");
         __builtin_amdgcn_sched_barrier(0);
-        for (int bt = 0; bt < nbatch; ++bt) {
+        // one batch, branch-free: u is the ring slot (a constant after unrolling)
+        auto batch = [&](int bt, int u) {
             const int pbase = bt * 16;
-            const unsigned long long nv = nxt;
-            const dt_u32x4 qc = qn;
-            if (bt + 1 < nbatch) {
-                if constexpr (PD > 1) {
-                    nxt = conv(pre[0]);
-#pragma unroll
-                    for (int i = 0; i + 2 < PD; ++i) pre[i] = pre[i + 1];
-                    pre[PD - 2] = raw(pbase + 16 * PD);
-                } else {
-                    nxt = conv(raw(pbase + 16));
-                }
-                asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(qn)
-                             : "v"(sh + (unsigned)pbase) : "memory");
-            }
-            const int jmax = min(16, W - pbase);
+            const uint32_t rcur = live(bt) ? rw[u] : 0u;   // zero bits: a zero pair
+            const unsigned long long nv = conv(rcur);
+            rw[u] = raw(bt + PD);
+            // the next batch's upper bytes, [pbase + 32, +48): inside the strip for every batch
+            // but the last (WPB >= 16 nbatch + 16), whose read is clamped and never used
+            dt_u32x4 qn;
+            asm volatile("ds_read_b128 %0, %1" : "=v"(qn)
+                         : "v"(sh + (unsigned)min(pbase + 32, WPB - 16)) : "memory");
             unsigned ad[16];
-            unsigned long long va[16];
-            // the 16 indices of this lane's half, from its own broadcast read: a bit-field
-            // extract and a shift-add per atomic on the VALU (the scalar unit is shared by the
-            // CU's 16 waves; extracting two halves there cost 6 SALU per atomic)
+            // one select and one byte permute per atomic: (x << 8) | lbo, x = the strip byte,
+            // lbo < 256 the (pair, k) slot; the Q x 2 x FS u64 bins are 256 B per x row
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
-                const unsigned qv = __builtin_amdgcn_ubfe(qc[j >> 2], 8 * (j & 3), 8);
-                ad[j] = lb[j] + qv * (unsigned)(2 * FS * 8);
-                va[j] = li <= j ? nv : cur;
+                const unsigned w = li <= j ? qa[j >> 2] : qb[j >> 2];
+                ad[j] = __builtin_amdgcn_perm(w, lbo[j], 0x0c0c0000u | ((4u + (j & 3)) << 8));
             }
-            if (jmax == 16) {
 #pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    asm volatile("ds_add_u64 %0, %1" ::"v"(ad[j]), "v"(va[j]) : "memory");
-                asm volatile("" ::"v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]),
-                             "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8]), "v"(ad[9]),
-                             "v"(ad[10]), "v"(ad[11]), "v"(ad[12]), "v"(ad[13]), "v"(ad[14]),
-                             "v"(ad[15]));
-                asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
-            } else {
-#pragma unroll
-                for (int j = 0; j < 16; ++j)
-                    if (j < jmax) asm volatile("ds_add_u64 %0, %1" ::"v"(ad[j]), "v"(va[j]) : "memory");
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            }
+            for (int j = 0; j < 16; ++j)
+                asm volatile("ds_add_u64 %0, %1" ::"v"(ad[j]), "v"(nv) : "memory");
+            asm volatile("" ::"v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]),
+                         "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8]), "v"(ad[9]),
+                         "v"(ad[10]), "v"(ad[11]), "v"(ad[12]), "v"(ad[13]), "v"(ad[14]),
+                         "v"(ad[15]));
+            // the wait redefines qn: no copy of its register can be taken before the read lands
+            asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(qn) :: "memory");
             __builtin_amdgcn_sched_barrier(0);
-            cur = nv;
+            qa = qb;
+            qb = qn;
+        };
+        int bt0 = 0;
+        for (; bt0 + PD <= nbatch; bt0 += PD) {
+#pragma unroll
+            for (int u = 0; u < PD; ++u) batch(bt0 + u, u);
         }
+#pragma unroll
+        for (int u = 0; u + 1 < PD; ++u)
+            if (bt0 + u < nbatch) batch(bt0 + u, u);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (want_col) {
@@ -736,18 +746,23 @@ extern "C" int srnn_mlp_dtab4(int dtype, const void* da, int64_t ldda, const int
         static bool attr = false;
         if (!attr) {
             for (const void* k : {(const void*)dtab_pk_kernel<bf16, 1>,
+                                  (const void*)dtab_pk_kernel<bf16, 2>,
                                   (const void*)dtab_pk_kernel<bf16, 4>,
                                   (const void*)dtab_pk_kernel<bf16, 4, true>})
                 SRNN_CHECK_HIP(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                                    160 * 1024));
             attr = true;
         }
-        // SRNN_DTAB_PD=1: the one-batch-ahead da load (default: four batches ahead);
+        // da prefetch depth, in batches (SRNN_DTAB_PD = 1 / 2 / 4 overrides): measured per B on
+        // one box (profiles/r05_dtab_rowmajor_perm_ab.txt) -- two ahead up to B = 256, one ahead
+        // at B = 512 (1.20 vs 1.29 / 1.32 ms; deeper prefetch there is slower, not faster);
         // blk: the column-blocked copy of da (SRNN_DTAB_BLK=0 reads the row-major da)
         const char* pde = getenv("SRNN_DTAB_PD");
         const bool useblk = blk && !getenv_off("SRNN_DTAB_BLK");
+        const int pd = (pde && pde[0]) ? atoi(pde) : (B >= 384 ? 1 : 2);
         auto pk = useblk ? dtab_pk_kernel<bf16, 4, true>
-                : (pde && pde[0] == '1') ? dtab_pk_kernel<bf16, 1> : dtab_pk_kernel<bf16, 4>;
+                : pd == 1 ? dtab_pk_kernel<bf16, 1>
+                : pd == 2 ? dtab_pk_kernel<bf16, 2> : dtab_pk_kernel<bf16, 4>;
         hipLaunchKernelGGL(pk, dim3(cdiv(D, 4)), dim3(DTAB_NT),
                            pk_lds_bytes(Q, Tlen), s, (const bf16*)da, ldda, x, ldx, xoff, Tlen, B,
                            st, amax_in, (bf16*)dtab_out, colsum, D, Q, (const bf16*)blk, x8,

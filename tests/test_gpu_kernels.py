@@ -779,7 +779,7 @@ def test_mlp_dtab2_colsum(hip, dtype, B, Tl, D):
 
 
 @pytest.mark.parametrize('B,Tl,skew', [(128, 1024, False), (9, 1024, True), (64, 256, True),
-                                        (3, 37, False)])
+                                        (3, 37, False), (5, 70, False), (2, 115, True)])
 def test_mlp_dtab_packed_bf16(hip, monkeypatch, B, Tl, skew):
     """The packed two-columns-per-atomic dTab (bf16 in / out, dtab_pk_kernel) against the exact
     2^-40 path and an fp64 scatter.  Its scale comes from max |da| and the most frequent sample
