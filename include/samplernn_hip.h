@@ -64,7 +64,10 @@ int srnn_gemm_bits(int dtype, int out_dtype, int transA, int transB, int M, int 
                    const float* bias, int bias_mode, int relu, int tile,
                    const unsigned short* mask_bits, int64_t ldmb, unsigned short* bits_out,
                    int64_t ldbo, void* stream);
-/* bits[row * ldb + c / 16] bit c % 16 = (a[row * lda + c] > 0), a in dtype (M x N). */
+/* bits[row * ldb + c / 16] bit c % 16 = (a[row * lda + c] > 0), a in dtype (M x N).
+ * ldb = 0: the grouped layout, u16 [c / 64][row][4] (N % 64 == 0) -- the same bits, laid
+ * out so a GEMM tile's 64-column block is contiguous; srnn_gemm_bits takes it (ldmb = 0)
+ * and its bf16 pair-mode kernels stage it by LDS-DMA ahead of the epilogue.            */
 int srnn_relu_bits(int dtype, const void* a, int64_t lda, int M, int N, unsigned short* bits,
                    int64_t ldb, void* stream);
 
@@ -180,7 +183,8 @@ int srnn_mlp_l1(int dtype, const void* tab, const int64_t* x, int64_t ldx, int x
                 int Tlen, int upper_dtype, const void* upper, int64_t ldu, void* out,
                 int64_t ldo, int D, int FS0, int Q, void* stream);
 /* The same (bf16 table, upper and a1) writing a1's ReLU mask as bits too (srnn_gemm_bits
- * layout, row stride ldb u16), for the masked GEMM of the backward.                    */
+ * layout, row stride ldb u16; ldb = 0: the grouped layout of srnn_relu_bits), for the
+ * masked GEMM of the backward.                                                         */
 int srnn_mlp_l1_bits(const void* tab, const int64_t* x, int64_t ldx, int xoff, int B, int Tlen,
                      const void* upper, int64_t ldu, void* out, int64_t ldo, int D, int FS0,
                      int Q, unsigned short* bits, int64_t ldb, void* stream);

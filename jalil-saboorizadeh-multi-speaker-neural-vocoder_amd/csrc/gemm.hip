@@ -380,7 +380,10 @@ static int gemm_core(int dtype, int out_dtype, int transA, int transB, int M, in
                      const float* bias, int bias_mode, int relu, int batch, int tile,
                      hipStream_t s, const void* mask, int64_t ldmask);
 
-// ---- ReLU masks as bits: bit c % 16 of u16 [row][c / 16] = (value(row, c) > 0) ----------
+// ---- ReLU masks as bits: bit c % 16 of the u16 of (row, column group c / 16) = (value(row,
+// c) > 0).  Two layouts (srnn_bits_index): row-major, u16 [row][c / 16] with row stride ldb;
+// or, ldb = 0, grouped by 64 columns, u16 [c / 64][row][4] (N % 64 == 0): a 256-row x 64-column
+// block of a GEMM tile is 2 KiB contiguous (its epilogue stages them by LDS-DMA, gemm3.hip)
 // (one thread per 16-column group; a column group past N contributes zero bits)
 template <typename T>
 __global__ void relu_bits_kernel(const T* __restrict__ a, int64_t lda, int M, int N,
@@ -392,7 +395,7 @@ __global__ void relu_bits_kernel(const T* __restrict__ a, int64_t lda, int M, in
     unsigned w = 0u;
     for (int c = 0; c < 16 && c0 + c < N; ++c)
         w |= (to_f(a[(int64_t)r * lda + c0 + c]) > 0.f ? 1u : 0u) << c;
-    bits[(int64_t)r * ldb + c0 / 16] = (unsigned short)w;
+    bits[srnn_bits_index(r, c0 / 16, M, ldb)] = (unsigned short)w;
 }
 
 // the bits as a mask tensor of the GEMM input dtype (1 / 0), for the paths without bit input
@@ -402,12 +405,15 @@ __global__ void bits_expand_kernel(const unsigned short* __restrict__ bits, int6
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (int64_t)M * N) return;
     const int r = (int)(e / N), c = (int)(e % N);
-    m[(int64_t)r * ldm + c] = from_f<T>((float)((bits[(int64_t)r * ldb + c / 16] >> (c & 15)) & 1u));
+    m[(int64_t)r * ldm + c] =
+        from_f<T>((float)((bits[srnn_bits_index(r, c / 16, M, ldb)] >> (c & 15)) & 1u));
 }
 
 int srnn_relu_bits_impl(int dtype, const void* a, int64_t lda, int M, int N, unsigned short* bits,
                         int64_t ldb, hipStream_t s) {
-    SRNN_REQUIRE(M >= 0 && N >= 0 && bits && ldb >= (N + 15) / 16, "relu_bits: bad args");
+    SRNN_REQUIRE(M >= 0 && N >= 0 && bits && (ldb >= (N + 15) / 16 || (ldb == 0 && N % 64 == 0)),
+                 "relu_bits: bad args (row stride >= N / 16, or 0 for the grouped layout with "
+                 "N % 64 == 0)");
     const int64_t n = (int64_t)M * ((N + 15) / 16);
     if (n == 0) return 0;
     if (dtype == SRNN_F32)
@@ -437,6 +443,8 @@ int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int 
                          ldb, strideB, beta, Cin, ldcin, strideCin, C, ldc, strideC, bias,
                          bias_mode, relu, batch, tile, s, mask, ldmask);
     SRNN_REQUIRE(batch == 1 && !(mbi && mask), "gemm: bit masks need batch 1 and no bf16 mask");
+    SRNN_REQUIRE(!(mbi && ldmbi == 0) || N % 64 == 0, "gemm: grouped mask bits need N % 64 == 0");
+    SRNN_REQUIRE(!(mbo && ldmbo == 0) || N % 64 == 0, "gemm: grouped mask bits need N % 64 == 0");
     if (M == 0 || N == 0) return 0;
     // the 256-tile kernel reads / writes the bits in its epilogue
     if ((tile < 0 || tile == 5) && (tile == 5 || g_use_gemm3())) {

@@ -165,9 +165,16 @@ __device__ __forceinline__ void g3_store4(bf16* p, const float (&v)[4]) {
 // epilogue of one finished tile (registers -> C); zeroes the accumulators
 // AMX: also reduce max |C| into g.amax (its own instantiation: tracking the max in the
 // plain epilogue pushed the main loops past 256 VGPRs -- ~100 spilled)
-template <typename TO, bool SW, bool CIN, bool MB = false, bool AMX = false, bool CS = false>
+// MB: ReLU mask bits -- 1: g.mbi / g.mbo row-major, read / written here; 2: g.mbi grouped
+// (srnn_bits_index, ldmbi = 0), this wave's 128 rows x 64 columns already staged in LDS at mbl
+// (8 B per row) by the kernel's LDS-DMA ahead of the epilogue
+// AMX: the lane's running max |C| bits (amx) over the launch's tiles: reduced and atomicMax-ed
+// once per wave at the end of the kernel (g3_amax_flush), not per tile -- one atomic address
+// taking 65536 per-tile atomics cost ~0.14 ms of a 1.2-ms GEMM
+template <typename TO, bool SW, bool CIN, int MB = 0, bool AMX = false, bool CS = false>
 __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
-                                              int n0, int wm, int wn, int lane, int kb) {
+                                              int n0, int wm, int wn, int lane, int kb,
+                                              const char* mbl = nullptr, unsigned* amx_run = nullptr) {
     if constexpr (!SW) {
         // plain fp32 partials: lane holds 4 rows x 1 column per fragment
         if (g.ksplit > 1 && g.part) {
@@ -209,7 +216,8 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
     // stores would also wait for every older store and in-flight DMA piece (vmcnt is in
     // order), serialising 32 round trips per tile.  Exactly 32 stores per wave follow.
     TO* Cp = reinterpret_cast<TO*>(g.C);
-    const bf16* mask = reinterpret_cast<const bf16*>(g.mask);
+    // (MB == 2 kernels take no bf16 mask: srnn_gemm3_try admits grouped bits without one)
+    const bf16* mask = MB == 2 ? nullptr : reinterpret_cast<const bf16*>(g.mask);
     const int rbase = m0 + wm * 128 + (lane & 15);
     const int cbase = n0 + wn * 64 + (lane >> 4) * 4;
     floatx4 bcol[4];
@@ -231,10 +239,11 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
     // bit mask: the row's 64 bits of the wave's columns, one 8-B load per row (per half,
     // with the bf16 mask's loads); lane's bit for (fragment j, element e) at
     // (j & 1) * 16 + (lane >> 4) * 4 + e of word j >> 1
-    const unsigned short* mbi = MB ? g.mbi : nullptr;
-    unsigned short* mbo = MB ? g.mbo : nullptr;
+    const unsigned short* mbi = MB == 1 ? g.mbi : nullptr;
+    unsigned short* mbo = MB == 1 ? g.mbo : nullptr;
+    const bool mbits = MB == 2 || mbi;             // outputs zeroed where the mask bit is clear
     const int g4 = (lane >> 4) * 4;
-    unsigned amx = 0u;
+    unsigned amx = AMX ? *amx_run : 0u;
     float cs[CS ? 4 : 1][4];                   // CS: the lane's 16 columns summed over its rows
     if constexpr (CS) {
 #pragma unroll
@@ -258,6 +267,10 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
             for (int i = 0; i < 4; ++i)
                 mk[i][0] = *reinterpret_cast<const u16x4*>(
                     mbi + (int64_t)(rbase + (4 * h + i) * 16) * g.ldmbi + (n0 + wn * 64) / 16);
+        } else if constexpr (MB == 2) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                mk[i][0] = *reinterpret_cast<const u16x4*>(mbl + ((lane & 15) + (4 * h + i) * 16) * 8);
         }
         auto mbit = [&](int ii, int j, int e) -> bool {
             const unsigned w = (unsigned)mk[ii][0][(j >> 1) * 2] |
@@ -296,7 +309,7 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 #pragma unroll
                             for (int e = 0; e < 4; ++e)
                                 v[e] = __uint_as_float((unsigned)mk[ii][j][e] << 16) > 0.f ? v[e] : 0.f;
-                        } else if (mbi) {
+                        } else if (mbits) {
 #pragma unroll
                             for (int e = 0; e < 4; ++e) v[e] = mbit(ii, j, e) ? v[e] : 0.f;
                         }
@@ -304,8 +317,6 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
                         for (int e = 0; e < 2; ++e) {
                             pk[t][e] = (unsigned)__bfloat16_as_ushort(__float2bfloat16(v[2 * e])) |
                                        ((unsigned)__bfloat16_as_ushort(__float2bfloat16(v[2 * e + 1])) << 16);
-                            if constexpr (AMX)
-                                amx = max(amx, max(pk[t][e] & 0x7fffu, (pk[t][e] >> 16) & 0x7fffu));
                             if constexpr (CS) {        // the stored (bf16-rounded) values
                                 cs[j][2 * e] += __uint_as_float(pk[t][e] << 16);
                                 cs[j][2 * e + 1] += __uint_as_float(pk[t][e] & 0xffff0000u);
@@ -327,6 +338,15 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
                         const auto r = __builtin_amdgcn_permlane16_swap(pk[0][e], pk[1][e], false, false);
                         pk[0][e] = r[0];
                         pk[1][e] = r[1];
+                    }
+                    if constexpr (AMX) {
+                        // (after the swap: the wave's maximum is the same over any lane
+                        //  permutation, and no pre-swap copy stays live)
+#pragma unroll
+                        for (int t = 0; t < 2; ++t)
+#pragma unroll
+                            for (int e = 0; e < 2; ++e)
+                                amx = max(amx, max(pk[t][e] & 0x7fffu, (pk[t][e] >> 16) & 0x7fffu));
                     }
                     *reinterpret_cast<uint4*>(Cp + (int64_t)row * g.ldc + cbase + 32 * jp + coff) =
                         make_uint4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
@@ -390,7 +410,7 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
                         v[e] = __uint_as_float((unsigned)mk[ii][j][e] << 16) > 0.f ? v[e] : 0.f;
-                } else if (mbi) {
+                } else if (mbits) {
 #pragma unroll
                     for (int e = 0; e < 4; ++e) v[e] = mbit(ii, j, e) ? v[e] : 0.f;
                 }
@@ -418,14 +438,7 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
             }
         g.csp[(int64_t)((m0 + wm * 128) / 128) * g.N + n0 + wn * 64 + g4 + (q >> 2) * 16 + (q & 3)] = o;
     }
-    if (AMX && g.amax) {
-        // (one atomic per wave and tile, younger than the epilogue's stores: the callers'
-        //  counted DMA waits then cover one store more than needed -- safe)
-        unsigned m = amx;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
-        if (lane == 0 && m) atomicMax(g.amax, m << 16);
-    }
+    if constexpr (AMX) *amx_run = amx;
 }
 
 // The Cin branch is resolved once per tile: a uniform branch inside the store loop makes
@@ -434,22 +447,25 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 // Returns the number of stores each wave issued (SW path): the main loops' counted DMA
 // waits leave exactly that many younger stores in flight, so the count must be exact -- a
 // larger allowance would let a stage's DMA pieces still be outstanding at the read.
-template <typename TO, bool SW, bool MB = false, bool AMX = false, bool CS = false>
+template <typename TO, bool SW, int MB = 0, bool AMX = false, bool CS = false>
 __device__ __forceinline__ int g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
-                                           int n0, int wm, int wn, int lane, int kb) {
+                                           int n0, int wm, int wn, int lane, int kb,
+                                           const char* mbl = nullptr, unsigned* amx_run = nullptr) {
     if constexpr (CS && sizeof(TO) == 2 && SW) {
         // the column-sum kernels (bf16 out, no Cin, no bit masks, no max |C|)
         g3_epilogue_t<TO, SW, false, false, false, true>(g, acc, m0, n0, wm, wn, lane, kb);
         return 17;
     }
     if constexpr (AMX) {
-        g3_epilogue_t<TO, SW, false, false, true>(g, acc, m0, n0, wm, wn, lane, kb);
+        // (with MB == 2 at most: max |C| is never combined with row-major bits or bits out)
+        g3_epilogue_t<TO, SW, false, MB == 2 ? 2 : 0, true>(g, acc, m0, n0, wm, wn, lane, kb, mbl,
+                                                            amx_run);
         return g.blk ? 48 : 16;                    // + the blocked copy's 2 stores per store
     }
-    if constexpr (MB) {
+    if constexpr (MB != 0) {
         // the bit-mask kernels (their own instantiation: the plain epilogue keeps its registers)
-        g3_epilogue_t<TO, SW, false, true>(g, acc, m0, n0, wm, wn, lane, kb);
-        return sizeof(TO) == 2 ? 16 + (g.mbo ? 2 : 0) : 32;
+        g3_epilogue_t<TO, SW, false, MB>(g, acc, m0, n0, wm, wn, lane, kb, mbl);
+        return sizeof(TO) == 2 ? 16 + (MB == 1 && g.mbo ? 2 : 0) : 32;
     }
     if (SW && g.beta != 0.f) {
         g3_epilogue_t<TO, SW, true>(g, acc, m0, n0, wm, wn, lane, kb);
@@ -722,7 +738,7 @@ __device__ __forceinline__ bf16x8 g3p_frag(const char* img, int f0, int u, int l
 // PF: the k-unit 1 fragments of a stage are read into a second register set while unit 0's
 // MFMAs run (3 reads after each of its last four MFMA rows), so the unit-1 MFMAs do not wait
 // for a burst of 12 LDS reads.
-template <typename TO, bool KCA, bool KCB, bool SW, bool MB = false, bool PF = false,
+template <typename TO, bool KCA, bool KCB, bool SW, int MB = 0, bool PF = false,
           bool AMX = false, bool CS = false>
 __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -761,9 +777,20 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     int iu = 0, kti = 0;
     const bf16* srcA[2];
     const bf16* srcB[2];
+    // MB == 2: tile iu's mask bits (grouped layout) for this wave's 128 rows x 64 columns, 1
+    // KiB, one 16-B LDS-DMA piece per lane issued with the tile's first DMA pieces into LDS
+    // buffer iu & 1 (the epilogue of tile iu - 1 reads the other); the stage waits retire it
+    // long before the epilogue reads it (this wave's own bytes: no barrier needed)
     auto set_src = [&]() {
         int m0, n0, kb;
         unit(iu, m0, n0, kb);
+        if constexpr (MB == 2) {
+            // (the wave's block offset is uniform: a scalar; < 2^31 u16 -- M N / 16)
+            const int o = __builtin_amdgcn_readfirstlane(((n0 + wn * 64) >> 6) * g.M + m0 + wm * 128);
+            __builtin_amdgcn_global_load_lds(
+                G3_GLB(g.mbi + (int64_t)o * 4 + 8 * lane),
+                G3_LDS(smem + g3p::LDS + (iu & 1) * 8192 + wave * 1024), 16, 0, 0);
+        }
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int c = wave * g3p::GLW + i;
@@ -827,11 +854,15 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
             else a1[f - 4] = g3p_frag<KCA>(img, wm * 128 + (f - 4) * 16, 1, lane);
         }
     };
+    unsigned amx_run = 0u;                     // AMX: this lane's max |C| bits so far
     auto finish_stage = [&]() {
         if (++ktc == nk) {
             int m0, n0, kb;
             unit(ic, m0, n0, kb);
-            epi = (g.diag & 8) ? 0 : g3_epilogue<TO, SW, MB, AMX, CS>(g, acc, m0, n0, wm, wn, lane, kb);
+            const char* mbl = smem + g3p::LDS + (ic & 1) * 8192 + wave * 1024;
+            epi = (g.diag & 8) ? 0
+                               : g3_epilogue<TO, SW, MB, AMX, CS>(g, acc, m0, n0, wm, wn, lane, kb, mbl,
+                                                                  &amx_run);
             ktc = 0;
             ++ic;
         }
@@ -920,6 +951,14 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
             __builtin_amdgcn_sched_barrier(0);
         }
         finish_stage();
+    }
+    if constexpr (AMX) {
+        if (g.amax) {
+            unsigned m = amx_run;
+#pragma unroll
+            for (int o = 32; o >= 1; o >>= 1) m = max(m, (unsigned)__shfl_xor((int)m, o));
+            if (lane == 0 && m) atomicMax(g.amax, m << 16);
+        }
     }
 }
 
@@ -1275,8 +1314,15 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
                                  : gemm3p_kernel<TO, KCA, KCB, SW>)
                            : gemm3_kernel<TO, KCA, KCB, SW>;
     int ki = q ? 3 : pp ? 2 : pair ? (pf ? 8 : 1) : 0;
+    const bool grouped = g.mbi && g.ldmbi == 0;
+    SRNN_REQUIRE(!grouped || (sizeof(TO) == 2 && SW && pair && !g.mbo),
+                 "gemm3: grouped mask bits need the bf16 pair-mode kernel");
     if constexpr (sizeof(TO) == 2 && SW) {
-        if (g.mbi || g.mbo) {        // ReLU bit masks (srnn_gemm3_try admits modes 0-2 only)
+        if (grouped) {               // grouped bits staged by LDS-DMA (+ max |C| for the dTab)
+            k = g.amax ? gemm3p_kernel<TO, KCA, KCB, SW, 2, false, true>
+                       : gemm3p_kernel<TO, KCA, KCB, SW, 2>;
+            ki = g.amax ? 14 : 13;
+        } else if (g.mbi || g.mbo) { // ReLU bit masks (srnn_gemm3_try admits modes 0-2 only)
             k = pair ? gemm3p_kernel<TO, KCA, KCB, SW, true> : gemm3_kernel<TO, KCA, KCB, SW, true>;
             ki += 4;
         } else if (g.csp && pair) {   // column sums wanted (srnn_gemm_csum_next)
@@ -1292,8 +1338,8 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
         }
     }
     SRNN_REQUIRE(!g.csp || pair, "gemm3: column sums need the pair-mode kernel");
-    const int lds = (pp || pair) ? g3p::LDS : g3::LDS;
-    static bool attr[13] = {};
+    const int lds = (pp || pair) ? g3p::LDS + (grouped ? 16 * 1024 : 0) : g3::LDS;
+    static bool attr[15] = {};
     if (!attr[ki]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -1406,7 +1452,12 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     if (dtype != SRNN_BF16) return -1;
     if ((mbi || mbo) && (out_dtype != SRNN_BF16 || g3_mode() > 2)) return -1;
     if ((mbi && ((uintptr_t)mbi % 8 || ldmbi % 4 || mask)) ||
-        (mbo && ((uintptr_t)mbo % 8 || ldmbo % 4 || beta != 0.f)))
+        (mbo && ((uintptr_t)mbo % 8 || ldmbo % 4 || ldmbo == 0 || beta != 0.f)))
+        return -1;
+    // grouped bits in (ldmbi = 0): the pair-mode kernels only (an operand k-contiguous, K a
+    // multiple of 64, modes 1-2); the caller's fallback expands them otherwise
+    if (mbi && ldmbi == 0 &&
+        (!(g3_mode() == 1 || (g3_mode() == 2 && (!transA || transB))) || K % g3p::BK || mbo))
         return -1;
     if (M % g3::BM || N % g3::BN || K % g3::BK || K == 0) return -1;
     auto al = [](const void* p, int64_t ld, int es) {
@@ -1462,7 +1513,7 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     if (out_dtype == SRNN_F32) return launch3_layout<float, true>(g, kca, kcb, s);
     // max |C| (srnn_gemm_amax_next): computed by the pair-mode kernels (an operand
     // k-contiguous, K a multiple of 64, no bit masks) -- the request is taken only then
-    if (g3_amax_pending() && beta == 0.f && !mbi && !mbo && (kca || kcb) &&
+    if (g3_amax_pending() && beta == 0.f && (!mbi || ldmbi == 0) && !mbo && (kca || kcb) &&
         K % g3p::BK == 0 && g3_mode() <= 2 && (g3_mode() != 0)) {
         g.amax = g3_amax_pending();
         // the blocked copy needs whole 4-column blocks (N % 256 == 0 holds here)

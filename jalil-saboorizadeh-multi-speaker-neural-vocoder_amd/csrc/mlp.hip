@@ -270,7 +270,11 @@ __global__ __launch_bounds__(L1L_NT, 1) void mlp_l1_lds_kernel(
                     nib |= (u - 1u < 0x7f80u ? 1u : 0u) << e;
                 }
                 const unsigned pn = dpp_u32<0xB1>(nib);
-                if (h == 0) bits[r * ldb + (c0 >> 4)] = (unsigned short)(nib | (pn << 8));
+                // (grouped layout, ldb = 0: the 4 column groups of a 64-column block share 8-B
+                //  words, written from one XCD's workgroups -- merged in its L2)
+                if (h == 0)
+                    bits[srnn_bits_index(r, c0 >> 4, (int64_t)B * Tlen, ldb)] =
+                        (unsigned short)(nib | (pn << 8));
             }
         }
         if (more) put_x(ib + ((b + 1 - b0) & 1) * WP);
@@ -361,7 +365,8 @@ extern "C" int srnn_mlp_l1_bits(const void* tab, const int64_t* x, int64_t ldx, 
                                 int Tlen, const void* upper, int64_t ldu, void* out, int64_t ldo,
                                 int D, int FS0, int Q, unsigned short* bits, int64_t ldb,
                                 void* stream) {
-    SRNN_REQUIRE(D % 16 == 0 && FS0 <= 32 && bits && ldb >= D / 16, "mlp_l1_bits: bad args");
+    SRNN_REQUIRE(D % 16 == 0 && FS0 <= 32 && bits && (ldb >= D / 16 || (ldb == 0 && D % 64 == 0)),
+                 "mlp_l1_bits: bad args (bit row stride >= D / 16, or 0 for the grouped layout)");
     if ((int64_t)B * Tlen <= 0) return 0;
     return mlp_l1_launch<bf16, bf16>((const bf16*)tab, x, ldx, xoff, nullptr, B, Tlen,
                                      (const bf16*)upper, ldu, (bf16*)out, ldo, D, FS0, Q,

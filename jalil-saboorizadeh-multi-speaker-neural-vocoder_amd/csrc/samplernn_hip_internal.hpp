@@ -13,6 +13,12 @@ int srnn_gemm_impl(int dtype, int out_dtype, int transA, int transB, int M, int 
 int srnn_relu_bits_impl(int dtype, const void* a, int64_t lda, int M, int N, unsigned short* bits,
                         int64_t ldb, hipStream_t s);
 
+// u16 index of (row r, 16-column group g) in a ReLU bit mask (gemm.hip): row-major [r][g] with
+// row stride ld, or ld == 0: grouped by 64 columns, [g / 4][M][4]
+__host__ __device__ __forceinline__ int64_t srnn_bits_index(int64_t r, int g, int64_t M, int64_t ld) {
+    return ld ? r * ld + g : ((int64_t)(g >> 2) * M + r) * 4 + (g & 3);
+}
+
 // y[M,N] = act(x[M,K] . W[N,K]^T + bias)   (nn.Linear / Conv1d(k=1) forward)
 static inline int linear_fwd(int dt, int odt, int M, int N, int K, const void* x, int64_t ldx,
                              const void* W, int64_t ldw, const float* bias, void* y, int64_t ldy,

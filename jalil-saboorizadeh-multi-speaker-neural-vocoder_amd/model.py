@@ -673,12 +673,24 @@ def mlp_forward(mlp, x, upper, ps):
     # hidden GEMM's bit epilogue costs 26 us and the L1 gather's 2-B bit stores 87 us.
     bits = T == torch.bfloat16 and upper.dtype == T and D % 64 == 0 and \
         os.environ.get('SRNN_MASK_BITS', '0') != '0'
+    # Default (bf16, D % 64 == 0): a1's mask alone leaves as bits, in the grouped layout
+    # (u16 [D / 64][B T][4]): the da1 GEMM stages a tile's bits by LDS-DMA with its first
+    # operand pieces instead of reading 2 B of a1 per output in its epilogue (SRNN_A1_BITS=0:
+    # the bf16 mask).  The grouped words of a 64-column block are written by one XCD's
+    # workgroups of the L1 kernel, merged in its L2 (the row-major layout's 2-B words came
+    # from all eight).
+    a1_bits = not bits and T == torch.bfloat16 and upper.dtype == T and D % 64 == 0 and \
+        os.environ.get('SRNN_A1_BITS', '1') != '0'
     m1 = m2 = None
     if bits:
         m1, m2 = H.relu_bits(B * Tl, D, dev), H.relu_bits(B * Tl, D, dev)
         H.lib().call('srnn_mlp_l1_bits', H.ptr(tab), H.ptr(x), x.stride(0), 0, B, Tl,
                      H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.ptr(m1), m1.stride(0),
                      H.stream())
+    elif a1_bits:
+        m1 = H.relu_bits_grouped(B * Tl, D, dev)
+        H.lib().call('srnn_mlp_l1_bits', H.ptr(tab), H.ptr(x), x.stride(0), 0, B, Tl,
+                     H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.ptr(m1), 0, H.stream())
     else:
         H.lib().call('srnn_mlp_l1', H.dcode(T), H.ptr(tab), H.ptr(x), x.stride(0), 0, B, Tl,
                      H.dcode(upper), H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())

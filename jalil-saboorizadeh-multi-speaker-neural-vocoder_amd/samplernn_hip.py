@@ -449,6 +449,19 @@ def relu_bits(rows, cols, device):
     return torch.empty((rows, (cols + 15) // 16), device=device, dtype=torch.int16)
 
 
+def relu_bits_grouped(rows, cols, device):
+    """A ReLU mask as bits in the grouped layout (u16 [cols / 64][rows][4], cols % 64 == 0;
+    srnn_relu_bits with ldb = 0): a 1-D int16 buffer, passed with row stride 0."""
+    if cols % 64:
+        raise ValueError('grouped mask bits need cols % 64 == 0 (got %d)' % cols)
+    return torch.empty((rows * (cols // 16),), device=device, dtype=torch.int16)
+
+
+def bits_ld(bits):
+    """Row stride (u16) of a bit-mask buffer: 0 for the grouped (1-D) layout."""
+    return bits.stride(0) if bits.dim() == 2 else 0
+
+
 def gemm(a, b, transA=False, transB=False, out=None, out_dtype=torch.float32, bias=None,
          bias_mode=1, relu=False, alpha=1.0, beta=0.0, cin=None, mask=None, M=None, N=None, K=None,
          lda=None, ldb=None, ldc=None, ldcin=None, batch=1, sA=0, sB=0, sC=0, sCin=0, tile=-1,
@@ -482,8 +495,8 @@ def gemm(a, b, transA=False, transB=False, out=None, out_dtype=torch.float32, bi
         lib().call('srnn_gemm_bits', dcode(a), dcode(out), int(transA), int(transB), M, N, K,
                    alpha, ptr(a), lda, ptr(b), ldb, beta, ptr(cin), ldcin or 0, ptr(out), ldc,
                    ptr(bias), bias_mode, int(relu), tile, ptr(mask_bits),
-                   mask_bits.stride(0) if mask_bits is not None else 0, ptr(bits_out),
-                   bits_out.stride(0) if bits_out is not None else 0, stream())
+                   bits_ld(mask_bits) if mask_bits is not None else 0, ptr(bits_out),
+                   bits_ld(bits_out) if bits_out is not None else 0, stream())
     else:
         lib().call('srnn_gemm', dcode(a), dcode(out), int(transA), int(transB), M, N, K, alpha,
                    ptr(a), lda, sA, ptr(b), ldb, sB, beta, ptr(cin), ldcin or 0, sCin, ptr(out),

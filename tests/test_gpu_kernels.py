@@ -1377,6 +1377,74 @@ def test_mlp_l1_bits(hip, B, Tl, D, monkeypatch):
         assert torch.equal(bits, _bits_ref(ref))
 
 
+def _bits_grouped_ref(a):
+    """The same bits in the grouped layout (u16 [N / 64][M][4], flat)."""
+    w = _bits_ref(a)                                        # (M, N / 16)
+    M, G = w.shape
+    return w.reshape(M, G // 4, 4).permute(1, 0, 2).reshape(-1).contiguous()
+
+
+@pytest.mark.parametrize('B,Tl,D', [(16, 1024, 1024), (3, 4096, 272 - 16), (6, 1000, 512)])
+def test_mlp_l1_bits_grouped(hip, B, Tl, D, monkeypatch):
+    """a1's mask bits in the grouped layout (ldb = 0; the L1 LDS kernel's fused bits and the
+    bits pass after the other gathers) == the grouped bits of the plain gather's a1."""
+    FS0, Q = 16, 256
+    g = torch.Generator().manual_seed(B * 5 + D)
+    tab = (torch.randn(FS0, Q, D, generator=g) * 0.3).to(DEV, torch.bfloat16)
+    x = torch.randint(0, Q, (B, Tl + FS0 + 3), generator=g).to(DEV)
+    upper = (torch.randn(B * Tl, D, generator=g) * 0.5).to(DEV, torch.bfloat16)
+    ref = torch.empty(B * Tl, D, device=DEV, dtype=torch.bfloat16)
+    hip.lib().call('srnn_mlp_l1', hip.BF16, hip.ptr(tab), hip.ptr(x), x.shape[1], 2, B, Tl,
+                   hip.BF16, hip.ptr(upper), D, hip.ptr(ref), D, D, FS0, Q, hip.stream())
+    for flag in ('1', '0'):
+        monkeypatch.setenv('SRNN_L1_LDS', flag)
+        out = torch.empty_like(ref)
+        bits = hip.relu_bits_grouped(B * Tl, D, DEV)
+        hip.lib().call('srnn_mlp_l1_bits', hip.ptr(tab), hip.ptr(x), x.shape[1], 2, B, Tl,
+                       hip.ptr(upper), D, hip.ptr(out), D, D, FS0, Q, hip.ptr(bits), 0,
+                       hip.stream())
+        torch.testing.assert_close(out, ref, atol=0, rtol=0)
+        assert torch.equal(bits, _bits_grouped_ref(ref))
+
+
+@pytest.mark.parametrize('M,N,K,amax', [(32768, 1024, 1024, True), (32768, 1024, 1024, False),
+                                        (8192, 512, 192, True), (1024, 256, 128, True),
+                                        (200, 128, 96, False)])
+def test_gemm_mask_bits_grouped(hip, M, N, K, amax):
+    """The grouped mask bits (the da1 GEMM's operand: staged by LDS-DMA in the bf16 pair-mode
+    kernel, expanded to a mask on the other paths) == the bf16 mask tensor, bit for bit, with
+    and without the max |C| request (the same maximum, taken by the same shapes)."""
+    bf = torch.bfloat16
+    A = _rand(M, K, seed=11).to(DEV, bf)
+    W = _rand(N, K, seed=12).to(DEV, bf)                  # W^T stored k-contiguous (NT)
+    act = _rand(M, N, seed=13).to(DEV, bf)
+    act[act.float().abs() < 0.3] = 0.0
+    bits = hip.relu_bits_grouped(M, N, DEV)
+    hip.lib().call('srnn_relu_bits', hip.BF16, hip.ptr(act), N, M, N, hip.ptr(bits), 0,
+                   hip.stream())
+    assert torch.equal(bits, _bits_grouped_ref(act))
+    res = []
+    for kw in (dict(mask=act), dict(mask_bits=bits)):
+        mx = torch.zeros(1, device=DEV, dtype=torch.int32)
+        if amax:
+            hip.lib().call('srnn_gemm_amax_next', hip.ptr(mx))
+        o = hip.gemm(A, W, transB=True, out_dtype=bf, **kw)
+        taken = hip.lib().dll.srnn_gemm_amax_taken() if amax else 0
+        torch.cuda.synchronize()
+        res.append((o, int(mx.item()), taken))
+    assert torch.equal(res[0][0], res[1][0])
+    assert res[0][2] == res[1][2]
+    if res[0][2]:
+        assert res[0][1] == res[1][1]
+        ref = res[0][0].float().abs().max().item()
+        assert res[1][1] == int(np.float32(ref).view(np.int32))
+    if M * N >= 32768 * 1024:
+        assert res[1][2] == 1 or not amax                   # the LDS-staged kernel took it
+    o3 = hip.gemm(A, W, transB=True, mask_bits=bits)       # fp32 out: the expanded fallback
+    o4 = hip.gemm(A, W, transB=True, mask=act)
+    assert torch.equal(o3, o4)
+
+
 @pytest.mark.parametrize('M,N,K,tB,tile', [(1024, 512, 256, False, 5), (512, 1024, 1024, True, 5),
                                            (768, 512, 512, False, 5), (200, 144, 96, False, -1),
                                            (256, 256, 64, True, -1)])

@@ -189,3 +189,32 @@ def test_mask_bits_step_bf16(hip, monkeypatch):
     assert outs[0][1].keys() == outs[1][1].keys()
     for k in outs[0][1]:
         assert torch.equal(outs[0][1][k], outs[1][1][k]), k
+
+
+def test_a1_bits_step_bf16(hip, monkeypatch):
+    """The default grouped a1 mask bits (SRNN_A1_BITS=1: the L1 kernel writes them, the da1
+    GEMM stages them by LDS-DMA): log-probs and every gradient equal the bf16-mask path's
+    (SRNN_A1_BITS=0) bit for bit, at D = 1024 (the pair-mode kernel's grouped-bits form)."""
+    import nn as snn
+    cfg = dict(recipe.CONFIGS['t3'], dim=1024)
+    B, T = 8, 1024
+    g = torch.Generator().manual_seed(5)
+    outs = []
+    for flag in ('0', '1'):
+        monkeypatch.setenv('SRNN_A1_BITS', flag)
+        m, pred = build(cfg, recipe.make_weights(cfg, 23), torch.bfloat16)
+        L = m.lookback
+        g.manual_seed(5)
+        x = torch.randint(0, 256, (B, L + T), generator=g)
+        cond = torch.rand(B, T // L, cfg['cond_dim'], generator=g)
+        spk = torch.arange(B).reshape(-1, 1) % cfg['spk_dim']
+        lp = pred(x[:, :-1].to(DEV), True, cond, spk)
+        loss = snn.sequence_nll_loss_bits(lp, x[:, L:].to(DEV))
+        loss.backward()
+        outs.append((lp.detach().cpu(), {k: p.grad.detach().cpu().clone()
+                                          for k, p in pred.named_parameters()
+                                          if p.grad is not None}))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert outs[0][1].keys() == outs[1][1].keys()
+    for k in outs[0][1]:
+        assert torch.equal(outs[0][1][k], outs[1][1][k]), k

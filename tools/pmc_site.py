@@ -27,7 +27,7 @@ def per_kernel(db, ctr, names):
     for name, cn, v in rows:
         if cn != ctr:
             continue
-        short = name.split('(')[0]
+        short = name.split('(')[0].replace(' ', '')     # template names: given without spaces
         key = next((k for k in names if k in short), None)
         if key is None:
             continue

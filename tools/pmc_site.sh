@@ -4,6 +4,7 @@
 # -> gpurun_out/<TAG>_pmc_<site>_b<rows>.txt (copy to profiles/ for bench.py's roofline.traffic)
 set -e
 R=$PWD; O=$R/gpurun_out; mkdir -p $O; export TMPDIR=/tmp; cd /tmp
+rm -rf /tmp/pf /tmp/pw                                  # (a previous site's databases)
 cmd="python3 $R/bench.py --steps 3 --warmup 2 --no-gen --no-cpu --no-extra --batch $ROWS"
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d /tmp/pf -o run -- $cmd > $O/pmc_${SITE}_f.log 2>&1
 timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d /tmp/pw -o run -- $cmd > $O/pmc_${SITE}_w.log 2>&1
