@@ -119,7 +119,7 @@ def step_mfma_flops(B, T=T_SEQ, D=D_MODEL, fs=FS, C=COND, S=SPK, Q=Q, n_rnn=1):
 
 def site_roofline(site, ms, work_per_step, dtype_peak):
     """Roofline entry of one probed launch site: achieved = algorithmic work / its time."""
-    if site in ('dtab_scatter', 'adam_clip'):
+    if site in ('dtab_scatter', 'adam_clip', 'mlp_l1_gather'):
         ach = work_per_step / (ms * 1e-3) / 1e9
         return {'bound': 'hbm', 'achieved': round(ach, 1), 'peak': MI355X_HBM_TBS * 1000,
                 'unit': 'GB/s', 'frac': round(ach / (MI355X_HBM_TBS * 1000), 4)}
@@ -140,6 +140,9 @@ SITE_NOTES = {
     'mlp_hidden_gemm': 'gemm3p_kernel: sample-level MLP hidden layer (B*T x D x D, bias + '
                        'ReLU epilogue)',
     'adam_clip': 'adam_clip_multi_kernel: fused clamp + Adam over every parameter',
+    'mlp_l1_gather': 'mlp_l1_lds_kernel: sample-level MLP input layer, the folded embedding.conv '
+                     'table gathered from LDS + upper, a1 = ReLU(.) and its mask bits '
+                     '(HBM: upper read, a1 written)',
     'mlp_da1_gemm': 'gemm3p_kernel: sample-level MLP input-activation gradient da1 = (da2 '
                     'W_hid) * [a1 > 0] (B*T x D x D, ReLU-mask epilogue, max |da1| for the '
                     'dTab scale)',

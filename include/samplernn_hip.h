@@ -65,9 +65,9 @@ int srnn_gemm_bits(int dtype, int out_dtype, int transA, int transB, int M, int 
                    const unsigned short* mask_bits, int64_t ldmb, unsigned short* bits_out,
                    int64_t ldbo, void* stream);
 /* bits[row * ldb + c / 16] bit c % 16 = (a[row * lda + c] > 0), a in dtype (M x N).
- * ldb = 0: the grouped layout, u16 [c / 64][row][4] (N % 64 == 0) -- the same bits, laid
- * out so a GEMM tile's 64-column block is contiguous; srnn_gemm_bits takes it (ldmb = 0)
- * and its bf16 pair-mode kernels stage it by LDS-DMA ahead of the epilogue.            */
+ * ldb = 0: the grouped layout, u16 [c / 16][row] (N % 64 == 0) -- the same bits, rows
+ * contiguous per 16-column group; srnn_gemm_bits takes it (ldmb = 0) and its bf16
+ * pair-mode kernels stage it by LDS-DMA ahead of the epilogue.                         */
 int srnn_relu_bits(int dtype, const void* a, int64_t lda, int M, int N, unsigned short* bits,
                    int64_t ldb, void* stream);
 

@@ -382,16 +382,19 @@ static int gemm_core(int dtype, int out_dtype, int transA, int transB, int M, in
 
 // ---- ReLU masks as bits: bit c % 16 of the u16 of (row, column group c / 16) = (value(row,
 // c) > 0).  Two layouts (srnn_bits_index): row-major, u16 [row][c / 16] with row stride ldb;
-// or, ldb = 0, grouped by 64 columns, u16 [c / 64][row][4] (N % 64 == 0): a 256-row x 64-column
-// block of a GEMM tile is 2 KiB contiguous (its epilogue stages them by LDS-DMA, gemm3.hip)
-// (one thread per 16-column group; a column group past N contributes zero bits)
+// or, ldb = 0, grouped: column-group-major u16 [c / 16][row] (N % 64 == 0) -- the L1 kernel's
+// 16-column workgroups write consecutive rows as one contiguous run, and a GEMM tile's rows
+// of a column group are contiguous for its LDS-DMA staging (gemm3.hip)
+// (one thread per 16-column group; a column group past N contributes zero bits; grouped:
+//  consecutive threads take consecutive rows)
 template <typename T>
 __global__ void relu_bits_kernel(const T* __restrict__ a, int64_t lda, int M, int N,
                                  unsigned short* __restrict__ bits, int64_t ldb) {
     const int ng = (N + 15) / 16;
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= (int64_t)M * ng) return;
-    const int r = (int)(e / ng), c0 = (int)(e % ng) * 16;
+    const int r = ldb ? (int)(e / ng) : (int)(e % M);
+    const int c0 = (ldb ? (int)(e % ng) : (int)(e / M)) * 16;
     unsigned w = 0u;
     for (int c = 0; c < 16 && c0 + c < N; ++c)
         w |= (to_f(a[(int64_t)r * lda + c0 + c]) > 0.f ? 1u : 0u) << c;

@@ -166,8 +166,8 @@ __device__ __forceinline__ void g3_store4(bf16* p, const float (&v)[4]) {
 // AMX: also reduce max |C| into g.amax (its own instantiation: tracking the max in the
 // plain epilogue pushed the main loops past 256 VGPRs -- ~100 spilled)
 // MB: ReLU mask bits -- 1: g.mbi / g.mbo row-major, read / written here; 2: g.mbi grouped
-// (srnn_bits_index, ldmbi = 0), this wave's 128 rows x 64 columns already staged in LDS at mbl
-// (8 B per row) by the kernel's LDS-DMA ahead of the epilogue
+// (srnn_bits_index, ldmbi = 0), this wave's 128 rows x 4 column groups already staged in LDS at
+// mbl ([group][row] u16) by the kernel's LDS-DMA ahead of the epilogue
 // AMX: the lane's running max |C| bits (amx) over the launch's tiles: reduced and atomicMax-ed
 // once per wave at the end of the kernel (g3_amax_flush), not per tile -- one atomic address
 // taking 65536 per-tile atomics cost ~0.14 ms of a 1.2-ms GEMM
@@ -268,9 +268,13 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
                 mk[i][0] = *reinterpret_cast<const u16x4*>(
                     mbi + (int64_t)(rbase + (4 * h + i) * 16) * g.ldmbi + (n0 + wn * 64) / 16);
         } else if constexpr (MB == 2) {
+            const unsigned short* mw = reinterpret_cast<const unsigned short*>(mbl);
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-                mk[i][0] = *reinterpret_cast<const u16x4*>(mbl + ((lane & 15) + (4 * h + i) * 16) * 8);
+            for (int i = 0; i < 4; ++i) {
+                const int r = (lane & 15) + (4 * h + i) * 16;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) mk[i][0][c] = mw[c * 128 + r];
+            }
         }
         auto mbit = [&](int ii, int j, int e) -> bool {
             const unsigned w = (unsigned)mk[ii][0][(j >> 1) * 2] |
@@ -777,18 +781,18 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     int iu = 0, kti = 0;
     const bf16* srcA[2];
     const bf16* srcB[2];
-    // MB == 2: tile iu's mask bits (grouped layout) for this wave's 128 rows x 64 columns, 1
-    // KiB, one 16-B LDS-DMA piece per lane issued with the tile's first DMA pieces into LDS
-    // buffer iu & 1 (the epilogue of tile iu - 1 reads the other); the stage waits retire it
-    // long before the epilogue reads it (this wave's own bytes: no barrier needed)
+    // MB == 2: tile iu's mask bits (grouped layout) for this wave's 128 rows x 4 column groups,
+    // 1 KiB: lane l takes 8 rows of group l / 16 (16 B), issued with the tile's first DMA
+    // pieces into LDS buffer iu & 1 (the epilogue of tile iu - 1 reads the other); the stage
+    // waits retire it long before the epilogue reads it (this wave's own bytes: no barrier)
     auto set_src = [&]() {
         int m0, n0, kb;
         unit(iu, m0, n0, kb);
         if constexpr (MB == 2) {
             // (the wave's block offset is uniform: a scalar; < 2^31 u16 -- M N / 16)
-            const int o = __builtin_amdgcn_readfirstlane(((n0 + wn * 64) >> 6) * g.M + m0 + wm * 128);
+            const int o = __builtin_amdgcn_readfirstlane(((n0 + wn * 64) >> 4) * g.M + m0 + wm * 128);
             __builtin_amdgcn_global_load_lds(
-                G3_GLB(g.mbi + (int64_t)o * 4 + 8 * lane),
+                G3_GLB(g.mbi + o + (int64_t)(lane >> 4) * g.M + (lane & 15) * 8),
                 G3_LDS(smem + g3p::LDS + (iu & 1) * 8192 + wave * 1024), 16, 0, 0);
         }
 #pragma unroll
@@ -1457,7 +1461,8 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     // grouped bits in (ldmbi = 0): the pair-mode kernels only (an operand k-contiguous, K a
     // multiple of 64, modes 1-2); the caller's fallback expands them otherwise
     if (mbi && ldmbi == 0 &&
-        (!(g3_mode() == 1 || (g3_mode() == 2 && (!transA || transB))) || K % g3p::BK || mbo))
+        (!(g3_mode() == 1 || (g3_mode() == 2 && (!transA || transB))) || K % g3p::BK || mbo ||
+         (uintptr_t)mbi % 16))
         return -1;
     if (M % g3::BM || N % g3::BN || K % g3::BK || K == 0) return -1;
     auto al = [](const void* p, int64_t ld, int es) {

@@ -270,8 +270,8 @@ __global__ __launch_bounds__(L1L_NT, 1) void mlp_l1_lds_kernel(
                     nib |= (u - 1u < 0x7f80u ? 1u : 0u) << e;
                 }
                 const unsigned pn = dpp_u32<0xB1>(nib);
-                // (grouped layout, ldb = 0: the 4 column groups of a 64-column block share 8-B
-                //  words, written from one XCD's workgroups -- merged in its L2)
+                // (grouped layout, ldb = 0: [column group][row] -- the wave's 32 rows are one
+                //  contiguous 64-B run)
                 if (h == 0)
                     bits[srnn_bits_index(r, c0 >> 4, (int64_t)B * Tlen, ldb)] =
                         (unsigned short)(nib | (pn << 8));

@@ -14,9 +14,9 @@ int srnn_relu_bits_impl(int dtype, const void* a, int64_t lda, int M, int N, uns
                         int64_t ldb, hipStream_t s);
 
 // u16 index of (row r, 16-column group g) in a ReLU bit mask (gemm.hip): row-major [r][g] with
-// row stride ld, or ld == 0: grouped by 64 columns, [g / 4][M][4]
+// row stride ld, or ld == 0: column-group-major [g][M] (the grouped layout)
 __host__ __device__ __forceinline__ int64_t srnn_bits_index(int64_t r, int g, int64_t M, int64_t ld) {
-    return ld ? r * ld + g : ((int64_t)(g >> 2) * M + r) * 4 + (g & 3);
+    return ld ? r * ld + g : (int64_t)g * M + r;
 }
 
 // y[M,N] = act(x[M,K] . W[N,K]^T + bias)   (nn.Linear / Conv1d(k=1) forward)

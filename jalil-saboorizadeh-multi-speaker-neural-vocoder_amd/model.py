@@ -674,14 +674,14 @@ def mlp_forward(mlp, x, upper, ps):
     bits = T == torch.bfloat16 and upper.dtype == T and D % 64 == 0 and \
         os.environ.get('SRNN_MASK_BITS', '0') != '0'
     # Default (bf16, D % 64 == 0): a1's mask alone leaves as bits, in the grouped layout
-    # (u16 [D / 64][B T][4]): the da1 GEMM stages a tile's bits by LDS-DMA with its first
+    # (u16 [D / 16][B T]): the da1 GEMM stages a tile's bits by LDS-DMA with its first
     # operand pieces instead of reading 2 B of a1 per output in its epilogue (SRNN_A1_BITS=0:
-    # the bf16 mask).  The grouped words of a 64-column block are written by one XCD's
-    # workgroups of the L1 kernel, merged in its L2 (the row-major layout's 2-B words came
-    # from all eight).
+    # the bf16 mask).  The L1 kernel's 16-column workgroups write a column group's rows as
+    # contiguous runs (the row-major layout's 2-B words of a row came from 64 workgroups).
     a1_bits = not bits and T == torch.bfloat16 and upper.dtype == T and D % 64 == 0 and \
         os.environ.get('SRNN_A1_BITS', '1') != '0'
     m1 = m2 = None
+    ev = H.roof_begin()
     if bits:
         m1, m2 = H.relu_bits(B * Tl, D, dev), H.relu_bits(B * Tl, D, dev)
         H.lib().call('srnn_mlp_l1_bits', H.ptr(tab), H.ptr(x), x.stride(0), 0, B, Tl,
@@ -694,6 +694,9 @@ def mlp_forward(mlp, x, upper, ps):
     else:
         H.lib().call('srnn_mlp_l1', H.dcode(T), H.ptr(tab), H.ptr(x), x.stride(0), 0, B, Tl,
                      H.dcode(upper), H.ptr(upper), D, H.ptr(a1), D, D, FS0, Q, H.stream())
+    # algorithmic bytes: upper read and a1 written once (+ its mask bits), the index windows
+    H.roof_end('mlp_l1_gather', ev, B * Tl * D * (upper.element_size() + a1.element_size()) +
+               (B * Tl * D // 8 if m1 is not None else 0) + B * (Tl + FS0 - 1) * 8)
     W_hid = _wcast(mlp.hidden, T).reshape(D, D)
     W_out = _wcast(mlp.output, T).reshape(Q, D)
     # bf16: the backward's activation-gradient GEMMs read W^T stored k-contiguous (the NT

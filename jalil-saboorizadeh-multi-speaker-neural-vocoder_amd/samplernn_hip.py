@@ -450,7 +450,7 @@ def relu_bits(rows, cols, device):
 
 
 def relu_bits_grouped(rows, cols, device):
-    """A ReLU mask as bits in the grouped layout (u16 [cols / 64][rows][4], cols % 64 == 0;
+    """A ReLU mask as bits in the grouped layout (u16 [cols / 16][rows], cols % 64 == 0;
     srnn_relu_bits with ldb = 0): a 1-D int16 buffer, passed with row stride 0."""
     if cols % 64:
         raise ValueError('grouped mask bits need cols % 64 == 0 (got %d)' % cols)

@@ -1378,10 +1378,8 @@ def test_mlp_l1_bits(hip, B, Tl, D, monkeypatch):
 
 
 def _bits_grouped_ref(a):
-    """The same bits in the grouped layout (u16 [N / 64][M][4], flat)."""
-    w = _bits_ref(a)                                        # (M, N / 16)
-    M, G = w.shape
-    return w.reshape(M, G // 4, 4).permute(1, 0, 2).reshape(-1).contiguous()
+    """The same bits in the grouped layout (u16 [N / 16][M], flat)."""
+    return _bits_ref(a).t().reshape(-1).contiguous()
 
 
 @pytest.mark.parametrize('B,Tl,D', [(16, 1024, 1024), (3, 4096, 272 - 16), (6, 1000, 512)])
