@@ -259,16 +259,22 @@ __global__ __launch_bounds__(L1L_NT, 1) void mlp_l1_lds_kernel(
             }
 #pragma unroll
             for (int k = 0; k < FS; ++k) l1l_add8(tv[k], a, lo1, hi1);
-            l1_store8(out + r * ldo + c0 + h * 8, a);
+            l1_u16x8 xv;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[e] = __bfloat16_as_ushort(__float2bfloat16(fmaxf(a[e], 0.f)));
+            *reinterpret_cast<l1_u16x8*>(out + r * ldo + c0 + h * 8) = xv;
             if (bits) {
                 // ReLU mask bits of the 16 columns (stored bf16 > 0): this thread's 8, its
-                // pair lane's 8 (DPP quad_perm 1,0,3,2)
-                unsigned nib = 0u;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    const unsigned u = __bfloat16_as_ushort(__float2bfloat16(fmaxf(a[e], 0.f)));
-                    nib |= (u - 1u < 0x7f80u ? 1u : 0u) << e;
-                }
+                // pair lane's 8 (DPP quad_perm 1,0,3,2).  A stored value is a bf16 in
+                // [0, 0x7f80] (fmax took NaN to 0), so u != 0 is bit 15 of u + 0x7fff, for
+                // both halves of a word in one add (no carry crosses: 0x7f80 + 0x7fff < 2^16)
+                const uint4 w = __builtin_bit_cast(uint4, xv);
+                const unsigned t0 = (w.x + 0x7fff7fffu) & 0x80008000u;
+                const unsigned t1 = (w.y + 0x7fff7fffu) & 0x80008000u;
+                const unsigned t2 = (w.z + 0x7fff7fffu) & 0x80008000u;
+                const unsigned t3 = (w.w + 0x7fff7fffu) & 0x80008000u;
+                const unsigned sb = (t0 >> 15) | (t1 >> 13) | (t2 >> 11) | (t3 >> 9);
+                const unsigned nib = (sb | (sb >> 15)) & 0xffu;   // bit e = value e
                 const unsigned pn = dpp_u32<0xB1>(nib);
                 // (grouped layout, ldb = 0: [column group][row] -- the wave's 32 rows are one
                 //  contiguous 64-B run)
