@@ -220,16 +220,19 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
     const bf16* mask = MB == 2 ? nullptr : reinterpret_cast<const bf16*>(g.mask);
     const int rbase = m0 + wm * 128 + (lane & 15);
     const int cbase = n0 + wn * 64 + (lane >> 4) * 4;
+    // MB == 2 (the da1 GEMM's kernels) is lean: no bias, ReLU or blocked copy (srnn_gemm3_try
+    // routes such calls elsewhere), so none of their code or registers is in the epilogue
+    constexpr bool LEAN = MB == 2;
     floatx4 bcol[4];
     float brow[8];
-    if (g.bias_mode == 1) {
+    if (!LEAN && g.bias_mode == 1) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) bcol[j] = *reinterpret_cast<const floatx4*>(g.bias + cbase + j * 16);
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) bcol[j] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
-    if (g.bias_mode == 2) {
+    if (!LEAN && g.bias_mode == 2) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) brow[i] = g.bias[rbase + i * 16];
     } else {
@@ -244,6 +247,7 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
     const bool mbits = MB == 2 || mbi;             // outputs zeroed where the mask bit is clear
     const int g4 = (lane >> 4) * 4;
     unsigned amx = AMX ? *amx_run : 0u;
+    unsigned amx2 = 0u;                        // LEAN: two 15-bit maxima, packed
     float cs[CS ? 4 : 1][4];                   // CS: the lane's 16 columns summed over its rows
     if constexpr (CS) {
 #pragma unroll
@@ -301,11 +305,29 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 #pragma unroll
                     for (int t = 0; t < 2; ++t) {
                         const int j = 2 * jp + t;
+                        if constexpr (LEAN) {
+                            // two columns per instruction: one packed conversion, then the
+                            // pair's two mask bits widened to a 32-bit AND mask (a zeroed
+                            // value's bits are +0, as the select's)
+                            const unsigned w = (unsigned)mk[ii][0][2 * jp] |
+                                               ((unsigned)mk[ii][0][2 * jp + 1] << 16);
+#pragma unroll
+                            for (int e = 0; e < 2; ++e) {
+                                typedef float g3f2 __attribute__((ext_vector_type(2)));
+                                typedef __bf16 g3b2 __attribute__((ext_vector_type(2)));
+                                const g3f2 pv = {g.alpha * acc[i][j][2 * e], g.alpha * acc[i][j][2 * e + 1]};
+                                const unsigned c = __builtin_bit_cast(unsigned, __builtin_convertvector(pv, g3b2));
+                                const unsigned x = __builtin_amdgcn_ubfe(w, (t << 4) + g4 + 2 * e, 2);
+                                pk[t][e] = c & __umul24((x | (x << 15)) & 0x10001u, 0xffffu);
+                            }
+                            acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+                            continue;
+                        }
                         float v[4];
 #pragma unroll
                         for (int e = 0; e < 4; ++e) v[e] = g.alpha * acc[i][j][e] + bcol[j][e] + brow[i];
                         acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-                        if (g.relu) {
+                        if (!LEAN && g.relu) {
 #pragma unroll
                             for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
                         }
@@ -345,16 +367,25 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
                     }
                     if constexpr (AMX) {
                         // (after the swap: the wave's maximum is the same over any lane
-                        //  permutation, and no pre-swap copy stays live)
+                        //  permutation, and no pre-swap copy stays live; LEAN: both halves at
+                        //  once, v_pk_max_u16, folded once per epilogue)
 #pragma unroll
                         for (int t = 0; t < 2; ++t)
 #pragma unroll
-                            for (int e = 0; e < 2; ++e)
-                                amx = max(amx, max(pk[t][e] & 0x7fffu, (pk[t][e] >> 16) & 0x7fffu));
+                            for (int e = 0; e < 2; ++e) {
+                                if constexpr (LEAN) {
+                                    typedef unsigned short g3u2 __attribute__((ext_vector_type(2)));
+                                    amx2 = __builtin_bit_cast(unsigned, __builtin_elementwise_max(
+                                        __builtin_bit_cast(g3u2, amx2),
+                                        __builtin_bit_cast(g3u2, pk[t][e] & 0x7fff7fffu)));
+                                } else {
+                                    amx = max(amx, max(pk[t][e] & 0x7fffu, (pk[t][e] >> 16) & 0x7fffu));
+                                }
+                            }
                     }
                     *reinterpret_cast<uint4*>(Cp + (int64_t)row * g.ldc + cbase + 32 * jp + coff) =
                         make_uint4(pk[0][0], pk[0][1], pk[1][0], pk[1][1]);
-                    if constexpr (AMX) {
+                    if constexpr (AMX && !LEAN) {
                         if (g.blk) {
                             // the same 8 columns as two 4-column blocks: 16 lanes (rows
                             // rbase .. + 15) of a block write one contiguous 128-B line
@@ -442,7 +473,7 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
             }
         g.csp[(int64_t)((m0 + wm * 128) / 128) * g.N + n0 + wn * 64 + g4 + (q >> 2) * 16 + (q & 3)] = o;
     }
-    if constexpr (AMX) *amx_run = amx;
+    if constexpr (AMX) *amx_run = LEAN ? max(amx, max(amx2 & 0xffffu, amx2 >> 16)) : amx;
 }
 
 // The Cin branch is resolved once per tile: a uniform branch inside the store loop makes
@@ -1462,7 +1493,7 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     // multiple of 64, modes 1-2); the caller's fallback expands them otherwise
     if (mbi && ldmbi == 0 &&
         (!(g3_mode() == 1 || (g3_mode() == 2 && (!transA || transB))) || K % g3p::BK || mbo ||
-         (uintptr_t)mbi % 16))
+         (uintptr_t)mbi % 16 || bias || relu || beta != 0.f))
         return -1;
     if (M % g3::BM || N % g3::BN || K % g3::BK || K == 0) return -1;
     auto al = [](const void* p, int64_t ld, int es) {
@@ -1521,8 +1552,9 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     if (g3_amax_pending() && beta == 0.f && (!mbi || ldmbi == 0) && !mbo && (kca || kcb) &&
         K % g3p::BK == 0 && g3_mode() <= 2 && (g3_mode() != 0)) {
         g.amax = g3_amax_pending();
-        // the blocked copy needs whole 4-column blocks (N % 256 == 0 holds here)
-        g.blk = g3_blk_pending();
+        // the blocked copy needs whole 4-column blocks (N % 256 == 0 holds here); the grouped-
+        // bits kernels write none (the caller sees taken == 1 and reads the row-major da1)
+        g.blk = (mbi && ldmbi == 0) ? nullptr : g3_blk_pending();
         g3_amax_pending() = nullptr;
         g3_blk_pending() = nullptr;
         g3_amax_taken() = g.blk ? 2 : 1;
