@@ -146,6 +146,9 @@ SITE_NOTES = {
     'mlp_da1_gemm': 'gemm3p_kernel: sample-level MLP input-activation gradient da1 = (da2 '
                     'W_hid) * [a1 > 0] (B*T x D x D, ReLU-mask epilogue, max |da1| for the '
                     'dTab scale)',
+    'mlp_da2_gemm': 'gemm3p_kernel: sample-level MLP hidden-activation gradient da2 = (dz '
+                    'W_out) * [a2 > 0] (B*T x D x Q, ReLU-mask epilogue, the hidden bias '
+                    'gradient as per-block column sums)',
     'mlp_dw_hid_gemm': 'gemm3_kernel: sample-level MLP hidden weight gradient da2^T a1 '
                        '(D x D x B*T, fp32 out)',
 }

@@ -171,7 +171,7 @@ __device__ __forceinline__ void g3_store4(bf16* p, const float (&v)[4]) {
 // AMX: the lane's running max |C| bits (amx) over the launch's tiles: reduced and atomicMax-ed
 // once per wave at the end of the kernel (g3_amax_flush), not per tile -- one atomic address
 // taking 65536 per-tile atomics cost ~0.14 ms of a 1.2-ms GEMM
-template <typename TO, bool SW, bool CIN, int MB = 0, bool AMX = false, bool CS = false>
+template <typename TO, bool SW, bool CIN, int MB = 0, bool AMX = false, int CS = 0>
 __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
                                               int n0, int wm, int wn, int lane, int kb,
                                               const char* mbl = nullptr, unsigned* amx_run = nullptr) {
@@ -221,18 +221,20 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
     const int rbase = m0 + wm * 128 + (lane & 15);
     const int cbase = n0 + wn * 64 + (lane >> 4) * 4;
     // MB == 2 (the da1 GEMM's kernels) is lean: no bias, ReLU or blocked copy (srnn_gemm3_try
-    // routes such calls elsewhere), so none of their code or registers is in the epilogue
+    // routes such calls elsewhere), so none of their code or registers is in the epilogue; the
+    // (the same for the column-sum kernels measured slower: da2 0.67 -> 0.70 ms, not kept)
     constexpr bool LEAN = MB == 2;
+    constexpr bool NOB = LEAN;
     floatx4 bcol[4];
     float brow[8];
-    if (!LEAN && g.bias_mode == 1) {
+    if (!NOB && g.bias_mode == 1) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) bcol[j] = *reinterpret_cast<const floatx4*>(g.bias + cbase + j * 16);
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) bcol[j] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
-    if (!LEAN && g.bias_mode == 2) {
+    if (!NOB && g.bias_mode == 2) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) brow[i] = g.bias[rbase + i * 16];
     } else {
@@ -325,9 +327,10 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
                         }
                         float v[4];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) v[e] = g.alpha * acc[i][j][e] + bcol[j][e] + brow[i];
+                        for (int e = 0; e < 4; ++e)
+                            v[e] = NOB ? g.alpha * acc[i][j][e] : g.alpha * acc[i][j][e] + bcol[j][e] + brow[i];
                         acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-                        if (!LEAN && g.relu) {
+                        if (!NOB && g.relu) {
 #pragma unroll
                             for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
                         }
@@ -482,13 +485,13 @@ __device__ __forceinline__ void g3_epilogue_t(const Gemm3Args& g, floatx4 (&acc)
 // Returns the number of stores each wave issued (SW path): the main loops' counted DMA
 // waits leave exactly that many younger stores in flight, so the count must be exact -- a
 // larger allowance would let a stage's DMA pieces still be outstanding at the read.
-template <typename TO, bool SW, int MB = 0, bool AMX = false, bool CS = false>
+template <typename TO, bool SW, int MB = 0, bool AMX = false, int CS = 0>
 __device__ __forceinline__ int g3_epilogue(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
                                            int n0, int wm, int wn, int lane, int kb,
                                            const char* mbl = nullptr, unsigned* amx_run = nullptr) {
     if constexpr (CS && sizeof(TO) == 2 && SW) {
         // the column-sum kernels (bf16 out, no Cin, no bit masks, no max |C|)
-        g3_epilogue_t<TO, SW, false, false, false, true>(g, acc, m0, n0, wm, wn, lane, kb);
+        g3_epilogue_t<TO, SW, false, 0, false, CS>(g, acc, m0, n0, wm, wn, lane, kb);
         return 17;
     }
     if constexpr (AMX) {
@@ -774,7 +777,7 @@ __device__ __forceinline__ bf16x8 g3p_frag(const char* img, int f0, int u, int l
 // MFMAs run (3 reads after each of its last four MFMA rows), so the unit-1 MFMAs do not wait
 // for a burst of 12 LDS reads.
 template <typename TO, bool KCA, bool KCB, bool SW, int MB = 0, bool PF = false,
-          bool AMX = false, bool CS = false>
+          bool AMX = false, int CS = 0>
 __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -1361,8 +1364,8 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
             k = pair ? gemm3p_kernel<TO, KCA, KCB, SW, true> : gemm3_kernel<TO, KCA, KCB, SW, true>;
             ki += 4;
         } else if (g.csp && pair) {   // column sums wanted (srnn_gemm_csum_next)
-            k = pf ? gemm3p_kernel<TO, KCA, KCB, SW, false, true, false, true>
-                   : gemm3p_kernel<TO, KCA, KCB, SW, false, false, false, true>;
+            k = pf ? gemm3p_kernel<TO, KCA, KCB, SW, 0, true, false, 1>
+                   : gemm3p_kernel<TO, KCA, KCB, SW, 0, false, false, 1>;
             ki = pf ? 12 : 11;
         } else if (g.amax && pair) {  // max |C| wanted (srnn_gemm_amax_next)
             // (SRNN_G3_AMX_PF: with the unit-1 fragment prefetch as well)

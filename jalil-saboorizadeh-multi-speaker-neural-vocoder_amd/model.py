@@ -756,10 +756,12 @@ def mlp_backward(ctx, dlogp, nll=None):
     if T == torch.bfloat16 and M % 256 == 0 and os.environ.get('SRNN_CSUM_EPI', '1') != '0':
         csp = torch.empty((M // 128, D), device=dev, dtype=torch.float32)
         H.lib().call('srnn_gemm_csum_next', H.ptr(csp))
+    ev = H.roof_begin()
     if m2 is not None:
         da2 = H.gemm(dz, Wo, transB=tB, mask_bits=m2, out_dtype=T)
     else:
         da2 = H.gemm(dz, Wo, transB=tB, mask=a2, out_dtype=T)
+    H.roof_end('mlp_da2_gemm', ev, 2.0 * M * D * Q)
     if csp is not None and not H.lib().dll.srnn_gemm_csum_taken():
         csp = None
     if csp is not None:
