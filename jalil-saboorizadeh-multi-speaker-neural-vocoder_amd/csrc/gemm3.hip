@@ -1357,9 +1357,13 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
                  "gemm3: grouped mask bits need the bf16 pair-mode kernel");
     if constexpr (sizeof(TO) == 2 && SW) {
         if (grouped) {               // grouped bits staged by LDS-DMA (+ max |C| for the dTab)
-            k = g.amax ? gemm3p_kernel<TO, KCA, KCB, SW, 2, false, true>
+            // with the unit-1 fragment prefetch (SRNN_G3_BITS_PF=0: without): da1 1.11 -> 1.09
+            // ms at B = 512 on one box (profiles/r05_da1_grouped_bits.txt)
+            const bool bpf = env_flag("SRNN_G3_BITS_PF", 1) != 0;
+            k = g.amax ? (bpf ? gemm3p_kernel<TO, KCA, KCB, SW, 2, true, true>
+                              : gemm3p_kernel<TO, KCA, KCB, SW, 2, false, true>)
                        : gemm3p_kernel<TO, KCA, KCB, SW, 2>;
-            ki = g.amax ? 14 : 13;
+            ki = g.amax ? (bpf ? 15 : 14) : 13;
         } else if (g.mbi || g.mbo) { // ReLU bit masks (srnn_gemm3_try admits modes 0-2 only)
             k = pair ? gemm3p_kernel<TO, KCA, KCB, SW, true> : gemm3_kernel<TO, KCA, KCB, SW, true>;
             ki += 4;
@@ -1377,7 +1381,7 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
     }
     SRNN_REQUIRE(!g.csp || pair, "gemm3: column sums need the pair-mode kernel");
     const int lds = (pp || pair) ? g3p::LDS + (grouped ? 16 * 1024 : 0) : g3::LDS;
-    static bool attr[15] = {};
+    static bool attr[16] = {};
     if (!attr[ki]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds));
