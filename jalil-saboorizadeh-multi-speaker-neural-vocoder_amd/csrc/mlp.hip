@@ -222,6 +222,7 @@ __global__ __launch_bounds__(L1L_NT, 1) void mlp_l1_lds_kernel(
     asm volatile("" : "+v"(one_lo), "+v"(one_hi));
     const l1_bf16x2 lo1 = __builtin_bit_cast(l1_bf16x2, one_lo);
     const l1_bf16x2 hi1 = __builtin_bit_cast(l1_bf16x2, one_hi);
+    const char* const tlh = tl + h * 16;                    // this lane's 8 columns of an entry
     load_x(b0);
     load_u(b0);
     put_x(ib);
@@ -254,8 +255,10 @@ __global__ __launch_bounds__(L1L_NT, 1) void mlp_l1_lds_kernel(
             uint4 tv[FS];
 #pragma unroll
             for (int k = 0; k < FS; ++k) {
+                // (q << 5) + this half's base, the tap's k Q 32 an immediate offset: one
+                // shift-add per read after the byte extract
                 const unsigned q = (q4[k >> 2] >> (8 * (k & 3))) & 0xffu;
-                tv[k] = *reinterpret_cast<const uint4*>(tl + ((k * Q + q) * 2 + h) * 16);
+                tv[k] = *reinterpret_cast<const uint4*>(tlh + k * Q * 32 + (q << 5));
             }
 #pragma unroll
             for (int k = 0; k < FS; ++k) l1l_add8(tv[k], a, lo1, hi1);
