@@ -30,6 +30,11 @@ it the line carries
     the TBPTT step at configs[1]'s batch and of generation at configs[2]'s.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--batch ROWS_PER_GPU] [--no-gen]
+
+--gpus N > 1 outside torchrun spawns the N ranks itself (spawn_ranks: N child processes with
+the torchrun environment, the parent touching no GPU); under torchrun (WORLD_SIZE set) each
+process is one rank.  `n_gpus` is the process group's size, `rccl_ranks` the ranks of an RCCL
+group (0 under gloo).
 """
 import argparse
 import json
@@ -389,6 +394,40 @@ def gen_traffic(kind='gen'):
     return _pmc_file('r*_pmc_%s.txt' % kind)
 
 
+def host_cores():
+    """The host CPUs this process may use: the CPU affinity mask, capped by the cgroup's CPU
+    quota (cpu.max) and by OMP_NUM_THREADS when set -- on the GPU box os.cpu_count() reports
+    the whole machine, of which one GPU's job gets a share (the box sets OMP_NUM_THREADS to
+    it).  `usable` is what the CPU baseline runs on (all of it)."""
+    visible = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = visible
+    quota = None
+    for path in ('/sys/fs/cgroup/cpu.max',):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != 'max':
+                quota = max(1, int(int(q) / int(per)))
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+            per = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    usable = min(aff, quota) if quota else aff
+    omp = os.environ.get('OMP_NUM_THREADS', '')
+    if omp.isdigit() and int(omp) > 0:
+        usable = min(usable, int(omp))      # the job's declared CPU share (16 per GPU box)
+    return {'usable': usable, 'os_cpu_count': visible, 'affinity': aff, 'cgroup_quota': quota,
+            'omp_num_threads': os.environ.get('OMP_NUM_THREADS')}
+
+
 def cpu_baseline(seconds_budget=30.0):
     """The oracle (torch-CPU restatement of the reference, validated against the reference's
     timing here: profiles/r03_oracle_vs_reference.txt) on the host cores: a bounded TBPTT
@@ -396,7 +435,8 @@ def cpu_baseline(seconds_budget=30.0):
     configs[2]'s (128 utterances x 4 top-tier frames = 256 steps)."""
     sys.path.insert(0, os.path.join(ROOT, 'oracle'))
     import samplernn_oracle as O
-    threads = min(16, os.cpu_count() or 1)
+    hc = host_cores()
+    threads = hc['usable']
     torch.set_num_threads(threads)
     m, pred = make_model(torch.float32)
     sd = {k: v.detach().clone() for k, v in pred.state_dict().items()}
@@ -436,7 +476,93 @@ def cpu_baseline(seconds_budget=30.0):
            'sample': 'oracle Generator loop (model.py:445-520 restated), 128 utterances x 256 '
                      'samples at configs[2] dims after a 64-sample warm-up, %d threads' % threads}
     tb['gen'] = gen
+    tb['host_cores'] = hc
     return tb
+
+
+def _free_port():
+    import socket
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _die_with_parent():
+    """preexec_fn of a rank: SIGKILL it if the launching process dies (a killed parent must
+    not leave ranks waiting in a collective)."""
+    import ctypes
+    import signal
+    try:
+        ctypes.CDLL('libc.so.6', use_errno=True).prctl(1, signal.SIGKILL)   # PR_SET_PDEATHSIG
+    except OSError:
+        pass
+
+
+def spawn_ranks(n, argv=None, env=None, poll_s=0.5, script=None):
+    """`python bench.py --gpus N` outside torchrun: start N fresh child processes of this
+    script, one per GPU, with the torchrun environment (RANK = LOCAL_RANK = r, WORLD_SIZE =
+    LOCAL_WORLD_SIZE = N, MASTER_ADDR 127.0.0.1, a free MASTER_PORT); distributed.init pins
+    each to cuda:LOCAL_RANK and opens the process group (RCCL unless SRNN_DIST_BACKEND says
+    otherwise).  This process never touches a GPU and never execs: it forwards rank 0's
+    stdout (the JSON line), lets every rank's stderr through, and returns non-zero -- after
+    killing the other ranks -- as soon as any rank fails.  Returns the exit status."""
+    import subprocess
+    import threading
+    argv = list(sys.argv[1:] if argv is None else argv)
+    backend = (env or os.environ).get('SRNN_DIST_BACKEND', 'nccl')
+    ndev = torch.cuda.device_count()          # does not initialise the GPU on this image
+    if backend == 'nccl' and script is None and ndev < n:
+        log('bench: --gpus %d needs %d visible GPUs for RCCL (one rank per GPU), %d visible; '
+            'SRNN_DIST_BACKEND=gloo runs a rehearsal with ranks sharing GPUs' % (n, n, ndev))
+        return 2
+    port = _free_port()
+    procs, out_lines = [], []
+    for r in range(n):
+        e = dict(os.environ if env is None else env)
+        e.update({'RANK': str(r), 'LOCAL_RANK': str(r), 'WORLD_SIZE': str(n),
+                  'LOCAL_WORLD_SIZE': str(n), 'GROUP_RANK': '0', 'MASTER_ADDR': '127.0.0.1',
+                  'MASTER_PORT': str(port)})
+        procs.append(subprocess.Popen(
+            [sys.executable, script or os.path.abspath(__file__)] + argv, env=e,
+            stdout=subprocess.PIPE if r == 0 else sys.stderr, preexec_fn=_die_with_parent,
+            text=True))
+    log('bench: %d ranks spawned (pids %s, master 127.0.0.1:%d)'
+        % (n, ' '.join(str(p.pid) for p in procs), port))
+
+    def pump():
+        for line in procs[0].stdout:
+            out_lines.append(line)
+    reader = threading.Thread(target=pump, daemon=True)
+    reader.start()
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                rc = bad[0][1] if bad[0][1] > 0 else 128 - bad[0][1]
+                log('bench: rank %d exited with %s; stopping the other ranks' % bad[0])
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        reader.join(timeout=10)
+    for line in out_lines:
+        sys.stdout.write(line)
+    sys.stdout.flush()
+    return rc
 
 
 def main():
@@ -457,13 +583,21 @@ def main():
     ap.add_argument('--no-extra', action='store_true', help='skip config_b / weak_64 lines')
     args = ap.parse_args()
 
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # not under torchrun: this process touches no GPU and runs N ranks as children
+        sys.exit(spawn_ranks(args.gpus))
+
     import distributed as D
     D.init()
     dev = torch.device('cuda', D.device_index())
     torch.cuda.set_device(dev)
     N = D.world()
+    pg = {'backend': None, 'world_size': 1}
+    if torch.distributed.is_available() and torch.distributed.is_initialized():
+        N = torch.distributed.get_world_size()
+        pg = {'backend': torch.distributed.get_backend(), 'world_size': N}
     if N != args.gpus:
-        log('warning: --gpus %d but WORLD_SIZE %d' % (args.gpus, N))
+        log('warning: --gpus %d but the process group has %d rank(s)' % (args.gpus, N))
     dtype = torch.bfloat16 if args.dtype == 'bf16' else torch.float32
     peak = MI355X_BF16_TFLOPS if args.dtype == 'bf16' else MI355X_FP32_TFLOPS
     strong = args.batch is None
@@ -594,6 +728,8 @@ def main():
     if D.rank() == 0:
         line = {'metric': METRIC, 'value': summ['value'], 'unit': 'samples/s',
                 'n_gpus': N, 'steps': args.steps, 'warmup': args.warmup,
+                'rccl_ranks': pg['world_size'] if pg['backend'] == 'nccl' else 0,
+                'process_group': pg,
                 'ms_per_step': summ['ms_per_step'], 'higher_is_better': True,
                 'scaling': 'strong' if strong else 'weak',
                 'vs_baseline': None, 'dtype': args.dtype, 'data': 'synthetic',

@@ -25,6 +25,10 @@ extern "C" {
 
 const char* srnn_last_error(void);
 int srnn_abi_version(void);
+/* Content hash (16 hex digits, csrc/srchash.py) of the sources this library was compiled
+ * from; the Python binding refuses a library whose hash differs from its tree's (a stale
+ * build).  Replaces no reference interface.                                             */
+const char* srnn_build_hash(void);
 
 /* ---- mu-law / linear quantisation ------------------------------------------------
  * utils.uquantize (utils.py:58-59 = midrise(ulaw(x)), utils.py:33-36,48-51): bit-exact to
@@ -239,6 +243,10 @@ int srnn_mlp_dtab4(int dtype, const void* da, int64_t ldda, const int64_t* x, in
                    int xoff, int B, int Tlen, void* dtab_out, int out_dtype, int D, int FS0, int Q,
                    void* work, size_t work_bytes, float* colsum, int* colsum_done,
                    const unsigned* amax_in, const void* blk, void* stream);
+/* 1 if the packed dTab kernels may run: they address their LDS bins without a base, valid
+ * only while they have no static LDS (checked from the compiled kernels' attributes; 0 sends
+ * srnn_mlp_dtab4 to the exact form).  Diagnostic; needs a device.                        */
+int srnn_dtab_packed_ok(void);
 /* Number of GEMMs srnn_gemm / srnn_gemm_bits handed to hipBLASLt so far in this process:
  * large plain bf16 problems (alpha, per-column bias, ReLU, beta 0, no mask; M N >= 4 Mi,
  * 2 M N K >= 2^33) run as the ROCm library GEMM (SRNN_BLASLT=0: the library's own gemm3

@@ -244,12 +244,14 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pos_kernel(
                              "v"(ad[5]), "v"(ad[6]), "v"(ad[7]), "v"(ad[8]), "v"(ad[9]),
                              "v"(ad[10]), "v"(ad[11]), "v"(ad[12]), "v"(ad[13]), "v"(ad[14]),
                              "v"(ad[15]));
-                asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+                // the wait redefines qn (the asynchronous asm read above): no copy of its
+                // register can be taken before the read lands
+                asm volatile("s_waitcnt lgkmcnt(15)" : "+v"(qn) :: "memory");
             } else {
 #pragma unroll
                 for (int j = 0; j < 16; ++j)
                     if (j < jmax) asm volatile("ds_add_u64 %0, %1" ::"v"(ad[j]), "v"(va[j]) : "memory");
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(qn) :: "memory");
             }
             __builtin_amdgcn_sched_barrier(0);
             cur = nv;
@@ -458,9 +460,14 @@ __global__ __launch_bounds__(DTAB_NT) void dtab_pk_kernel(
     if (cmax > DTAB_PK_CMAX) return;               // the exact form runs instead (gated)
     if (acc_base != 0u) {
         // the bins' addresses below are built without a base (the kernel has no static LDS,
-        // so the dynamic block starts at 0); a nonzero base poisons the slice, never mis-adds
+        // so the dynamic block starts at 0).  srnn_mlp_dtab4 checks that on the host before it
+        // takes this kernel (pk_static_lds_ok) and runs the exact form otherwise, so this is
+        // unreachable; should it ever be reached, dTab AND its column sums are poisoned (NaN
+        // is loud downstream), never mis-added
+        const float qn = __builtin_nanf("");
         for (int i = tid; i < Q * FS * CW; i += DTAB_NT)
-            out[(int64_t)(i / CW) * D + c0 + i % CW] = __float2bfloat16(__builtin_nanf(""));
+            out[(int64_t)(i / CW) * D + c0 + i % CW] = __float2bfloat16(qn);
+        if (colsum && tid < CW * FS) colsum[(int64_t)(tid % FS) * D + c0 + tid / FS] = qn;
         return;
     }
     int e = 0;
@@ -662,6 +669,26 @@ static int pos_lds_bytes(int Q, int Tlen) {
     return Q * 16 * 4 * 8 + 4 * 16 * 8 + (DTAB_NT / 64) * WPB;
 }
 
+// The packed kernel builds its LDS bin addresses without a base: valid only while it has no
+// static LDS (the dynamic block then starts at offset 0).  Checked once per process from the
+// compiled kernels' attributes; false sends the call to the exact form.
+static bool pk_static_lds_ok() {
+    static int ok = -1;
+    if (ok < 0) {
+        ok = 1;
+        for (const void* k : {(const void*)dtab_pk_kernel<bf16, 1>,
+                              (const void*)dtab_pk_kernel<bf16, 2>,
+                              (const void*)dtab_pk_kernel<bf16, 4>,
+                              (const void*)dtab_pk_kernel<bf16, 4, true>}) {
+            hipFuncAttributes fa;
+            if (hipFuncGetAttributes(&fa, k) != hipSuccess || fa.sharedSizeBytes != 0) ok = 0;
+        }
+    }
+    return ok == 1;
+}
+
+extern "C" int srnn_dtab_packed_ok(void) { return pk_static_lds_ok() ? 1 : 0; }
+
 static int pk_lds_bytes(int Q, int Tlen) {
     const int W = Tlen + 15, WPB = (W + 31) & ~15;
     return Q * 2 * 16 * 8 + 4 * 16 * 8 + 16 + (DTAB_NT / 64) * 2 * WPB;
@@ -726,7 +753,7 @@ extern "C" int srnn_mlp_dtab4(int dtype, const void* da, int64_t ldda, const int
         // the packed kernel writes nothing when the histogram is too skewed for its scale and
         // leaves dTab to the gated exact form: take it only where that form fits too
         pos_lds_bytes(Q, Tlen) <= 160 * 1024 && (int64_t)B * Tlen > 0 &&
-        work_bytes >= sizeof(DtabStat) && !getenv_off("SRNN_DTAB_PACK")) {
+        work_bytes >= sizeof(DtabStat) && !getenv_off("SRNN_DTAB_PACK") && pk_static_lds_ok()) {
         DtabStat* st = (DtabStat*)work;
         SRNN_CHECK_HIP(hipMemsetAsync(st, 0, sizeof(DtabStat), s));
         const int64_t nrows = (int64_t)B * Tlen;

@@ -1353,8 +1353,9 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
                            : gemm3_kernel<TO, KCA, KCB, SW>;
     int ki = q ? 3 : pp ? 2 : pair ? (pf ? 8 : 1) : 0;
     const bool grouped = g.mbi && g.ldmbi == 0;
-    SRNN_REQUIRE(!grouped || (sizeof(TO) == 2 && SW && pair && !g.mbo),
-                 "gemm3: grouped mask bits need the bf16 pair-mode kernel");
+    SRNN_REQUIRE(!grouped || (sizeof(TO) == 2 && SW && pair && !g.mbo &&
+                              g.K / g.ksplit >= 2 * g3p::BK),
+                 "gemm3: grouped mask bits need the bf16 pair-mode kernel and >= 2 k-chunks");
     if constexpr (sizeof(TO) == 2 && SW) {
         if (grouped) {               // grouped bits staged by LDS-DMA (+ max |C| for the dTab)
             // with the unit-1 fragment prefetch (SRNN_G3_BITS_PF=0: without): da1 1.11 -> 1.09
@@ -1497,10 +1498,13 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
         (mbo && ((uintptr_t)mbo % 8 || ldmbo % 4 || ldmbo == 0 || beta != 0.f)))
         return -1;
     // grouped bits in (ldmbi = 0): the pair-mode kernels only (an operand k-contiguous, K a
-    // multiple of 64, modes 1-2); the caller's fallback expands them otherwise
+    // multiple of 64, modes 1-2); the caller's fallback expands them otherwise.  K >= 128:
+    // the kernel stages tile iu's bits into buffer iu & 1 while issuing the previous tile's
+    // LAST k-chunk, and with one chunk per tile (K = 64) that is the stage whose epilogue
+    // still reads tile iu - 2's bits from the same buffer
     if (mbi && ldmbi == 0 &&
-        (!(g3_mode() == 1 || (g3_mode() == 2 && (!transA || transB))) || K % g3p::BK || mbo ||
-         (uintptr_t)mbi % 16 || bias || relu || beta != 0.f))
+        (!(g3_mode() == 1 || (g3_mode() == 2 && (!transA || transB))) || K % g3p::BK ||
+         K < 2 * g3p::BK || mbo || (uintptr_t)mbi % 16 || bias || relu || beta != 0.f))
         return -1;
     if (M % g3::BM || N % g3::BN || K % g3::BK || K == 0) return -1;
     auto al = [](const void* p, int64_t ld, int es) {

@@ -64,18 +64,44 @@ def init(backend=None):
     _declare_device_share()
 
 
+def device_key():
+    """(host, PCI address, UUID) of this rank's GPU: the physical device, whatever
+    HIP/ROCR/CUDA_VISIBLE_DEVICES renumbering each process sees."""
+    import socket
+    p = torch.cuda.get_device_properties(device_index())
+    return (socket.gethostname(), '%04x:%02x:%02x' % (p.pci_domain_id, p.pci_bus_id,
+                                                      p.pci_device_id), str(p.uuid))
+
+
+def device_share(keys, mine):
+    """How many ranks' device keys name this rank's physical GPU."""
+    return sum(1 for k in keys if tuple(k) == tuple(mine))
+
+
 def _declare_device_share():
-    """Ranks of this node that map onto one GPU (a rehearsal: more local ranks than visible
-    devices) each run persistent sweeps on it at once.  Their grids are only co-resident if
-    they fit the device together, so the HIP library is told how many processes share it
+    """Ranks that map onto one physical GPU (a rehearsal: two ranks on one card) each run
+    persistent sweeps on it at once.  Their grids are only co-resident if they fit the device
+    together, so the HIP library is told how many processes share it
     (samplernn_hip.set_device_share): launches are then sized to 1/share of the CUs or take
     the per-step kernels -- declared up front instead of a sweep waiting on CUs that another
-    process's sweep holds."""
+    process's sweep holds.  The share is counted from the real device mapping: every rank's
+    (host, PCI address, UUID) is all-gathered once at init and this rank counts the ranks
+    naming its own card -- correct for per-rank *_VISIBLE_DEVICES isolation (each process
+    sees one device 0), for launchers that set no LOCAL_WORLD_SIZE (srun / mpirun) and for
+    several nodes.  SRNN_DEVICE_SHARE overrides."""
     n = torch.cuda.device_count()
     if n <= 0:
         return 1
-    lws = int(os.environ.get('LOCAL_WORLD_SIZE', str(world())))
-    share = (lws + n - 1) // n
+    env = os.environ.get('SRNN_DEVICE_SHARE')
+    if env:
+        share = max(1, int(env))
+    elif dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        mine = device_key()
+        keys = [None] * dist.get_world_size()
+        dist.all_gather_object(keys, mine)
+        share = device_share(keys, mine)
+    else:
+        share = 1
     if share > 1:
         import warnings
         import samplernn_hip as H

@@ -132,6 +132,16 @@ class _Lib:
         self.dll = ctypes.CDLL(path)
         self.dll.srnn_last_error.restype = ctypes.c_char_p
         self.dll.srnn_last_error.argtypes = []
+        # the library must be built from the sources beside it: a stale .so that still has
+        # every symbol would otherwise run old kernels silently
+        self.dll.srnn_build_hash.restype = ctypes.c_char_p
+        self.dll.srnn_build_hash.argtypes = []
+        self.build_hash = self.dll.srnn_build_hash().decode()
+        want = csrc_hash()
+        if self.build_hash != want and os.environ.get('SRNN_ALLOW_STALE_LIB', '0') != '1':
+            raise ImportError('%s is stale: built from sources %s, the tree has %s -- rebuild '
+                              '(__graft_entry__.build() or make -C csrc)'
+                              % (path, self.build_hash, want))
         for name, args in _SIGS.items():
             fn = getattr(self.dll, name)
             fn.argtypes = args
@@ -186,7 +196,8 @@ def exported_symbols():
                             'srnn_gen_persistent_rows', 'srnn_gru_xcd_work_bytes',
                             'srnn_gru_xcd_bwd_work_bytes', 'srnn_gru_xcd_error',
                             'srnn_persistent_error_take', 'srnn_gemm_amax_taken',
-                            'srnn_gemm_csum_taken', 'srnn_blaslt_calls', 'srnn_device_share']
+                            'srnn_gemm_csum_taken', 'srnn_blaslt_calls', 'srnn_device_share',
+                            'srnn_build_hash', 'srnn_dtab_packed_ok']
 
 
 # Callbacks run just before a persistent sweep (gru_xcd / gru_seq) is enqueued.  Such a sweep
@@ -389,22 +400,17 @@ def gru_seq_supported(dtype, B, D):
 # ------------------------------------------------------------------ helpers
 def csrc_hash():
     """Content hash of the HIP sources the library is built from (csrc/*.hip, *.hpp, *.h,
-    *.cpp and the C-ABI header): 16 hex digits.  Profiles record it, so a committed counter
-    pass is only attributed to the kernels it measured (bench.py's roofline.traffic)."""
-    import hashlib
+    *.cpp and the C-ABI header): 16 hex digits (csrc/srchash.py, which the Makefile also
+    compiles into the library as srnn_build_hash()).  Profiles record it, so a committed
+    counter pass is only attributed to the kernels it measured (bench.py's roofline.traffic),
+    and lib() refuses a library built from other sources."""
+    import importlib.util
     here = os.path.dirname(os.path.abspath(__file__))
-    csrc = os.path.join(here, 'csrc')
-    files = sorted(f for f in os.listdir(csrc) if f.endswith(('.hip', '.hpp', '.h', '.cpp')))
-    h = hashlib.sha256()
-    for f in files:
-        h.update(f.encode())
-        with open(os.path.join(csrc, f), 'rb') as fh:
-            h.update(fh.read())
-    hdr = os.path.join(os.path.dirname(here), 'include', 'samplernn_hip.h')
-    if os.path.exists(hdr):
-        with open(hdr, 'rb') as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
+    spec = importlib.util.spec_from_file_location('_srnn_srchash',
+                                                  os.path.join(here, 'csrc', 'srchash.py'))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod.csrc_hash(os.path.join(here, 'csrc'))
 
 
 def ptr(t):

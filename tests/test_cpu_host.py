@@ -29,6 +29,25 @@ def test_library_exports_every_header_symbol():
     assert lib.dll.srnn_abi_version() == 1
 
 
+def test_library_build_hash_matches_tree():
+    """The library carries the hash of the sources it was built from (srnn_build_hash) and
+    it equals the tree's (verdict r05 #7: a stale .so is refused at load)."""
+    import samplernn_hip as H
+    lib = H.lib()
+    assert lib.build_hash == H.csrc_hash()
+    assert len(lib.build_hash) == 16
+
+
+def test_stale_library_is_refused(monkeypatch):
+    import samplernn_hip as H
+    monkeypatch.setattr(H, 'csrc_hash', lambda: '0123456789abcdef')
+    monkeypatch.delenv('SRNN_ALLOW_STALE_LIB', raising=False)
+    with pytest.raises(ImportError, match='stale'):
+        H._Lib(H.LIB_PATH)
+    monkeypatch.setenv('SRNN_ALLOW_STALE_LIB', '1')
+    H._Lib(H.LIB_PATH)                      # explicit override only
+
+
 def test_no_torch_types_in_header():
     txt = open(os.path.join(ROOT, 'include', 'samplernn_hip.h')).read()
     assert 'torch' not in txt.lower().replace('torch.nn', '').replace('torch>', '') or True

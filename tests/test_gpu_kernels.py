@@ -1407,7 +1407,11 @@ def test_mlp_l1_bits_grouped(hip, B, Tl, D, monkeypatch):
 
 @pytest.mark.parametrize('M,N,K,amax', [(32768, 1024, 1024, True), (32768, 1024, 1024, False),
                                         (8192, 512, 192, True), (1024, 256, 128, True),
-                                        (200, 128, 96, False)])
+                                        (200, 128, 96, False),
+                                        # K = 64 (one k-chunk per tile) with 2 tiles per
+                                        # workgroup: the expanded fallback
+                                        (131072, 256, 64, True), (131072, 256, 64, False),
+                                        (131072, 256, 128, True)])
 def test_gemm_mask_bits_grouped(hip, M, N, K, amax):
     """The grouped mask bits (the da1 GEMM's operand: staged by LDS-DMA in the bf16 pair-mode
     kernel, expanded to a mask on the other paths) == the bf16 mask tensor, bit for bit, with
@@ -1436,7 +1440,7 @@ def test_gemm_mask_bits_grouped(hip, M, N, K, amax):
         assert res[0][1] == res[1][1]
         ref = res[0][0].float().abs().max().item()
         assert res[1][1] == int(np.float32(ref).view(np.int32))
-    if M * N >= 32768 * 1024:
+    if M * N >= 32768 * 1024 and K >= 128:
         assert res[1][2] == 1 or not amax                   # the LDS-staged kernel took it
     o3 = hip.gemm(A, W, transB=True, mask_bits=bits)       # fp32 out: the expanded fallback
     o4 = hip.gemm(A, W, transB=True, mask=act)
