@@ -1,0 +1,85 @@
+"""gemm3e (the 8-phase ping-pong NT kernel, csrc/gemm3.hip) == the pair-mode gemm3p kernel bit
+for bit: the same MFMA k order per output fragment, so switching kernels must not change a
+single output bit (bf16 / fp32 outputs, bias, ReLU, ReLU bits out, alpha), for one tile, one
+round of tiles, several tiles per workgroup and a ragged last round.  Both are also held to a
+torch fp32 reference.  These are the GEMMs of model.py:287-301 (SampleLevelMLP layers) and
+nn.py:33-43 (LearnedUpsampling1d) in their forward NT layout."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+def _rand(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(*shape, generator=g) * 2 - 1
+
+
+SHAPES = [(256, 256, 128), (512, 768, 192), (8192, 512, 1024), (65536, 1024, 256),
+          (256 * 37, 256 * 9, 320), (4096, 3072, 128)]
+
+
+def _run(hip, monkeypatch, g3e, a, w, **kw):
+    monkeypatch.setenv('SRNN_BLASLT', '0')
+    monkeypatch.setenv('SRNN_G3E', '1' if g3e else '0')
+    out = hip.gemm(a, w, transB=True, **kw)
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize('M,N,K', SHAPES)
+@pytest.mark.parametrize('kind', ['bf16_bias_relu_bits', 'bf16_plain', 'fp32_bias', 'bf16_alpha'])
+def test_gemm3e_equals_pair_mode(hip, monkeypatch, M, N, K, kind):
+    bf = torch.bfloat16
+    a = _rand(M, K, seed=1).to(DEV, bf)
+    w = _rand(N, K, seed=2).to(DEV, bf)
+    bias = (_rand(N, seed=3) * 0.5).to(DEV)
+    kw = {}
+    if kind == 'bf16_bias_relu_bits':
+        kw = dict(out_dtype=bf, bias=bias, relu=True)
+    elif kind == 'bf16_plain':
+        kw = dict(out_dtype=bf)
+    elif kind == 'fp32_bias':
+        kw = dict(out_dtype=torch.float32, bias=bias)
+    else:
+        kw = dict(out_dtype=bf, alpha=0.37, bias=bias)
+    res = []
+    for g3e in (False, True):
+        bits = hip.relu_bits(M, N, DEV) if kind == 'bf16_bias_relu_bits' else None
+        o = _run(hip, monkeypatch, g3e, a, w, bits_out=bits, **kw)
+        res.append((o, bits))
+    assert torch.equal(res[0][0], res[1][0])
+    if res[0][1] is not None:
+        assert torch.equal(res[0][1], res[1][1])
+    # both against a torch fp32 product (a sample of rows for the big shapes)
+    rows = torch.arange(0, M, max(1, M // 512), device=DEV)
+    ref = a[rows].float() @ w.float().t()
+    ref = ref * kw.get('alpha', 1.0)
+    if 'bias' in kw:
+        ref = ref + bias
+    if kw.get('relu'):
+        ref = ref.clamp_min(0)
+    tol = 2e-3 * np.sqrt(K) + (0.02 if kw['out_dtype'] == bf else 0.0) * ref.abs().max().item()
+    torch.testing.assert_close(res[1][0][rows].float(), ref, atol=tol, rtol=1e-2)
+    if res[1][1] is not None:
+        # the bits are those of the stored bf16 values (> 0)
+        st = res[1][0][rows].float() > 0
+        bits = res[1][1][rows].to(torch.int32) & 0xffff
+        cols = torch.arange(N, device=DEV)
+        got = ((bits[:, cols // 16] >> (cols % 16)) & 1).bool()
+        assert torch.equal(got, st)
+
+
+def test_gemm3e_k64_takes_pair_mode(hip, monkeypatch):
+    """K = 64 (one k-tile per output tile) is not admitted to gemm3e (its bias buffers need
+    two k-tiles per tile): the call runs on the pair mode and matches it."""
+    bf = torch.bfloat16
+    a = _rand(4096, 64, seed=4).to(DEV, bf)
+    w = _rand(512, 64, seed=5).to(DEV, bf)
+    bias = _rand(512, seed=6).to(DEV)
+    o0 = _run(hip, monkeypatch, False, a, w, out_dtype=bf, bias=bias, relu=True)
+    o1 = _run(hip, monkeypatch, True, a, w, out_dtype=bf, bias=bias, relu=True)
+    assert torch.equal(o0, o1)
