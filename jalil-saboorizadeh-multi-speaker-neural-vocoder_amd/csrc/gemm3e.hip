@@ -206,40 +206,54 @@ __global__ __launch_bounds__(512, 1) void gemm3e_kernel(Gemm3Args g) {
 
     // DMA cursor: the k-tile (unit iu, k-step kti) whose pieces are issued next.  This wave
     // issues pieces wave * 4 .. + 3 of each operand (rows 32 wave .. + 31 of the k-tile image)
-    // (pieces c and c + 2 differ by 16 rows, which keeps the row swizzle ((row >> 1) & 7):
-    // two per-lane pointers per operand cover the four)
+    // as buffer loads to LDS: the per-lane byte offset (row within the tile, swizzled 16-B
+    // slot) does not depend on the tile, the tile's row / k offset is a scalar soffset -- one
+    // VGPR per piece pair instead of 64-bit pointers (register pressure here spilled, and a
+    // spill reload's vmcnt(0) drains the DMA queue).  Pieces c and c + 2 are 16 rows apart,
+    // which keeps the row swizzle ((row >> 1) & 7)
     int iu = 0, kti = 0;
-    const bf16* srcA[2];
-    const bf16* srcB[2];
-    const float* srcb = nullptr;
+    const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16*>(A), (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16*>(B), (short)0, 0x7fffffff, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(g.bias), (short)0, 0x7fffffff, 0x00020000);
+    unsigned voA[2], voB[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        const int row = (wave * 4 + i) * 8 + (lane >> 3);
+        const int slot = (lane & 7) ^ ((row >> 1) & 7);
+        voA[i] = (unsigned)(((int64_t)row * g.lda + slot * 8) * 2);
+        voB[i] = (unsigned)(((int64_t)row * g.ldb + slot * 8) * 2);
+    }
+    const unsigned vob = (unsigned)((wn * 64 + lane) * 4);
+    unsigned soA = 0, soB = 0, sob = 0;            // the current unit's scalar offsets
     auto set_src = [&]() {
         int m0, n0;
         unit(iu, m0, n0);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            srcA[i] = g3p_src<true>(A, g.lda, m0, 0, wave * 4 + i, lane);
-            srcB[i] = g3p_src<true>(B, g.ldb, n0, 0, wave * 4 + i, lane);
-        }
-        if (hasb) srcb = g.bias + n0 + wn * 64 + lane;
+        soA = (unsigned)((int64_t)m0 * g.lda * 2);
+        soB = (unsigned)((int64_t)n0 * g.ldb * 2);
+        sob = (unsigned)(n0 * 4);
     };
     set_src();
-    const int64_t stepA = (int64_t)16 * g.lda, stepB = (int64_t)16 * g.ldb;
-    auto issue_op = [&](const bf16* const (&src)[2], int64_t step, char* img) {
-        const int64_t ko = (int64_t)kti * g3p::BK;
+    const unsigned stA = (unsigned)(16 * g.lda * 2), stB = (unsigned)(16 * g.ldb * 2);
+    auto issue_op = [&](const __amdgpu_buffer_rsrc_t& rs, const unsigned (&vo)[2], unsigned so,
+                        unsigned st, char* img) {
+        const unsigned s0 = so + (unsigned)(kti * g3p::BK * 2);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_global_load_lds(G3_GLB(src[i & 1] + ko + (i >> 1) * step),
-                                             G3_LDS(img + (wave * 4 + i) * 1024), 16, 0, 0);
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rs, G3_LDS(img + (wave * 4 + i) * 1024), 16, vo[i & 1], s0 + (i >> 1) * st, 0, 0);
     };
-    // the B pieces, the tile's bias slice with its first k-tile; returns the DMAs issued
-    auto issue_b = [&](char* img) -> int {
-        issue_op(srcB, stepB, img + g3p::OPB);
-        int n = 4;
+    // one k-tile's pieces (+ with a tile's first k-tile its bias slice); returns the DMAs
+    auto issue_kt = [&](char* slot) -> int {
+        issue_op(rsA, voA, soA, stA, slot);
+        issue_op(rsB, voB, soB, stB, slot + g3p::OPB);
+        int n = 8;
         if (hasb && kti == 0) {
-            __builtin_amdgcn_global_load_lds(G3_GLB(srcb),
-                                             G3_LDS(smem + g3p::LDS + (iu & 1) * 2048 + wave * 256),
-                                             4, 0, 0);
-            n = 5;
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                rsb, G3_LDS(smem + g3p::LDS + (iu & 1) * 2048 + wave * 256), 4, vob, sob, 0, 0);
+            n = 9;
         }
         if (++kti == nk) {
             kti = 0;
@@ -248,14 +262,10 @@ __global__ __launch_bounds__(512, 1) void gemm3e_kernel(Gemm3Args g) {
         return n;
     };
     // prologue: k-tiles 0 and 1 in flight, k-tile 0 landed
-    if (S > 0) {
-        issue_op(srcA, stepA, smem);
-        issue_b(smem);
-    }
+    if (S > 0) (void)issue_kt(smem);
     if (S > 1) {
-        issue_op(srcA, stepA, smem + g3p::SLOT);
-        const int nb = issue_b(smem + g3p::SLOT);
-        g3e_wait_vm(4 + nb);
+        const int n1 = issue_kt(smem + g3p::SLOT);
+        g3e_wait_vm(n1);
     } else {
         g3_wait_vm<0>();
     }
@@ -272,7 +282,6 @@ __global__ __launch_bounds__(512, 1) void gemm3e_kernel(Gemm3Args g) {
     for (int u = 0; u < 2; ++u)
         lb[u] = (unsigned)((lane & 15) * 128 + (((u * 4 + (lane >> 4)) ^ ((lane >> 1) & 7)) * 16));
     int ic = 0, ktc = 0;                           // the k-tile being computed
-    int epi = 0;                                   // stores of the epilogue run this k-tile
     auto seg_end = [&]() {
         __builtin_amdgcn_sched_barrier(0);
         __builtin_amdgcn_s_barrier();
@@ -294,9 +303,15 @@ __global__ __launch_bounds__(512, 1) void gemm3e_kernel(Gemm3Args g) {
     auto bias_lds = [&](int i) -> unsigned {
         return hasb ? sm0 + (unsigned)(g3p::LDS + (i & 1) * 2048 + wave * 256) : ~0u;
     };
+    // segment order per k-tile s (Y one segment behind X; the reads of a segment complete
+    // during the barrier that closes it, their lgkmcnt wait opens the MFMA segment):
+    //   R0: the finished tile's epilogue, reads m 0-3 / n 0-1 | M0
+    //   R1: reads m 4-7 / n 2-3 | M1          R2: - | M2
+    //   R3: the pieces of k-tile s + 2 into k-tile s's slot (its reads retired >= 2 segments
+    //       ago); wait for k-tile s + 1 (younger: the epilogue's stores, k-tile s + 2) | M3
     for (int s = 0; s < S; ++s) {
-        char* wimg = smem + (s & 1) * g3p::SLOT;       // k-tile s + 2's slot = this one
-        // ---- R0: the finished tile's epilogue, then m 0-3 / n 0-1 of this k-tile
+        int epi = 0;
+        // ---- R0
         if (ktc == 0 && s > 0) {
             int m0, n0;
             unit(ic - 1, m0, n0);
@@ -316,29 +331,26 @@ __global__ __launch_bounds__(512, 1) void gemm3e_kernel(Gemm3Args g) {
                      :                                                                        \
                      : "memory");
         G3E_RD_B(0) G3E_RD_B(1) G3E_RD_A(0) G3E_RD_A(1) G3E_RD_A(2) G3E_RD_A(3)
-        G3E_WAIT(0, 0)
         seg_end();
+        G3E_WAIT(0, 0)
+        __builtin_amdgcn_sched_barrier(0);
         quad(0, 0);                                    // M0
-        // ---- R1: m 4-7 / n 2-3
+        // ---- R1
         G3E_RD_B(2) G3E_RD_B(3) G3E_RD_A(4) G3E_RD_A(5) G3E_RD_A(6) G3E_RD_A(7)
+        seg_end();
         G3E_WAIT(4, 2)
+        __builtin_amdgcn_sched_barrier(0);
 #undef G3E_RD_A
 #undef G3E_RD_B
 #undef G3E_WAIT
-        seg_end();
         quad(0, 2);                                    // M1
-        // ---- R2: A pieces of k-tile s + 2 into this slot (every wave's reads of it are done)
-        const bool more = s + 2 < S;
-        if (more) issue_op(srcA, stepA, wimg);
+        // ---- R2
         seg_end();
         quad(4, 2);                                    // M2
-        // ---- R3: B pieces of k-tile s + 2 (+ a bias slice); wait for k-tile s + 1 (this
-        // wave's pieces of it and everything older: younger are s + 2's pieces and this
-        // k-tile's epilogue stores)
-        int nb = 0;
-        if (more) nb = issue_b(wimg);
-        if (s + 1 < S) g3e_wait_vm((more ? 4 + nb : 0) + epi);
-        epi = 0;
+        // ---- R3
+        int nis = 0;
+        if (s + 2 < S) nis = issue_kt(smem + (s & 1) * g3p::SLOT);
+        if (s + 1 < S) g3e_wait_vm(epi + nis);
         seg_end();
         quad(4, 0);                                    // M3
         if (++ktc == nk) {
@@ -356,6 +368,9 @@ __global__ __launch_bounds__(512, 1) void gemm3e_kernel(Gemm3Args g) {
 
 
 int srnn_gemm3e_launch(const Gemm3Args& g, bool out_f32, int ncu, hipStream_t s) {
+    // (buffer-load DMA: every operand byte offset below 2^31)
+    if ((int64_t)g.M * g.lda * 2 >= (1ll << 31) || (int64_t)g.N * g.ldb * 2 >= (1ll << 31))
+        return -1;
     if (g.ksplit != 1 || g.amax || g.csp || g.mbi || g.mask || g.blk || g.beta != 0.f ||
         g.bias_mode == 2 || (g.mbo && out_f32) || g.K % g3p::BK || g.K < 2 * g3p::BK || g.diag)
         return -1;
