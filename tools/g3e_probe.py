@@ -39,7 +39,13 @@ shapes = [('hid_fwd', M, 1024, 1024, bf, True, True, True),
           ('up_fwd', M // 16, 16384, 1024, bf, True, False, False),
           ('out_fwd', M, 256, 1024, torch.float32, True, False, False),
           ('gi_fwd', M // 16, 3072, 1024, torch.float32, True, False, False),
-          ('plain_bf16', M // 4, 1024, 1024, bf, False, False, False)]
+          ('plain_bf16', M // 4, 1024, 1024, bf, False, False, False),
+          # the da2 GEMM's shape (K = Q = 256: 4 k-tiles per output tile, epilogue-heavy)
+          ('k256_bf16', M, 1024, 256, bf, False, False, False),
+          ('k256_bits', M, 1024, 256, bf, True, True, True)]
+ONLY = [x for x in os.environ.get('ONLY', '').split(',') if x]
+if ONLY:
+    shapes = [sh for sh in shapes if sh[0] in ONLY]
 g = torch.Generator(device='cuda').manual_seed(5)
 res = {}
 for name, m, n, k, od, hb, relu, bo in shapes:
