@@ -233,6 +233,14 @@ int srnn_gemm_amax_blk_next(unsigned* amax, void* blk);
  * GEMM did since (host state; also clears a request no GEMM took).                        */
 int srnn_gemm_csum_next(float* part);
 int srnn_gemm_csum_taken(void);
+/* Ask the next fp32-output NT GEMM with N = 256 (one 256-column tile: whole rows) that runs
+ * on the gemm3 pair path -- the SampleLevelMLP's logits, model.py:324 -- to write
+ * log_softmax of every output row (model.py:325) instead of the row: logp = (v - max) -
+ * log(sum exp(v - max)), v = alpha A B^T + bias, the logsoftmax_nll arithmetic.
+ * srnn_gemm_logsoftmax_taken() returns 1 if a GEMM did since (host state; also clears a
+ * request no GEMM took).                                                              */
+int srnn_gemm_logsoftmax_next(void);
+int srnn_gemm_logsoftmax_taken(void);
 /* srnn_mlp_dtab3 with blk (device, may be NULL): the column-blocked copy of da
  * (blk[D / 4][B * Tlen][4], srnn_gemm_amax_blk_next) the packed form reads instead of da
  * (whole 128-B lines per load).  Same outputs bit for bit.  A sample histogram skewed past

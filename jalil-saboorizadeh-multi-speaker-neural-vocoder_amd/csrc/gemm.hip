@@ -542,7 +542,8 @@ static int gemm_core(int dtype, int out_dtype, int transA, int transB, int M, in
     }
     // large plain bf16 problems: hipBLASLt (blaslt.cpp) unless a fused epilogue or a pending
     // max |C| / column-sum request needs gemm3
-    if (tile < 0 && batch == 1 && !mask && !srnn_gemm_amax_pending() && !srnn_gemm_csum_pending()) {
+    if (tile < 0 && batch == 1 && !mask && !srnn_gemm_amax_pending() && !srnn_gemm_csum_pending() &&
+        !srnn_gemm_lsm_pending()) {
         int rc = srnn_blaslt_try(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, B, ldb,
                                  beta, C, ldc, bias, bias_mode, relu, s);
         if (rc >= 0) return rc;

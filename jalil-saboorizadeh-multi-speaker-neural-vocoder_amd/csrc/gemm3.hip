@@ -614,11 +614,88 @@ __global__ __launch_bounds__(512, 1) void gemm3_kernel(Gemm3Args g) {
 }
 
 // ---------------------------------------------------------------------------------
+// Log-softmax epilogue (g.lsm; fp32 out, N = 256, so a tile holds whole rows): logp =
+// (v - max) - log(sum exp(v - max)) per row with v = alpha acc + bias, the same arithmetic as
+// logsoftmax_nll_kernel (mlp.hip), so the (B T, Q) logits never round-trip through HBM
+// (model.py:324-325).  A row's 256 columns live in the 4 waves of equal wm (64 each): the
+// per-wave row maxima, then the per-wave sums of exp, meet in LDS (red: [2][2 wm][4 wn][128]
+// floats) across two raw barriers every wave of the workgroup takes.  Returns the stores (32).
+__device__ __forceinline__ int g3_epilogue_lsm(const Gemm3Args& g, floatx4 (&acc)[8][4], int m0,
+                                               int n0, int wm, int wn, int lane, float* red) {
+    const int rl = lane & 15;
+    const int rbase = m0 + wm * 128 + rl;
+    const int cbase = n0 + wn * 64 + (lane >> 4) * 4;
+    floatx4 bcol[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        bcol[j] = g.bias ? *reinterpret_cast<const floatx4*>(g.bias + cbase + j * 16)
+                         : floatx4{0.f, 0.f, 0.f, 0.f};
+    float mx[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        float m = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            acc[i][j] = acc[i][j] * g.alpha + bcol[j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) m = fmaxf(m, acc[i][j][e]);
+        }
+        m = fmaxf(m, __shfl_xor(m, 16));
+        m = fmaxf(m, __shfl_xor(m, 32));
+        mx[i] = m;
+    }
+    float* rmax = red + (wm * 4) * 128;            // [wn][128] for this wm
+    float* rsum = red + (8 + wm * 4) * 128;
+    if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rmax[wn * 128 + i * 16 + rl] = mx[i];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    float sm[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int r = i * 16 + rl;
+        const float m = fmaxf(fmaxf(rmax[r], rmax[128 + r]), fmaxf(rmax[256 + r], rmax[384 + r]));
+        mx[i] = m;
+        float sv = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) sv += expf(acc[i][j][e] - m);
+        sv += __shfl_xor(sv, 16);
+        sv += __shfl_xor(sv, 32);
+        sm[i] = sv;
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) rsum[wn * 128 + i * 16 + rl] = sm[i];
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    float* Cf = reinterpret_cast<float*>(g.C);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const int r = i * 16 + rl;
+        const float ls = logf(rsum[r] + rsum[128 + r] + rsum[256 + r] + rsum[384 + r]);
+        const float m = mx[i];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            floatx4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = (acc[i][j][e] - m) - ls;
+            acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+            *reinterpret_cast<floatx4*>(Cf + (int64_t)(rbase + i * 16) * g.ldc + cbase + j * 16) = o;
+        }
+    }
+    return 32;
+}
+
 // PF: the k-unit 1 fragments of a stage are read into a second register set while unit 0's
 // MFMAs run (3 reads after each of its last four MFMA rows), so the unit-1 MFMAs do not wait
 // for a burst of 12 LDS reads.
 template <typename TO, bool KCA, bool KCB, bool SW, int MB = 0, bool PF = false,
-          bool AMX = false, int CS = 0>
+          bool AMX = false, int CS = 0, int LS = 0>
 __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -739,9 +816,15 @@ __global__ __launch_bounds__(512, 1) void gemm3p_kernel(Gemm3Args g) {
             int m0, n0, kb;
             unit(ic, m0, n0, kb);
             const char* mbl = smem + g3p::LDS + (ic & 1) * 8192 + wave * 1024;
-            epi = (g.diag & 8) ? 0
-                               : g3_epilogue<TO, SW, MB, AMX, CS>(g, acc, m0, n0, wm, wn, lane, kb, mbl,
-                                                                  &amx_run);
+            if constexpr (LS) {
+                (void)mbl;
+                epi = g3_epilogue_lsm(g, acc, m0, n0, wm, wn, lane,
+                                      reinterpret_cast<float*>(smem + g3p::LDS));
+            } else {
+                epi = (g.diag & 8) ? 0
+                                   : g3_epilogue<TO, SW, MB, AMX, CS>(g, acc, m0, n0, wm, wn, lane,
+                                                                      kb, mbl, &amx_run);
+            }
             ktc = 0;
             ++ic;
         }
@@ -1249,9 +1332,18 @@ static int launch3(const Gemm3Args& g, hipStream_t s) {
             ki = amx_pf ? 10 : 9;
         }
     }
+    if constexpr (sizeof(TO) == 4 && SW && KCA && KCB) {
+        if (g.lsm) {                 // row log-softmax in the epilogue (srnn_gemm_logsoftmax_next)
+            SRNN_REQUIRE(pair && g.N == g3::BN && g.ksplit == 1,
+                         "gemm3: the log-softmax epilogue needs one pair-mode tile column");
+            k = gemm3p_kernel<TO, KCA, KCB, SW, 0, false, false, 0, 1>;
+            ki = 16;
+        }
+    }
     SRNN_REQUIRE(!g.csp || pair, "gemm3: column sums need the pair-mode kernel");
-    const int lds = (pp || pair) ? g3p::LDS + (grouped ? 16 * 1024 : 0) : g3::LDS;
-    static bool attr[16] = {};
+    const int lds = (pp || pair) ? g3p::LDS + (grouped ? 16 * 1024 : g.lsm ? 8 * 1024 : 0)
+                                 : g3::LDS;
+    static bool attr[24] = {};
     if (!attr[ki]) {
         SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds));
@@ -1340,6 +1432,32 @@ extern "C" int srnn_gemm_csum_next(float* part) {
     return 0;
 }
 
+// log-softmax request for the next fp32-output NT GEMM with N = 256 that takes the gemm3
+// pair path (the SampleLevelMLP's logits)
+static int& g3_lsm_pending() {
+    static int p = 0;
+    return p;
+}
+static int& g3_lsm_taken() {
+    static int t = 0;
+    return t;
+}
+
+int srnn_gemm_lsm_pending() { return g3_lsm_pending(); }
+
+extern "C" int srnn_gemm_logsoftmax_next(void) {
+    g3_lsm_pending() = 1;
+    g3_lsm_taken() = 0;
+    return 0;
+}
+
+extern "C" int srnn_gemm_logsoftmax_taken(void) {
+    const int t = g3_lsm_taken();
+    g3_lsm_pending() = 0;
+    g3_lsm_taken() = 0;
+    return t;
+}
+
 extern "C" int srnn_gemm_csum_taken(void) {
     const int t = g3_csum_taken();
     g3_csum_pending() = nullptr;
@@ -1394,6 +1512,7 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
     g.amax = nullptr;
     g.blk = nullptr;
     g.csp = nullptr;
+    g.lsm = 0;
     const int tiles = (M / g3::BM) * (N / g3::BN);
     const bool plain = beta == 0.f && !bias && !relu && !mask && !mbi && !mbo &&
                        out_dtype == SRNN_F32;
@@ -1426,7 +1545,16 @@ int srnn_gemm3_try(int dtype, int out_dtype, int transA, int transB, int M, int 
         if (rc || !g.part) return rc;
         return srnn_splitk_sum((const float*)g.part, (float*)C, ldc, M, N, ks, s);
     }
-    if (out_dtype == SRNN_F32) return launch3_layout<float, true>(g, kca, kcb, s);
+    if (out_dtype == SRNN_F32) {
+        if (g3_lsm_pending() && N == g3::BN && g.ksplit == 1 && beta == 0.f && !mask && !mbi && !mbo &&
+            (!bias || bias_mode == 1) && kca && kcb && K % g3p::BK == 0 &&
+            (g3_mode() == 1 || g3_mode() == 2)) {
+            g.lsm = 1;
+            g3_lsm_pending() = 0;
+            g3_lsm_taken() = 1;
+        }
+        return launch3_layout<float, true>(g, kca, kcb, s);
+    }
     // max |C| (srnn_gemm_amax_next): computed by the pair-mode kernels (an operand
     // k-contiguous, K a multiple of 64, no bit masks) -- the request is taken only then
     if (g3_amax_pending() && beta == 0.f && (!mbi || ldmbi == 0) && !mbo && (kca || kcb) &&

@@ -40,6 +40,10 @@ struct Gemm3Args {
     // block, csp[M / 128][N] fp32 (each entry written once; the caller sums the blocks) --
     // the bias gradient of the layer whose output gradient this GEMM produces
     float* csp;
+    // optional (srnn_gemm_logsoftmax_next; fp32 out, N = 256 = one tile column): the epilogue
+    // writes log_softmax of every output row (the SampleLevelMLP's logits, model.py:324-325)
+    // instead of the row itself
+    int lsm;
 };
 
 namespace g3 {

@@ -72,3 +72,4 @@ int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int
 int srnn_gemm_amax_pending();
 // gemm3.hip: a column-sum request (srnn_gemm_csum_next) waits for the next bf16 gemm3 launch
 int srnn_gemm_csum_pending();
+int srnn_gemm_lsm_pending();

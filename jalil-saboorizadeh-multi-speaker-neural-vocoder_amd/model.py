@@ -34,7 +34,7 @@ import samplernn_hip as H
 
 verbose = False
 # (tests) how often a fused side result was consumed, and which recurrence kernels ran
-_STATS = {'fused_colsum': 0, 'fused_lp': 0, 'csum_epi': 0, 'gru_xcd_fwd': 0, 'gru_xcd_bwd': 0, 'gru_seq': 0,
+_STATS = {'fused_colsum': 0, 'fused_lp': 0, 'csum_epi': 0, 'lsm_epi': 0, 'gru_xcd_fwd': 0, 'gru_xcd_bwd': 0, 'gru_seq': 0,
           'gru_cell_steps': 0, 'gru_cell_bwd_steps': 0}
 
 
@@ -705,10 +705,20 @@ def mlp_forward(mlp, x, upper, ps):
     ev = H.roof_begin()
     a2 = H.linear(a1, W_hid, bias=mlp.hidden.bias, relu=True, out_dtype=T, bits_out=m2)
     H.roof_end('mlp_hidden_gemm', ev, 2.0 * B * Tl * D * D)
+    # bf16: the logits GEMM's epilogue applies the row log-softmax itself (its 256-column
+    # tiles hold whole rows), so the (B T, Q) fp32 logits never round-trip through HBM
+    # (SRNN_LSM_EPI=0: the separate logsoftmax pass)
+    lsm = T == torch.bfloat16 and Q == 256 and os.environ.get('SRNN_LSM_EPI', '1') != '0'
+    if lsm:
+        H.lib().dll.srnn_gemm_logsoftmax_next()
     z = H.linear(a2, W_out, bias=mlp.output.bias)                    # (B*T, Q) fp32
-    logp = torch.empty((B * Tl, Q), device=dev, dtype=torch.float32)
-    H.lib().call('srnn_logsoftmax_nll', H.ptr(z), Q, None, 0, Tl, B * Tl, Q, None,
-                 H.ptr(logp), Q, None, H.F32, 0, 0.0, H.stream())
+    if lsm and H.lib().dll.srnn_gemm_logsoftmax_taken():
+        logp = z
+        _STATS['lsm_epi'] += 1
+    else:
+        logp = torch.empty((B * Tl, Q), device=dev, dtype=torch.float32)
+        H.lib().call('srnn_logsoftmax_nll', H.ptr(z), Q, None, 0, Tl, B * Tl, Q, None,
+                     H.ptr(logp), Q, None, H.F32, 0, 0.0, H.stream())
     ctx = _State()
     ctx.mlp = mlp
     ctx.T = T

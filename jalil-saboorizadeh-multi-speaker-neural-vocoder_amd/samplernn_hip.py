@@ -150,6 +150,7 @@ class _Lib:
         # every pointer argument needs its declared type)
         for name, args in (('srnn_gru_xcd_error', [_P]), ('srnn_persistent_error_take', []),
                            ('srnn_gemm_amax_taken', []), ('srnn_gemm_csum_taken', []),
+                           ('srnn_gemm_logsoftmax_next', []), ('srnn_gemm_logsoftmax_taken', []),
                            ('srnn_blaslt_calls', [])):
             fn = getattr(self.dll, name)
             fn.argtypes = args
@@ -197,7 +198,8 @@ def exported_symbols():
                             'srnn_gru_xcd_bwd_work_bytes', 'srnn_gru_xcd_error',
                             'srnn_persistent_error_take', 'srnn_gemm_amax_taken',
                             'srnn_gemm_csum_taken', 'srnn_blaslt_calls', 'srnn_device_share',
-                            'srnn_build_hash', 'srnn_dtab_packed_ok']
+                            'srnn_build_hash', 'srnn_dtab_packed_ok', 'srnn_gemm_logsoftmax_next',
+                            'srnn_gemm_logsoftmax_taken']
 
 
 # Callbacks run just before a persistent sweep (gru_xcd / gru_seq) is enqueued.  Such a sweep

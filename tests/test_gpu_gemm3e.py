@@ -83,3 +83,46 @@ def test_gemm3e_k64_takes_pair_mode(hip, monkeypatch):
     o0 = _run(hip, monkeypatch, False, a, w, out_dtype=bf, bias=bias, relu=True)
     o1 = _run(hip, monkeypatch, True, a, w, out_dtype=bf, bias=bias, relu=True)
     assert torch.equal(o0, o1)
+
+
+@pytest.mark.parametrize('M', [32768, 131072])
+def test_logits_gemm_logsoftmax_epilogue(hip, M):
+    """srnn_gemm_logsoftmax_next: the logits GEMM (bf16 a2 (M, 1024) . W_out^T (256, 1024) +
+    bias, fp32 out) writes log_softmax of its rows (model.py:324-325) -- against torch's
+    log_softmax of the fp32 product and against the unfused path (fp32 logits, then
+    srnn_logsoftmax_nll); several tiles per workgroup at M = 131072."""
+    bf = torch.bfloat16
+    a = (_rand(M, 1024, seed=7) * 2).to(DEV, bf)
+    w = (_rand(256, 1024, seed=8) * 0.2).to(DEV, bf)
+    b = _rand(256, seed=9).to(DEV)
+    lib = hip.lib().dll
+    lib.srnn_gemm_logsoftmax_next()
+    lp = hip.linear(a, w, bias=b)
+    assert lib.srnn_gemm_logsoftmax_taken() == 1
+    z = hip.linear(a, w, bias=b)                              # plain logits (no request)
+    assert lib.srnn_gemm_logsoftmax_taken() == 0
+    lp2 = torch.empty_like(z)
+    hip.lib().call('srnn_logsoftmax_nll', hip.ptr(z), 256, None, 0, M, M, 256, None,
+                   hip.ptr(lp2), 256, None, hip.F32, 0, 0.0, hip.stream())
+    torch.cuda.synchronize()
+    rows = torch.arange(0, M, max(1, M // 1024), device=DEV)
+    ref = torch.log_softmax(a[rows].double() @ w.double().t() + b.double(), dim=1)
+    assert (lp[rows].double() - ref).abs().max().item() < 5e-5
+    assert (lp - lp2).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize('M', [300, 4096])
+def test_logsoftmax_request_not_taken_falls_back(hip, M):
+    """Shapes the epilogue does not take (M not a multiple of 256; too few 256-row tiles for
+    the gemm3 path): the request is not taken, the GEMM writes plain logits, and taken()
+    clears the request."""
+    bf = torch.bfloat16
+    a = _rand(M, 1024, seed=10).to(DEV, bf)
+    w = _rand(256, 1024, seed=11).to(DEV, bf)
+    lib = hip.lib().dll
+    lib.srnn_gemm_logsoftmax_next()
+    z = hip.linear(a, w)
+    assert lib.srnn_gemm_logsoftmax_taken() == 0
+    torch.cuda.synchronize()
+    ref = a.float() @ w.float().t()
+    torch.testing.assert_close(z, ref, atol=2e-3 * 32, rtol=1e-2)
