@@ -711,10 +711,12 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
             else __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         const float cdar = o.dar, cdaz = o.daz, cdghn = o.dghn, cdan = o.dan;
-        if (m + 1 < MT) fetch(t, m + 1, dyv, gr, gz, gn, gg, hp);
-        else if (t > 0) fetch(t - 1, 0, dyv, gr, gz, gn, gg, hp);
+        if (!(a.exp & 64)) {                       // (timing: SRNN_GX_EXP 64 skips the fetch)
+            if (m + 1 < MT) fetch(t, m + 1, dyv, gr, gz, gn, gg, hp);
+            else if (t > 0) fetch(t - 1, 0, dyv, gr, gz, gn, gg, hp);
+        }
         const int row = row_of(m);
-        if (rv && row < B) {
+        if (rv && row < B && !(a.exp & 1)) {     // (timing: SRNN_GX_EXP 1 skips the stores)
             const int64_t ob = (int64_t)row * a.ldd + (int64_t)t * a.sd;
             if (a.dgh) {
                 float* dg = a.dgh + ob;
