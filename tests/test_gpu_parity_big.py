@@ -157,8 +157,12 @@ def test_bf16_loss_trajectory_50_chunks(hip):
     set from the round-4 measurements on MI355X: max relative loss difference 2.7e-3 .. 5.7e-3
     (chunk 35 / 43, depending on the summation order of one bias gradient), mean 6.8e-4 ..
     9.3e-4, and the bf16 run's own one-ulp-perturbation sensitivity up to 5.1e-3
-    (profiles/r04_traj_50chunks.log) -- every chunk within 8e-3 relative of the fp32
-    trajectory, the mean below 1.5e-3, chunk 0 (no Adam step yet) within 1e-3; DESIGN §4."""
+    (profiles/r04_traj_50chunks.log).  Round 6 re-measured the envelope with the log-softmax
+    epilogue on and off and from two one-ulp weight perturbations (tools/traj_env.py,
+    profiles/r06_traj_envelope.txt): max 8.5e-3 (epilogue on), 5.7e-3 (off), 4.3e-3 and 8.9e-3
+    (perturbed), means 8.1e-4 .. 1.28e-3 -- a one-ulp change of the initial weights alone
+    reaches 8.9e-3, so the bound is 1.5e-2 on every chunk (1.7x the largest rounding-level
+    excursion), the mean below 1.5e-3, chunk 0 (no Adam step yet) within 1e-3; DESIGN §4."""
     import bench
     import nn as snn
     import optim
@@ -189,7 +193,7 @@ def test_bf16_loss_trajectory_50_chunks(hip):
           % (N, rel.max(), int(rel.argmax()), rel.mean(), b[0], b[-1], a[0], a[-1]))
     assert np.all(np.isfinite(a))
     assert rel[0] < 1e-3
-    assert rel.max() < 8e-3 and rel.mean() < 1.5e-3
+    assert rel.max() < 1.5e-2 and rel.mean() < 1.5e-3
 
 
 def test_persistent_fp32_long_teacher_forced(hip):
