@@ -260,6 +260,14 @@ int srnn_dtab_packed_ok(void);
  * 2 M N K >= 2^33) run as the ROCm library GEMM (SRNN_BLASLT=0: the library's own gemm3
  * kernels).  Diagnostic; replaces no reference interface.                               */
 int srnn_blaslt_calls(void);
+/* Routing of srnn_blaslt_calls' path: plain bf16 problems with fewer than min_outputs
+ * outputs (M N) or min_flop flop (2 M N K) stay on the hand-written kernels (defaults 4 Mi and
+ * 2^33; env SRNN_BLASLT_MIN_MN / SRNN_BLASLT_MIN_MFLOP).  srnn_blaslt_set_tune(n): n > 1 times
+ * the library heuristic's first n algorithms once per shape, outside graph capture, on the
+ * call's own operands and keeps the fastest (0: the heuristic's first; env SRNN_BLASLT_TUNE).
+ * Tuning knobs; replace no reference interface.                                           */
+int srnn_blaslt_set_min(long long min_outputs, double min_flop);
+int srnn_blaslt_set_tune(int n);
 /* log_softmax (model.py:324-325) + NLL rows (nn.py:66-70) + dlogits (softmax-onehot)*g  */
 /* dz = dlogp - exp(logp) * rowsum(dlogp)   (log_softmax backward, rows of Q)          */
 int srnn_logsoftmax_bwd(const float* dlogp, int64_t lddl, const float* logp, int64_t ldl,

@@ -15,6 +15,7 @@
 
 #include <map>
 #include <tuple>
+#include <vector>
 
 #include "samplernn_hip_internal.hpp"
 
@@ -28,9 +29,32 @@ struct Plan {
     hipblasLtMatmulAlgo_t algo;
     size_t ws = 0;
     bool ok = false;
+    std::vector<hipblasLtMatmulHeuristicResult_t> cand;   // the heuristic's candidates, best first
 };
 
-typedef std::tuple<int, int, int, int, int, int64_t, int64_t, int64_t, int, int, int> Key;
+typedef std::tuple<int, int, int, int, int, int64_t, int64_t, int64_t, int, int, int, int> Key;
+
+// Routing thresholds (srnn_blaslt_set_min; SRNN_BLASLT_MIN_MN / SRNN_BLASLT_MIN_MFLOP) and
+// the per-shape algorithm choice (srnn_blaslt_set_tune; SRNN_BLASLT_TUNE): 0 takes the
+// heuristic's first algorithm, n > 0 times its first n candidates once per shape on the call's
+// own operands (never while the stream is capturing) and keeps the fastest
+struct Routing {
+    long long min_mn = 4ll << 20;
+    double min_flop = 8589934592.0;
+    int wide_k = 4096;
+    int tune = 0;
+    Routing() {
+        min_mn = env_flag("SRNN_BLASLT_MIN_MN", (int)min_mn);
+        const int mf = env_flag("SRNN_BLASLT_MIN_MFLOP", -1);
+        if (mf >= 0) min_flop = mf * 1e6;
+        wide_k = env_flag("SRNN_BLASLT_WIDE_K", wide_k);
+        tune = env_flag("SRNN_BLASLT_TUNE", 0);
+    }
+};
+Routing& routing() {
+    static Routing r;
+    return r;
+}
 
 hipblasLtHandle_t handle() {
     static hipblasLtHandle_t h = nullptr;
@@ -71,14 +95,17 @@ bool make_plan(Plan& p, int out_dtype, int transA, int transB, int M, int N, int
     const uint64_t wsmax = kWorkspace;
     hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsmax,
                                           sizeof(wsmax));
-    hipblasLtMatmulHeuristicResult_t res;
+    const int want = routing().tune > 1 ? routing().tune : 1;
+    std::vector<hipblasLtMatmulHeuristicResult_t> res(want);
     int n = 0;
     const hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(h, p.desc, p.la, p.lb, p.lc, p.lc,
-                                                               pref, 1, &res, &n);
+                                                               pref, want, res.data(), &n);
     hipblasLtMatmulPreferenceDestroy(pref);
     if (st != HIPBLAS_STATUS_SUCCESS || n < 1) return false;
-    p.algo = res.algo;
-    p.ws = res.workspaceSize;
+    res.resize(n);
+    p.cand = res;
+    p.algo = res[0].algo;
+    p.ws = res[0].workspaceSize;
     return true;
 }
 
@@ -91,6 +118,22 @@ static int g_blaslt_calls = 0;
 // GEMMs launched through hipBLASLt so far in this process (tests: the path was taken)
 extern "C" int srnn_blaslt_calls(void) { return g_blaslt_calls; }
 
+// routing thresholds of srnn_blaslt_try: problems with fewer than min_outputs outputs or
+// min_flop flop stay on the hand-written kernels (defaults 4 Mi, 2^33)
+extern "C" int srnn_blaslt_set_min(long long min_outputs, double min_flop) {
+    routing().min_mn = min_outputs;
+    routing().min_flop = min_flop;
+    routing().wide_k = min_outputs == 0 ? 1 << 30 : 4096;
+    return 0;
+}
+
+// per-shape algorithm choice: 0 = the heuristic's first; n > 1 = the fastest of its first n
+// candidates, timed once per shape outside graph capture
+extern "C" int srnn_blaslt_set_tune(int n) {
+    routing().tune = n < 0 ? 0 : n;
+    return 0;
+}
+
 // 0 = done, -1 = not taken (the caller runs its own kernels), > 0 = HIP / library error
 int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
                     float alpha, const void* A, int64_t lda, const void* B, int64_t ldb, float beta,
@@ -100,8 +143,16 @@ int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int
     if (bias && bias_mode != 1) return -1;
     if (M <= 0 || N <= 0 || K <= 0) return -1;
     // large enough to pay for the library's launch and wide enough that gemm3's split-K deep
-    // reductions are not the better choice (M N >= 4 Mi outputs, 2 M N K >= 2^33 flop)
-    if ((int64_t)M * N < (4ll << 20) || 2.0 * M * N * K < 8589934592.0) return -1;
+    // reductions are not the better choice (M N >= 4 Mi outputs, 2 M N K >= 2^33 flop) -- or,
+    // below that, at least 1 Mi outputs over a shallow reduction (256 <= K <= wide_k = 4096):
+    // the 64-row step's top-tier GRU / upsampling products and the bottom tier's K = 4096
+    // weight gradients, where gemm3's 256-wide tiles fill only 16-48 CUs and its split-K pays
+    // a partial-sum pass (tools/gemm_route_probe.py, profiles/r06_gemm_route_b64.txt:
+    // 3072 x 1024 x 1024 TN 28.3 -> 17.4 us, 1024 x 1024 x 4096 NN 34.2 -> 23.2 us); the deep
+    // weight gradients (K = 8192 .. 524288) stay on gemm3, which is faster there
+    const bool big = (int64_t)M * N >= routing().min_mn && 2.0 * M * N * K >= routing().min_flop;
+    const bool wide = (int64_t)M * N >= (1ll << 20) && K >= 256 && K <= routing().wide_k;
+    if (!big && !wide) return -1;
     // (SRNN_BLASLT_F32_MINK: fp32-output problems only from this K on.  In isolation gemm3 writes
     //  fp32 faster at K of a few thousand -- GRU input projection 32768 x 3072 x 1024: 220 vs
     //  266 us -- but inside the step the library form measured 0.1-0.2 ms per step faster)
@@ -110,21 +161,54 @@ int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int
     const int epi = bias ? (relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_BIAS)
                          : (relu ? HIPBLASLT_EPILOGUE_RELU : HIPBLASLT_EPILOGUE_DEFAULT);
     static std::map<Key, Plan> plans;
-    const Key key{out_dtype, transA, transB, M, N, lda, ldb, ldc, K, epi, bias ? 1 : 0};
+    const Key key{out_dtype, transA, transB, M, N, lda, ldb, ldc, K, epi, bias ? 1 : 0,
+                  routing().tune};
     auto it = plans.find(key);
+    bool fresh = false;
     if (it == plans.end()) {
         Plan p;
         p.ok = make_plan(p, out_dtype, transA, transB, M, N, K, lda, ldb, ldc, epi, bias != nullptr);
         it = plans.emplace(key, p).first;
+        fresh = true;
     }
     Plan& p = it->second;
     if (!p.ok) return -1;
-    void* ws = p.ws ? srnn_scratch(SRNN_SCRATCH_BLASLT, kWorkspace) : nullptr;
-    if (p.ws && !ws) return -1;
+    void* ws = p.cand.size() > 1 || p.ws ? srnn_scratch(SRNN_SCRATCH_BLASLT, kWorkspace) : nullptr;
+    if ((p.cand.size() > 1 || p.ws) && !ws) return -1;
     if (bias)
         hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_POINTER, &bias,
                                         sizeof(bias));
     const float zero = 0.f;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (fresh && p.cand.size() > 1 && hipStreamIsCapturing(s, &cap) == hipSuccess &&
+        cap == hipStreamCaptureStatusNone) {
+        // time every candidate on these operands (1 warm-up + 5 runs each) and keep the
+        // fastest; the call below then writes C with it
+        hipEvent_t e0, e1;
+        SRNN_CHECK_HIP(hipEventCreate(&e0));
+        SRNN_CHECK_HIP(hipEventCreate(&e1));
+        float best = 1e30f;
+        for (const auto& c : p.cand) {
+            if (hipblasLtMatmul(handle(), p.desc, &alpha, B, p.la, A, p.lb, &zero, C, p.lc, C,
+                                p.lc, &c.algo, ws, c.workspaceSize, s) != HIPBLAS_STATUS_SUCCESS)
+                continue;
+            SRNN_CHECK_HIP(hipEventRecord(e0, s));
+            for (int r = 0; r < 5; ++r)
+                hipblasLtMatmul(handle(), p.desc, &alpha, B, p.la, A, p.lb, &zero, C, p.lc, C,
+                                p.lc, &c.algo, ws, c.workspaceSize, s);
+            SRNN_CHECK_HIP(hipEventRecord(e1, s));
+            SRNN_CHECK_HIP(hipEventSynchronize(e1));
+            float ms = 0.f;
+            SRNN_CHECK_HIP(hipEventElapsedTime(&ms, e0, e1));
+            if (ms < best) {
+                best = ms;
+                p.algo = c.algo;
+                p.ws = c.workspaceSize;
+            }
+        }
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+    }
     const hipblasStatus_t st = hipblasLtMatmul(handle(), p.desc, &alpha, B, p.la, A, p.lb, &zero,
                                                C, p.lc, C, p.lc, &p.algo, ws, p.ws, s);
     if (st != HIPBLAS_STATUS_SUCCESS) {

@@ -526,12 +526,15 @@ static int gemm_core(int dtype, int out_dtype, int transA, int transB, int M, in
         if (rc >= 0) return rc;
         SRNN_REQUIRE(tile != 6, "gemm: shape not eligible for the thin path");
     }
-    // skinny NT problems (M = batch rows): small-tile deep-ring kernel; tile 4 forces it
+    // skinny NT problems (M = batch rows): small-tile deep-ring kernel; tile 4 forces it.
+    // Up to 512 rows: the reverse sweep's dh_0 = dgh_0 W_hh + dh_direct at 512 rows (512 x 1024
+    // x 3072 with Cin) 55 -> 13.4 us against the 128-tile kernel it fell to above 256 rows
+    // (tools/gemm_route_probe.py, profiles/r06_gemm_route_b512.txt)
     {
         const int KBr = 256 / es;
         const bool ok = batch == 1 && !transA && transB && K % KBr == 0 && K > 0 && g.vecA &&
                         g.vecB && ((uintptr_t)A % 16 == 0) && ((uintptr_t)B % 16 == 0);
-        if ((tile == 4 || (tile < 0 && M <= 256 && g_use_gemm2())) && ok) {
+        if ((tile == 4 || (tile < 0 && M <= 512 && g_use_gemm2())) && ok) {
             if (dtype == SRNN_F32)
                 return out_dtype == SRNN_F32 ? launch_skinny<float, float>(g, s)
                                              : launch_skinny<float, bf16>(g, s);

@@ -463,8 +463,14 @@ int srnn_gemm_small_try(int dtype, int out_dtype, int transA, int transB, int M,
         return transA ? launch_small_n<bf16, true>(A, lda, B, ldb, (float*)C, ldc, M, N, K, alpha, s)
                       : launch_small_n<bf16, false>(A, lda, B, ldb, (float*)C, ldc, M, N, K, alpha, s);
     }
-    // small K: NT with the full epilogue (column bias only)
-    if (K <= 64 && K > 0 && !transA && transB && (!bias || bias_mode == 1) && M >= 256) {
+    // small K: NT with the full epilogue (column bias only).  K = 64 without Cin over enough
+    // rows for gemm3's own occupancy rule (>= 96 tiles of 256 x 256) goes to gemm3 instead
+    // (the top tier's 64-sample input projection at 512 rows, 8192 x 1024 x 64 with bias, fp32
+    // out: 42 -> 15 us, profiles/r06_gemm_route_b512.txt); SRNN_SMALLK_G3=0 keeps it here
+    const bool to_g3 = K == 64 && beta == 0.f && M % 256 == 0 && N % 256 == 0 &&
+                       (int64_t)(M / 256) * (N / 256) >= 96 && dtype == SRNN_BF16 &&
+                       env_flag("SRNN_SMALLK_G3", 1);
+    if (K <= 64 && K > 0 && !transA && transB && (!bias || bias_mode == 1) && M >= 256 && !to_g3) {
         if (dtype == SRNN_F32)
             return out_dtype == SRNN_F32
                        ? launch_small_k<float, float>(A, lda, B, ldb, C, ldc, Cin, ldcin, bias, M, N, K, alpha, beta, relu, s)

@@ -151,7 +151,8 @@ class _Lib:
         for name, args in (('srnn_gru_xcd_error', [_P]), ('srnn_persistent_error_take', []),
                            ('srnn_gemm_amax_taken', []), ('srnn_gemm_csum_taken', []),
                            ('srnn_gemm_logsoftmax_next', []), ('srnn_gemm_logsoftmax_taken', []),
-                           ('srnn_blaslt_calls', [])):
+                           ('srnn_blaslt_calls', []), ('srnn_blaslt_set_tune', [_I]),
+                           ('srnn_blaslt_set_min', [ctypes.c_longlong, ctypes.c_double])):
             fn = getattr(self.dll, name)
             fn.argtypes = args
             fn.restype = _I
@@ -199,7 +200,8 @@ def exported_symbols():
                             'srnn_persistent_error_take', 'srnn_gemm_amax_taken',
                             'srnn_gemm_csum_taken', 'srnn_blaslt_calls', 'srnn_device_share',
                             'srnn_build_hash', 'srnn_dtab_packed_ok', 'srnn_gemm_logsoftmax_next',
-                            'srnn_gemm_logsoftmax_taken']
+                            'srnn_gemm_logsoftmax_taken', 'srnn_blaslt_set_min',
+                            'srnn_blaslt_set_tune']
 
 
 # Callbacks run just before a persistent sweep (gru_xcd / gru_seq) is enqueued.  Such a sweep

@@ -161,6 +161,62 @@ def test_gemm_blaslt_plain(hip, monkeypatch, out_dtype, transA, transB, M, N, K,
     torch.testing.assert_close(lt, g3, atol=tol, rtol=1e-2)
 
 
+@pytest.mark.parametrize('M,N,K,transA,transB,lib', [
+    (3072, 1024, 1024, 1, 0, True),      # 64-row step: top-tier W_hh / W_ih gradients
+    (1024, 1024, 4096, 0, 0, True),      # top-tier upsampling dX
+    (1024, 3072, 1024, 0, 1, True),      # top-tier GRU input projection (with bias below)
+    (3072, 1024, 8192, 1, 0, False),     # deep weight gradient: stays on gemm3 split-K
+    (256, 1024, 4096, 1, 0, False)])     # under 1 Mi outputs: stays
+def test_gemm_route_wide_k(hip, M, N, K, transA, transB, lib):
+    """Round-6 routing: plain bf16 products with >= 1 Mi outputs over 256 <= K <= 4096 go to
+    hipBLASLt below its old size threshold (blaslt.cpp); deeper or smaller ones stay on the
+    hand-written kernels.  Results against the fp32 product of the same operands."""
+    A = _rand(K, M, seed=4) if transA else _rand(M, K, seed=4)
+    B = _rand(N, K, seed=5) if transB else _rand(K, N, seed=5)
+    Ad, Bd = A.to(DEV, torch.bfloat16), B.to(DEV, torch.bfloat16)
+    Af, Bf = Ad.float().cpu(), Bd.float().cpu()
+    ref = (Af.t() if transA else Af) @ (Bf.t() if transB else Bf)
+    kw = dict(transA=bool(transA), transB=bool(transB), out_dtype=torch.float32)
+    if transB:
+        bias = _rand(N, seed=6)
+        kw['bias'] = bias.to(DEV)
+        ref = ref + bias
+    n0 = hip.lib().dll.srnn_blaslt_calls()
+    out = hip.gemm(Ad, Bd, **kw)
+    torch.cuda.synchronize()
+    assert hip.lib().dll.srnn_blaslt_calls() - n0 == (1 if lib else 0)
+    torch.testing.assert_close(out.cpu(), ref, atol=2e-3 * np.sqrt(K), rtol=1e-2)
+
+
+def test_gemm_route_k64_and_skinny512(hip, monkeypatch):
+    """Round-6 routing: the 64-deep input projection over many rows on gemm3 (8192 x 1024 x 64,
+    bias, fp32 out) and the 512-row dh_0 product on the skinny kernel (A rows strided, Cin);
+    both against the fp32 product of the same operands and against the previous routes."""
+    A = _rand(8192, 64, seed=7).to(DEV, torch.bfloat16)
+    W = _rand(1024, 64, seed=8).to(DEV, torch.bfloat16)
+    b = _rand(1024, seed=9).to(DEV)
+    ref = A.float().cpu() @ W.float().cpu().t() + b.cpu()
+    out = hip.linear(A, W, bias=b)
+    monkeypatch.setenv('SRNN_SMALLK_G3', '0')
+    old = hip.gemm(A, W, transB=True, bias=b, tile=6)            # the thin small-K kernel
+    monkeypatch.delenv('SRNN_SMALLK_G3')
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.cpu(), ref, atol=1e-3, rtol=1e-3)
+    torch.testing.assert_close(out.cpu(), old.cpu(), atol=1e-4, rtol=1e-4)
+    Fr, D = 4, 1024
+    G = _rand(512, Fr, 3 * D, seed=10).to(DEV, torch.bfloat16)
+    Wt = _rand(D, 3 * D, seed=11).to(DEV, torch.bfloat16)
+    cin = _rand(512, D, seed=12).to(DEV)
+    ref = G[:, 0].float().cpu() @ Wt.float().cpu().t() + cin.cpu()
+    out = hip.gemm(G[:, 0], Wt, transB=True, M=512, N=D, K=3 * D, lda=Fr * 3 * D, ldb=3 * D,
+                   cin=cin, beta=1.0)
+    prev = hip.gemm(G[:, 0], Wt, transB=True, M=512, N=D, K=3 * D, lda=Fr * 3 * D, ldb=3 * D,
+                    cin=cin, beta=1.0, tile=0)                   # the 128-tile kernel
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.cpu(), ref, atol=2e-3 * np.sqrt(3 * D), rtol=1e-2)
+    torch.testing.assert_close(out.cpu(), prev.cpu(), atol=2e-3 * np.sqrt(3 * D), rtol=1e-2)
+
+
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('transA', [0, 1])
 @pytest.mark.parametrize('M,N,K', [(1024, 16, 8192), (1024, 43, 2048), (1000, 6, 128),
