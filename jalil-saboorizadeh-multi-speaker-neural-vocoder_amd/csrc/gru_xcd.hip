@@ -97,17 +97,52 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     // ---- resident W_hh fragments: unit j of this wave = k-range [(wave + NW j) * 32, +32)
     bf16x8 wf[UPW][NT];
     {
+        // The workgroup's 3 x 32 W_hh rows are staged through the front of the dynamic LDS one
+        // gate at a time (32 x D bf16, whole-row 16-B loads; the reduction buffers there are
+        // first used after this block), and each lane reads its 16-B fragments from there:
+        // read from global memory, every fragment load touched 16 rows' lines (round 6, the
+        // reverse sweep's form of this cut its launch intercept by ~18 us).  Row pitch
+        // 2 D + 16 B.
+        const int PW = 2 * D + 16;
+        const int PPR = D / 8;                                  // 16-B pieces per row
+        char* stg = smem;
         uint4 lw[UPW][NT];
 #pragma unroll
-        for (int j = 0; j < UPW; ++j) {
-            const int u = wave + NW * j;
-            const int ke = min(u * UK + (lane >> 4) * 8, D - 8);
+        for (int gate = 0; gate < 3; ++gate) {
+            if (gate) __syncthreads();                          // the previous gate's reads
+            const bf16* src = a.whh + (int64_t)(gate * D + u0) * D;
+            if constexpr (DC != 0) {
+                constexpr int NPT = 32 * (DC / 8) / NTHR;
+                uint4 v[NPT];
 #pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                const int row = (t >> 1) * D + u0 + (t & 1) * 16 + (lane & 15);
-                lw[j][t] = *reinterpret_cast<const uint4*>(a.whh + (int64_t)row * D + ke);
+                for (int i = 0; i < NPT; ++i) {
+                    const int e = tid + i * NTHR, rr = e / PPR, c = e - rr * PPR;
+                    v[i] = *reinterpret_cast<const uint4*>(src + (int64_t)rr * D + c * 8);
+                }
+#pragma unroll
+                for (int i = 0; i < NPT; ++i) {
+                    const int e = tid + i * NTHR, rr = e / PPR, c = e - rr * PPR;
+                    *reinterpret_cast<uint4*>(stg + rr * PW + c * 16) = v[i];
+                }
+            } else {
+                for (int e = tid; e < 32 * PPR; e += NTHR) {
+                    const int rr = e / PPR, c = e - rr * PPR;
+                    *reinterpret_cast<uint4*>(stg + rr * PW + c * 16) =
+                        *reinterpret_cast<const uint4*>(src + (int64_t)rr * D + c * 8);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < UPW; ++j) {
+                const int u = wave + NW * j;
+                const int ke = min(u * UK + (lane >> 4) * 8, D - 8);
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    lw[j][2 * gate + h] = *reinterpret_cast<const uint4*>(
+                        stg + (h * 16 + (lane & 15)) * PW + ke * 2);
             }
         }
+        __syncthreads();                                        // staging area free again
 #pragma unroll
         for (int j = 0; j < UPW; ++j) {
             const bool kv = wave + NW * j < NU;
@@ -578,26 +613,53 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
     const int u0 = p * CU;
     bf16x8 wf[UPW][NTB];
     {
-        // lane's k' = [32 u + 8 (lane >> 4), +8): input units iu, iu + 1, slots 0..3 each
-        unsigned lw[UPW][NTB][3];
+        // lane's k' = [32 u + 8 (lane >> 4), +8): input units iu, iu + 1, slots 0..3 each.
+        // The workgroup's 32 W_hh^T rows are staged through LDS one gate at a time (32 x D
+        // bf16, whole-row 16-B loads), and each lane picks its 4-B pairs from there: read
+        // straight from global memory, those 96 4-B loads per lane touched 16 rows' lines per
+        // instruction and cost ~20 us per launch (round 6, tools/gru_fixed_probe.py: reverse
+        // sweep intercept 22.7 -> 4.4 us at B = 64 without them).  Row pitch 2 D + 16 B: the
+        // 16 rows x 4 lane groups of a b32 read hit 64 distinct banks.  The staging area is the
+        // front of the dynamic LDS, free until the reduction buffers are first used below.
+        constexpr int PW = 2 * D + 16;
+        constexpr int PPR = D / 8;                              // 16-B pieces per row
+        constexpr int NPT = 32 * PPR / NTHR;                    // pieces per thread per gate
+        static_assert((32 * PPR) % NTHR == 0, "gru_xcd_bwd_pk: staging split");
+        char* stg = smem;
+        // one array per gate (constant indices only: a [3] dimension indexed by the gate loop
+        // was placed in scratch)
+        unsigned lr[UPW][NTB], lz[UPW][NTB], ln[UPW][NTB];
+        auto stage = [&](int gt, unsigned (&lw)[UPW][NTB]) __attribute__((always_inline)) {
+            if (gt) __syncthreads();                            // the previous gate's reads
+            // (unrolled load / store pairs: global and LDS do not alias, so the loads issue
+            //  back to back; an array of the NPT pieces was left in scratch at 243 VGPRs)
 #pragma unroll
-        for (int j = 0; j < UPW; ++j) {
-            const int u = wave + NW * j;
-            const int iu = u * 8 + (lane >> 4) * 2;
-#pragma unroll
-            for (int t = 0; t < NTB; ++t) {
-                const bf16* row = a.whh_t + (int64_t)(u0 + t * 16 + (lane & 15)) * 3 * D;
-#pragma unroll
-                for (int gt = 0; gt < 3; ++gt)
-                    lw[j][t][gt] = *reinterpret_cast<const unsigned*>(row + gt * D + iu);
+            for (int i = 0; i < NPT; ++i) {
+                const int e = tid + i * NTHR, rr = e / PPR, c = e - rr * PPR;
+                *reinterpret_cast<uint4*>(stg + rr * PW + c * 16) =
+                    *reinterpret_cast<const uint4*>(a.whh_t + (int64_t)(u0 + rr) * 3 * D +
+                                                    gt * D + c * 8);
             }
-        }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < UPW; ++j) {
+                const int iu = (wave + NW * j) * 8 + (lane >> 4) * 2;
+#pragma unroll
+                for (int t = 0; t < NTB; ++t)
+                    lw[j][t] = *reinterpret_cast<const unsigned*>(
+                        stg + (t * 16 + (lane & 15)) * PW + iu * 2);
+            }
+        };
+        stage(0, lr);
+        stage(1, lz);
+        stage(2, ln);
+        __syncthreads();                                        // staging area free again
 #pragma unroll
         for (int j = 0; j < UPW; ++j)
 #pragma unroll
             for (int t = 0; t < NTB; ++t) {
                 // [r0 z0 n0 0 | r1 z1 n1 0] (low / high halves of each gate word)
-                const unsigned r2 = lw[j][t][0], z2 = lw[j][t][1], n2 = lw[j][t][2];
+                const unsigned r2 = lr[j][t], z2 = lz[j][t], n2 = ln[j][t];
                 const uint4 v = make_uint4((r2 & 0xffffu) | (z2 << 16), n2 & 0xffffu,
                                            (r2 >> 16) | (z2 & 0xffff0000u), n2 >> 16);
                 __builtin_memcpy(&wf[j][t], &v, 16);
@@ -991,9 +1053,12 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
     a.RV = L.rv;
     const int NU = 3 * D / gx::UK;
     const int KW = pk ? gx::NW : NU < gx::NW ? NU : gx::NW;
-    const size_t lds = (size_t)2 * KW * 2 * 4 * gx::PS * 4 + 64 +
-                       (L.mt > 1 ? (size_t)L.mt * 5 * gx::NTHR * 4 : 0);
+    size_t lds = (size_t)2 * KW * 2 * 4 * gx::PS * 4 + 64 +
+                 (L.mt > 1 ? (size_t)L.mt * 5 * gx::NTHR * 4 : 0);
     if (pk) {
+        // (the prologue stages 32 W_hh^T rows of one gate in the same dynamic LDS)
+        const size_t stage = (size_t)32 * (2 * D + 16);
+        if (lds < stage) lds = stage;
         typedef void (*PkK)(GruXBwdArgs);
         static const PkK kp[4][3] = {
             {gru_xcd_bwd_pk_kernel<4, 1>, gru_xcd_bwd_pk_kernel<4, 2>, gru_xcd_bwd_pk_kernel<4, 4>},
@@ -1004,6 +1069,13 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
              gru_xcd_bwd_pk_kernel<16, 4>}};
         const int mi = L.mt == 1 ? 0 : L.mt == 2 ? 1 : 2;
         const PkK k = kp[D / 256 - 1][mi];
+        static bool attr[4][3] = {};
+        if (!attr[D / 256 - 1][mi]) {
+            SRNN_CHECK_HIP(hipFuncSetAttribute((const void*)k,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               160 * 1024));
+            attr[D / 256 - 1][mi] = true;
+        }
         if (srnn_persist_check((const void*)k, gx::NTHR, lds, (int64_t)a.G * a.P, "gru_xcd_bwd"))
             return 1;
         hipLaunchKernelGGL(k, dim3(a.G * a.P), dim3(gx::NTHR), lds, s, a);

@@ -13,6 +13,7 @@ sys.path.insert(0, os.path.join(HERE, '..', 'jalil-saboorizadeh-multi-speaker-ne
 import bench  # noqa: E402
 
 dev = torch.device('cuda', 0)
+print('SRNN_GX_EXP=%s' % os.environ.get('SRNN_GX_EXP', '0'), flush=True)
 for B in (64, 512):
     pts = {}
     for Fr in (16, 64, 128):
