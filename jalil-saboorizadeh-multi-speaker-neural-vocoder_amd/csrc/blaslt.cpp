@@ -32,7 +32,9 @@ struct Plan {
     std::vector<hipblasLtMatmulHeuristicResult_t> cand;   // the heuristic's candidates, best first
 };
 
-typedef std::tuple<int, int, int, int, int, int64_t, int64_t, int64_t, int, int, int, int> Key;
+typedef std::tuple<int, int, int, int, int, int64_t, int64_t, int64_t, int, int, int, int, int,
+                   int64_t, int64_t, int64_t>
+    Key;
 
 // Routing thresholds (srnn_blaslt_set_min; SRNN_BLASLT_MIN_MN / SRNN_BLASLT_MIN_MFLOP) and
 // the per-shape algorithm choice (srnn_blaslt_set_tune; SRNN_BLASLT_TUNE): 0 takes the
@@ -67,7 +69,8 @@ hipblasLtHandle_t handle() {
 }
 
 bool make_plan(Plan& p, int out_dtype, int transA, int transB, int M, int N, int K, int64_t lda,
-               int64_t ldb, int64_t ldc, int epi, bool bias) {
+               int64_t ldb, int64_t ldc, int epi, bool bias, int batch, int64_t sA, int64_t sB,
+               int64_t sC) {
     hipblasLtHandle_t h = handle();
     if (!h) return false;
     const hipDataType tout = out_dtype == SRNN_F32 ? HIP_R_32F : HIP_R_16BF;
@@ -90,6 +93,19 @@ bool make_plan(Plan& p, int out_dtype, int transA, int transB, int M, int N, int
             HIPBLAS_STATUS_SUCCESS ||
         hipblasLtMatrixLayoutCreate(&p.lc, tout, N, M, ldc) != HIPBLAS_STATUS_SUCCESS)
         return false;
+    if (batch > 1) {
+        // lt A = our B (stride sB), lt B = our A (sA), C (sC); a stride of 0 repeats the operand
+        const int32_t bc = batch;
+        const int64_t st[3] = {sB, sA, sC};
+        hipblasLtMatrixLayout_t ls[3] = {p.la, p.lb, p.lc};
+        for (int i = 0; i < 3; ++i)
+            if (hipblasLtMatrixLayoutSetAttribute(ls[i], HIPBLASLT_MATRIX_LAYOUT_BATCH_COUNT, &bc,
+                                                  sizeof(bc)) != HIPBLAS_STATUS_SUCCESS ||
+                hipblasLtMatrixLayoutSetAttribute(ls[i],
+                                                  HIPBLASLT_MATRIX_LAYOUT_STRIDED_BATCH_OFFSET,
+                                                  &st[i], sizeof(st[i])) != HIPBLAS_STATUS_SUCCESS)
+                return false;
+    }
     hipblasLtMatmulPreference_t pref;
     if (hipblasLtMatmulPreferenceCreate(&pref) != HIPBLAS_STATUS_SUCCESS) return false;
     const uint64_t wsmax = kWorkspace;
@@ -138,8 +154,9 @@ extern "C" int srnn_blaslt_set_tune(int n) {
 int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
                     float alpha, const void* A, int64_t lda, const void* B, int64_t ldb, float beta,
                     void* C, int64_t ldc, const float* bias, int bias_mode, int relu,
-                    hipStream_t s) {
-    if (!srnn_blaslt_enabled() || dtype != SRNN_BF16 || beta != 0.f) return -1;
+                    hipStream_t s, int batch, int64_t sA, int64_t sB, int64_t sC) {
+    if (!srnn_blaslt_enabled() || dtype != SRNN_BF16 || beta != 0.f || batch < 1) return -1;
+    if (batch > 1 && (bias || sA % 8 || sB % 8 || sC % 8 || sC == 0)) return -1;
     if (bias && bias_mode != 1) return -1;
     if (M <= 0 || N <= 0 || K <= 0) return -1;
     // large enough to pay for the library's launch and wide enough that gemm3's split-K deep
@@ -150,8 +167,9 @@ int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int
     // a partial-sum pass (tools/gemm_route_probe.py, profiles/r06_gemm_route_b64.txt:
     // 3072 x 1024 x 1024 TN 28.3 -> 17.4 us, 1024 x 1024 x 4096 NN 34.2 -> 23.2 us); the deep
     // weight gradients (K = 8192 .. 524288) stay on gemm3, which is faster there
-    const bool big = (int64_t)M * N >= routing().min_mn && 2.0 * M * N * K >= routing().min_flop;
-    const bool wide = (int64_t)M * N >= (1ll << 20) && K >= 256 && K <= routing().wide_k;
+    const int64_t outs = (int64_t)M * N * batch;
+    const bool big = outs >= routing().min_mn && 2.0 * outs * K >= routing().min_flop;
+    const bool wide = outs >= (1ll << 20) && K >= 256 && K <= routing().wide_k;
     if (!big && !wide) return -1;
     // (SRNN_BLASLT_F32_MINK: fp32-output problems only from this K on.  In isolation gemm3 writes
     //  fp32 faster at K of a few thousand -- GRU input projection 32768 x 3072 x 1024: 220 vs
@@ -162,12 +180,13 @@ int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int
                          : (relu ? HIPBLASLT_EPILOGUE_RELU : HIPBLASLT_EPILOGUE_DEFAULT);
     static std::map<Key, Plan> plans;
     const Key key{out_dtype, transA, transB, M, N, lda, ldb, ldc, K, epi, bias ? 1 : 0,
-                  routing().tune};
+                  routing().tune, batch, sA, sB, sC};
     auto it = plans.find(key);
     bool fresh = false;
     if (it == plans.end()) {
         Plan p;
-        p.ok = make_plan(p, out_dtype, transA, transB, M, N, K, lda, ldb, ldc, epi, bias != nullptr);
+        p.ok = make_plan(p, out_dtype, transA, transB, M, N, K, lda, ldb, ldc, epi, bias != nullptr,
+                         batch, sA, sB, sC);
         it = plans.emplace(key, p).first;
         fresh = true;
     }
@@ -212,6 +231,10 @@ int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int
     const hipblasStatus_t st = hipblasLtMatmul(handle(), p.desc, &alpha, B, p.la, A, p.lb, &zero,
                                                C, p.lc, C, p.lc, &p.algo, ws, p.ws, s);
     if (st != HIPBLAS_STATUS_SUCCESS) {
+        if (batch > 1) {          // (a batched form the library declines: own kernels from now)
+            p.ok = false;
+            return -1;
+        }
         srnn_set_error("hipblasLtMatmul failed (%d) for %dx%dx%d", (int)st, M, N, K);
         return 2;
     }

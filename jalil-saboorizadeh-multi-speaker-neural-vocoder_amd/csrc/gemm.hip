@@ -544,11 +544,14 @@ static int gemm_core(int dtype, int out_dtype, int transA, int transB, int M, in
         SRNN_REQUIRE(tile != 4, "gemm: shape not eligible for the skinny path");
     }
     // large plain bf16 problems: hipBLASLt (blaslt.cpp) unless a fused epilogue or a pending
-    // max |C| / column-sum request needs gemm3
-    if (tile < 0 && batch == 1 && !mask && !srnn_gemm_amax_pending() && !srnn_gemm_csum_pending() &&
+    // max |C| / column-sum request needs gemm3; strided batches too (the folded
+    // embedding . conv table, 16 x (256 x 1024 x 256) with the embedding shared: 33 us on the
+    // 128-tile kernel per step at every batch size)
+    if (tile < 0 && !mask && !srnn_gemm_amax_pending() && !srnn_gemm_csum_pending() &&
         !srnn_gemm_lsm_pending()) {
         int rc = srnn_blaslt_try(dtype, out_dtype, transA, transB, M, N, K, alpha, A, lda, B, ldb,
-                                 beta, C, ldc, bias, bias_mode, relu, s);
+                                 beta, C, ldc, bias, bias_mode, relu, s, batch, strideA, strideB,
+                                 strideC);
         if (rc >= 0) return rc;
     }
     // large aligned bf16 problems: the 256x256 8-wave kernel (gemm3.hip); tile 5 forces it

@@ -64,10 +64,12 @@ int srnn_splitk_sum(const float* part, float* C, int64_t ldc, int M, int N, int 
 // blaslt.cpp: plain large bf16 GEMMs (alpha, optional per-column bias, optional ReLU, beta 0)
 // through hipBLASLt; 0 done, -1 not taken (run the library's own kernels), > 0 error
 int srnn_blaslt_enabled();
+// (batch > 1: strided batches, element strides sA / sB / sC; sA or sB may be 0 -- one
+//  operand shared by every batch)
 int srnn_blaslt_try(int dtype, int out_dtype, int transA, int transB, int M, int N, int K,
                     float alpha, const void* A, int64_t lda, const void* B, int64_t ldb, float beta,
                     void* C, int64_t ldc, const float* bias, int bias_mode, int relu,
-                    hipStream_t s);
+                    hipStream_t s, int batch = 1, int64_t sA = 0, int64_t sB = 0, int64_t sC = 0);
 // gemm3.hip: a max |C| request (srnn_gemm_amax_next) waits for the next bf16 gemm3 launch
 int srnn_gemm_amax_pending();
 // gemm3.hip: a column-sum request (srnn_gemm_csum_next) waits for the next bf16 gemm3 launch

@@ -1690,3 +1690,22 @@ def test_nll_bits_passes_nll_loss_arguments(hip, args, kwargs):
     dkw = {k: (v.to(DEV) if torch.is_tensor(v) else v) for k, v in kwargs.items()}
     got = snn.sequence_nll_loss_bits(lp.to(DEV), tgt.to(DEV), *args, **dkw)
     torch.testing.assert_close(got.cpu().double(), ref.double(), atol=2e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize('out_dtype', [torch.bfloat16, torch.float32])
+def test_gemm_batched_shared_operand_blaslt(hip, out_dtype):
+    """Strided-batch GEMM with one operand shared by every batch (stride 0) -- the folded
+    embedding . conv table build, Tab[k] = E . Wp[k]^T (model._build_tab) -- goes to hipBLASLt
+    (round 6) and equals the per-batch fp32 products of the same bf16 operands."""
+    Q, D, FS = 256, 1024, 16
+    E = _rand(Q, Q, seed=13).to(DEV, torch.bfloat16)
+    Wp = _rand(FS, D, Q, seed=14).to(DEV, torch.bfloat16)
+    out = torch.empty((FS, Q, D), device=DEV, dtype=out_dtype)
+    n0 = hip.lib().dll.srnn_blaslt_calls()
+    hip.gemm(E, Wp, transB=True, out=out, out_dtype=out_dtype, M=Q, N=D, K=Q, lda=Q, ldb=Q,
+             ldc=D, batch=FS, sA=0, sB=D * Q, sC=Q * D)
+    torch.cuda.synchronize()
+    assert hip.lib().dll.srnn_blaslt_calls() - n0 == 1
+    ref = torch.einsum('qj,kdj->kqd', E.float().cpu(), Wp.float().cpu())
+    tol = 2e-3 * np.sqrt(Q) if out_dtype == torch.float32 else 1e-2 * np.sqrt(Q)
+    torch.testing.assert_close(out.float().cpu(), ref, atol=tol, rtol=1e-2)
