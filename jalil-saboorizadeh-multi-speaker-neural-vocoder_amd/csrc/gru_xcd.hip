@@ -16,6 +16,8 @@
 //     -- and publishes its 16 x 32 slice of h_t the same way; h is double-buffered (a buffer
 //     is rewritten only after every member read the previous step from it);
 //   * gate math, outputs and saved gates are gru_seq's (fp32 state, bf16 MMA operands).
+#include <algorithm>
+
 #include "samplernn_hip_internal.hpp"
 #include "handoff.hpp"
 #include "gru_point.hpp"
@@ -203,16 +205,22 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
     // would wait for the loads at once)
     struct Gi { float r, z, n; };
     Gi ga, gb{0.f, 0.f, 0.f};
+    // The input projections are read once and the outputs / saved gates are not read again in
+    // this launch: non-temporal (nt) loads and stores, so they do not compete in the L2 with
+    // the hand-off lines every poll reads (the reverse sweep's operand loads: 11.8 -> 10.8 us
+    // per step at 512 rows).  SRNN_GX_EXP bit 512: plain loads, bit 2048: plain stores (A/B)
+    const bool ntl = !(a.exp & 512), nts = !(a.exp & 2048);
+    auto ld = [ntl](const float* p) { return ntl ? __builtin_nontemporal_load(p) : *p; };
     {
         const float* gp0 = a.gi + (int64_t)min(row_of(0), B - 1) * a.ldgi;
-        ga = Gi{gp0[unit], gp0[D + unit], gp0[2 * D + unit]};
+        ga = Gi{ld(gp0 + unit), ld(gp0 + D + unit), ld(gp0 + 2 * D + unit)};
     }
     auto fetch_gi = [&](int t, int m, Gi& nx) {     // operands of the (step, tile) after (t, m)
         if (a.exp & 2) return;
         int tn = t, mn = m + 1;
         if (mn == MT) { mn = 0; tn = min(t + 1, a.Fr - 1); }
         const float* gp = a.gi + (int64_t)min(row_of(mn), B - 1) * a.ldgi + (int64_t)tn * a.sgi;
-        nx.r = gp[unit]; nx.z = gp[D + unit]; nx.n = gp[2 * D + unit];
+        nx.r = ld(gp + unit); nx.z = ld(gp + D + unit); nx.n = ld(gp + 2 * D + unit);
     };
     auto step = [&](int t, int m, const Gi& cu, Gi& nx) {
             floatx4 acc[NT];
@@ -308,11 +316,24 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_fwd_kernel(GruXArgs a) {
             const int row = row_of(m);
             if (rv && row < B && !(a.exp & 1)) {
                 const int64_t o = (int64_t)row * a.ldo + (int64_t)t * a.so + unit;
-                a.out[o] = hn;
-                a.out_lp[o] = __float2bfloat16(hn);
-                if (a.hp_lp && t + 1 < a.Fr) a.hp_lp[o + a.so] = __float2bfloat16(hn);
                 float* gt = a.gates + (int64_t)row * a.ldg + (int64_t)t * a.sg;
-                gt[unit] = rr; gt[D + unit] = zz; gt[2 * D + unit] = nn; gt[3 * D + unit] = ghn;
+                const unsigned short hb = __bfloat16_as_ushort(__float2bfloat16(hn));
+                unsigned short* olp = reinterpret_cast<unsigned short*>(a.out_lp);
+                unsigned short* hlp = reinterpret_cast<unsigned short*>(a.hp_lp);
+                if (nts) {
+                    __builtin_nontemporal_store(hn, a.out + o);
+                    __builtin_nontemporal_store(hb, olp + o);
+                    if (a.hp_lp && t + 1 < a.Fr) __builtin_nontemporal_store(hb, hlp + o + a.so);
+                    __builtin_nontemporal_store(rr, gt + unit);
+                    __builtin_nontemporal_store(zz, gt + D + unit);
+                    __builtin_nontemporal_store(nn, gt + 2 * D + unit);
+                    __builtin_nontemporal_store(ghn, gt + 3 * D + unit);
+                } else {
+                    a.out[o] = hn;
+                    olp[o] = hb;
+                    if (a.hp_lp && t + 1 < a.Fr) hlp[o + a.so] = hb;
+                    gt[unit] = rr; gt[D + unit] = zz; gt[2 * D + unit] = nn; gt[3 * D + unit] = ghn;
+                }
             }
             // (no barrier: the next (step, tile) writes the other red buffer, and this one is
             //  rewritten only after every wave passed the next (step, tile)'s barrier)
@@ -679,14 +700,31 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
     const __amdgpu_buffer_rsrc_t rx = hx_rsrc(a.xg);
     const size_t bufw = (size_t)a.G * MT * RG * D;              // granules per buffer
     const int lrow = lane & 15;
+    // The next (step, tile)'s operands -- dy, the saved gates, h_{t-1}: read once, ~1.5 MB per
+    // XCD and step at 512 rows -- as non-temporal (nt) buffer loads, so they stream past the
+    // L2 instead of competing there with the hand-off lines every poll reads: reverse sweep
+    // 11.8 -> 10.8 us per step at 512 rows (round 6, tools/gru_fixed_probe.py; no change at 64
+    // rows).  Issuing them earlier in the step (after the hand-off's MFMAs) measured no better
+    // at 512 rows and slower at 64.  SRNN_GX_EXP bit 512: plain loads (A/B).  32-bit byte
+    // offsets, resources in SGPRs.
+    const __amdgpu_buffer_rsrc_t rdy = hx_rsrc(a.dy), rgt = hx_rsrc(a.gates),
+                                 rho = hx_rsrc(a.hout), rh0 = hx_rsrc(a.h0);
+    const bool plain = (a.exp & 512) != 0;
+    auto ldf = [plain](__amdgpu_buffer_rsrc_t r, uint32_t off) {
+        return __uint_as_float(plain ? __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0)
+                                     : __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 2 /*nt*/));
+    };
+    // (the host sends launches with a byte offset past 2 GB -- very long sequences -- to the
+    //  unpacked kernel, whose operand loads use 64-bit pointers)
     auto fetch = [&](int t, int m, float& dyv, float& gr, float& gz, float& gn, float& gg,
                      float& hp) {
-        const int b = min(row_of(m), B - 1);
-        dyv = a.dy[(int64_t)b * a.lddy + (int64_t)t * a.sdy + unit];
-        const float* gp = a.gates + (int64_t)b * a.ldg + (int64_t)t * a.sg;
-        gr = gp[unit]; gz = gp[D + unit]; gn = gp[2 * D + unit]; gg = gp[3 * D + unit];
-        hp = t > 0 ? a.hout[(int64_t)b * a.ldo + (int64_t)(t - 1) * a.so + unit]
-                   : a.h0[(int64_t)b * D + unit];
+        const uint32_t b = (uint32_t)min(row_of(m), B - 1);
+        dyv = ldf(rdy, (uint32_t)(b * a.lddy + t * a.sdy + unit) * 4u);
+        const uint32_t go = (uint32_t)(b * a.ldg + t * a.sg + unit) * 4u;
+        gr = ldf(rgt, go); gz = ldf(rgt, go + 4u * D); gn = ldf(rgt, go + 8u * D);
+        gg = ldf(rgt, go + 12u * D);
+        hp = t > 0 ? ldf(rho, (uint32_t)(b * a.ldo + (t - 1) * a.so + unit) * 4u)
+                   : ldf(rh0, (uint32_t)(b * D + unit) * 4u);
     };
     float dyv, gr, gz, gn, gg, hp;
     float ddir1 = 0.f, sar1 = 0.f, saz1 = 0.f, sghn1 = 0.f, san1 = 0.f;
@@ -784,16 +822,34 @@ __global__ __launch_bounds__(gx::NTHR, 2) void gru_xcd_bwd_pk_kernel(GruXBwdArgs
                 float* dg = a.dgh + ob;
                 dg[unit] = cdar; dg[D + unit] = cdaz; dg[2 * D + unit] = cdghn;
             }
-            bf16* dl = a.dgh_lp + ob;
-            const bf16 har = __float2bfloat16(cdar), haz = __float2bfloat16(cdaz);
-            dl[unit] = har; dl[D + unit] = haz; dl[2 * D + unit] = __float2bfloat16(cdghn);
+            // (the bf16 GEMM operands are read by later launches only: nt stores, as the
+            //  operand loads; SRNN_GX_EXP bit 2048: plain stores)
+            unsigned short* dl = reinterpret_cast<unsigned short*>(a.dgh_lp + ob);
+            const unsigned short har = __bfloat16_as_ushort(__float2bfloat16(cdar)),
+                                 haz = __bfloat16_as_ushort(__float2bfloat16(cdaz)),
+                                 hgn = __bfloat16_as_ushort(__float2bfloat16(cdghn)),
+                                 han = __bfloat16_as_ushort(__float2bfloat16(cdan));
+            const bool nts = !(a.exp & 2048);
+            if (nts) {
+                __builtin_nontemporal_store(har, dl + unit);
+                __builtin_nontemporal_store(haz, dl + D + unit);
+                __builtin_nontemporal_store(hgn, dl + 2 * D + unit);
+            } else {
+                dl[unit] = har; dl[D + unit] = haz; dl[2 * D + unit] = hgn;
+            }
             if (a.dgi) {
                 float* di = a.dgi + ob;
                 di[unit] = cdar; di[D + unit] = cdaz; di[2 * D + unit] = cdan;
             }
             if (a.dgi_lp) {
-                bf16* dj = a.dgi_lp + ob;
-                dj[unit] = har; dj[D + unit] = haz; dj[2 * D + unit] = __float2bfloat16(cdan);
+                unsigned short* dj = reinterpret_cast<unsigned short*>(a.dgi_lp + ob);
+                if (nts) {
+                    __builtin_nontemporal_store(har, dj + unit);
+                    __builtin_nontemporal_store(haz, dj + D + unit);
+                    __builtin_nontemporal_store(han, dj + 2 * D + unit);
+                } else {
+                    dj[unit] = har; dj[D + unit] = haz; dj[2 * D + unit] = han;
+                }
             }
             if (MT == 1) {
                 sar1 += cdar; saz1 += cdaz; sghn1 += cdghn; san1 += cdan;
@@ -1026,8 +1082,14 @@ extern "C" int srnn_gru_xcd_bwd2(int dtype, int B, int D, int Fr, const float* d
     // packed hand-off form (gru_xcd_bwd_pk_kernel): one {3 x bf16, tag} granule per unit;
     // tags (<= Fr) must stay finite bf16 patterns (< 0x7f80); SRNN_GX_PK=0 restores the form
     // with {2 x bf16, 32-bit tag} granules
+    // (the packed kernel's operand fetch uses 32-bit buffer offsets: a launch with any byte
+    //  offset past 2 GB -- very long sequences -- takes the unpacked kernel's 64-bit pointers)
+    const int64_t omax = std::max({((int64_t)(B - 1) * lddy + (int64_t)(Fr - 1) * sdy + D) * 4,
+                                   ((int64_t)(B - 1) * ldg + (int64_t)(Fr - 1) * sg + 4 * D) * 4,
+                                   ((int64_t)(B - 1) * ldo + (int64_t)(Fr - 1) * so + D) * 4,
+                                   (int64_t)B * D * 4});
     const bool pk = D % 64 == 0 && D / 64 <= 16 && (D / 64) % 4 == 0 && Fr < 0x7f80 &&
-                    env_flag("SRNN_GX_PK", 1);
+                    omax < 0x7fffffffll - 64 && env_flag("SRNN_GX_PK", 1);
     const size_t clear = pk ? gx::HDR + (size_t)2 * L.G * L.mt * gx::RG * D * 8 : need;
     SRNN_CHECK_HIP(hipMemsetAsync(work, 0, clear, s));
     GruXBwdArgs a;
