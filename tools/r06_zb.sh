@@ -4,5 +4,5 @@
 set -e
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python3 bench.py > gpurun_out/r06z_bench.json 2> gpurun_out/r06z_bench.err
+timeout -k 10 400 python3 bench.py > gpurun_out/${TAG:-r06z}_bench.json 2> gpurun_out/${TAG:-r06z}_bench.err
 echo ok
