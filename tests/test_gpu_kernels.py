@@ -1709,3 +1709,31 @@ def test_gemm_batched_shared_operand_blaslt(hip, out_dtype):
     ref = torch.einsum('qj,kdj->kqd', E.float().cpu(), Wp.float().cpu())
     tol = 2e-3 * np.sqrt(Q) if out_dtype == torch.float32 else 1e-2 * np.sqrt(Q)
     torch.testing.assert_close(out.float().cpu(), ref, atol=tol, rtol=1e-2)
+
+
+@pytest.mark.parametrize('src_dt,dst_dt', [(torch.float32, torch.bfloat16),
+                                           (torch.float32, torch.float32),
+                                           (torch.bfloat16, torch.float32),
+                                           (torch.bfloat16, torch.bfloat16)])
+@pytest.mark.parametrize('rows,cols', [(1, 1), (1, 7), (3, 5), (131072, 43), (4097, 1024)])
+def test_cast_dense_and_strided(hip, src_dt, dst_dt, rows, cols):
+    """srnn_copy2d: the dense four-per-lane path (with its scalar tail) and the strided
+    element path both give torch's round-to-nearest-even conversion bit for bit."""
+    x = (_rand(rows, cols, seed=rows + cols) * 3.0).to(DEV, src_dt)
+    x[0, 0] = float('nan') if src_dt == torch.float32 else x[0, 0]
+    got = torch.empty((rows, cols), device=DEV, dtype=dst_dt)
+    hip.lib().call('srnn_copy2d', hip.dcode(x), hip.dcode(got), rows, cols, hip.ptr(x), cols,
+                   hip.ptr(got), cols, hip.stream())
+    want = x.to(dst_dt)
+    assert got.shape == want.shape
+    assert torch.equal(got.view(-1).float().nan_to_num(7.0), want.view(-1).float().nan_to_num(7.0))
+    # strided source and destination (a column window of wider rows): the element path
+    if cols > 1:
+        src = torch.zeros((rows, cols + 3), device=DEV, dtype=src_dt)
+        src[:, 1:cols + 1] = x
+        dst = torch.full((rows, cols + 5), -1.0, device=DEV, dtype=dst_dt)
+        hip.lib().call('srnn_copy2d', hip.dcode(src), hip.dcode(dst), rows, cols - 1,
+                       hip.ptr(src[:, 1:]), cols + 3, hip.ptr(dst[:, 2:]), cols + 5, hip.stream())
+        assert torch.equal(dst[:, 2:cols + 1].float().nan_to_num(7.0),
+                           x[:, :cols - 1].to(dst_dt).float().nan_to_num(7.0))
+        assert bool((dst[:, :2] == -1).all()) and bool((dst[:, cols + 1:] == -1).all())
